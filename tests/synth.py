@@ -1,0 +1,111 @@
+"""Field-structured synthetic libfm data, numpy version.
+
+The same generator is implemented on the device by the product library
+(`vbfm_synth_*` in csrc/vbfm_synth.hip) so that bench-scale data (10^8 rows) can be
+generated in HBM; the definition below is the specification both follow:
+
+  h(stream, i)   = splitmix64(seed * K1 + stream * K2 + i)           (uint64, wrapping)
+  feature(r, f)  = f * S + h(1, r * F + f) % S                       (one id per field)
+  x(r, f)        = 1.0f                              if xmode == 0
+                 = 0.5f + (h(2, r * F + f) >> 40) * 2^-24 (fp32)     if xmode == 1
+  b(j)           = ((h(3, j) >> 11) * 2^-53 - 0.5)                  (planted per-id bias)
+  y(r)           = clamp(rint(3 + sum_f b(feature(r, f)) + 1.5 * ((h(4, r) >> 11) * 2^-53 - 0.5)), 1, 5)
+
+Rows list their features in field order, i.e. in ascending feature id.
+"""
+import numpy as np
+
+K1 = np.uint64(0x9E3779B97F4A7C15)
+K2 = np.uint64(0xD1B54A32D192ED03)
+_M1 = np.uint64(0xBF58476D1CE4E5B9)
+_M2 = np.uint64(0x94D049BB133111EB)
+
+
+def splitmix64(z):
+    z = np.asarray(z, dtype=np.uint64)
+    with np.errstate(over="ignore"):
+        z = z + K1
+        z = (z ^ (z >> np.uint64(30))) * _M1
+        z = (z ^ (z >> np.uint64(27))) * _M2
+        return z ^ (z >> np.uint64(31))
+
+
+def h(seed, stream, i):
+    with np.errstate(over="ignore"):
+        base = np.uint64(seed) * K1 + np.uint64(stream) * K2
+        return splitmix64(base + np.asarray(i, dtype=np.uint64))
+
+
+def generate(n_rows, n_fields, ids_per_field, seed, xmode=0):
+    """Return (row_ptr uint64[N+1], feat uint32[N*F], val float32[N*F], y float32[N])."""
+    N, F, S = int(n_rows), int(n_fields), int(ids_per_field)
+    idx = np.arange(N * F, dtype=np.uint64)
+    fld = (idx % np.uint64(F)).astype(np.uint64)
+    feat = (fld * np.uint64(S) + h(seed, 1, idx) % np.uint64(S)).astype(np.uint32)
+    if xmode:
+        val = (np.float32(0.5) + (h(seed, 2, idx) >> np.uint64(40)).astype(np.float32)
+               * np.float32(2.0 ** -24)).astype(np.float32)
+    else:
+        val = np.ones(N * F, dtype=np.float32)
+    D = F * S
+    b = (h(seed, 3, np.arange(D, dtype=np.uint64)) >> np.uint64(11)).astype(np.float64) * 2.0 ** -53 - 0.5
+    s = np.zeros(N, dtype=np.float64)
+    fe = feat.reshape(N, F)
+    for f in range(F):            # summed in field order (the device generator does the same)
+        s = s + b[fe[:, f]]
+    noise = (h(seed, 4, np.arange(N, dtype=np.uint64)) >> np.uint64(11)).astype(np.float64) * 2.0 ** -53 - 0.5
+    y = np.clip(np.rint(3.0 + s + 1.5 * noise), 1.0, 5.0).astype(np.float32)
+    row_ptr = np.arange(N + 1, dtype=np.uint64) * np.uint64(F)
+    return row_ptr, feat, val, y
+
+
+def write_libfm(path, row_ptr, feat, val, y):
+    """libfm text: '<y> <id>:<x> ...' with x printed to round-trip fp32 exactly."""
+    with open(path, "w") as fh:
+        for r in range(len(y)):
+            b, e = int(row_ptr[r]), int(row_ptr[r + 1])
+            parts = ["%.9g" % float(y[r])]
+            parts += ["%d:%.9g" % (int(feat[j]), float(val[j])) for j in range(b, e)]
+            fh.write(" ".join(parts) + "\n")
+
+
+def csr_to_csc(n_rows, n_feature, row_ptr, feat, val):
+    """Data::create_data_t order (ascending rows per column, file order within a row)."""
+    nnz = len(feat)
+    rows = np.repeat(np.arange(n_rows, dtype=np.uint32), np.diff(row_ptr.astype(np.int64)))
+    order = np.argsort(feat, kind="stable")
+    col_ptr = np.zeros(n_feature + 1, dtype=np.uint64)
+    np.cumsum(np.bincount(feat, minlength=n_feature)[:n_feature], out=col_ptr[1:])
+    assert int(col_ptr[-1]) == nnz
+    return col_ptr, rows[order], val[order]
+
+
+def write_binary(base, n_feature, row_ptr, feat, val, y):
+    """Reference binary format (src/util/fmatrix.h:46-52,66-82; matrix.h:296-312):
+    base.x (rows), base.xt (transposed), base.y (targets)."""
+    N = len(y)
+    nnz = len(feat)
+
+    def write_sparse(path, nrows, ncols, ptr, ids, vals):
+        with open(path, "wb") as fh:
+            hdr = np.zeros(1, dtype=[("id", "<u4"), ("fs", "<u4"), ("nv", "<u8"),
+                                     ("nr", "<u4"), ("nc", "<u4")])
+            hdr["id"], hdr["fs"], hdr["nv"], hdr["nr"], hdr["nc"] = 2, 4, nnz, nrows, ncols
+            fh.write(hdr.tobytes())
+            ptr64 = ptr.astype(np.int64)
+            sizes = np.diff(ptr64).astype(np.uint32)
+            words = np.empty(nrows + 2 * len(ids), dtype="<u4")
+            row_off = np.arange(nrows, dtype=np.int64) + 2 * ptr64[:-1]
+            words[row_off] = sizes
+            ent_row = np.repeat(np.arange(nrows, dtype=np.int64), sizes.astype(np.int64))
+            ent_off = ent_row + 1 + 2 * np.arange(len(ids), dtype=np.int64)
+            words[ent_off] = ids
+            words[ent_off + 1] = np.asarray(vals, dtype="<f4").view("<u4")
+            fh.write(words.tobytes())
+
+    write_sparse(base + ".x", N, n_feature, row_ptr, feat, val)
+    col_ptr, crow, cval = csr_to_csc(N, n_feature, row_ptr, feat, val)
+    write_sparse(base + ".xt", n_feature, N, col_ptr, crow, cval)
+    with open(base + ".y", "wb") as fh:
+        fh.write(np.array([1, 4, N], dtype="<u4").tobytes())
+        fh.write(y.astype("<f4").tobytes())

@@ -1,0 +1,172 @@
+"""Pin the oracle (C restatement, oracle/vbfm_oracle.c) against the compiled reference.
+
+The fixtures in tests/golden/ were produced by oracle/_ref/ref_driver, i.e. by the
+reference's own fm_learn_vb / fm_learn_mcmc code (tests/golden/make_golden.py). The oracle
+must reproduce them BIT FOR BIT: same expressions, same loop order, plain IEEE doubles.
+"""
+import ctypes
+import json
+import os
+
+import numpy as np
+import pytest
+
+import oracle_ctypes as oc
+from conftest import GOLDEN, load_case
+
+
+def test_glibc_rand_restatement_matches_fixture_and_libc():
+    kat = json.load(open(os.path.join(GOLDEN, "rng", "glibc_rand.json")))
+    libc = ctypes.CDLL(None)
+    for seed, expect in kat.items():
+        oc.lib().or_srand(int(seed))
+        got = [oc.lib().or_rand() for _ in range(len(expect))]
+        assert got == expect, seed
+        libc.srand(ctypes.c_uint(int(seed)))
+        assert [libc.rand() for _ in range(len(expect))] == expect, seed
+
+
+def _tiny(case):
+    d = os.path.join(GOLDEN, case)
+    return oc.Data(os.path.join(d, "train.libfm")), oc.Data(os.path.join(d, "test.libfm"))
+
+
+@pytest.mark.parametrize("case", ["tiny", "tiny_dup"])
+def test_loader_counts(case):
+    tr, te = _tiny(case)
+    t, _ = load_case(case + "/steps")
+    n = t["nums"]
+    assert tr.num_rows == n["train_rows"] and te.num_rows == n["test_rows"]
+    assert tr.num_feature == n["train_nf"] and te.num_feature == n["test_nf"]
+    assert oc.num_all_attribute(tr, te) == n["D"]
+
+
+@pytest.mark.parametrize("case", ["tiny", "tiny_dup"])
+def test_vb_steps_bit_exact(case):
+    """update_all step by step (fm_learn_vb.h:383-440): every cache and parameter equal."""
+    t, a = load_case(case + "/steps")
+    m = t["meta"]
+    tr, te = _tiny(case)
+    k0, k1, k = [int(x) for x in m["dim"].split(",")]
+    vb = oc.VB(k0, k1, k, oc.num_all_attribute(tr, te))
+    vb.init_params(m["seed"], m["init_stdev"])
+    s = vb.s
+    np.testing.assert_array_equal(oc.arr(s.fm_v, s.k * s.D), a["init_fm_v"])
+    np.testing.assert_array_equal(oc.arr(s.fm_w, s.D), a["init_fm_w"])
+    np.testing.assert_array_equal(vb.params()["mu_w"], a["s0_mu_w"])
+    np.testing.assert_array_equal(vb.params()["mu_v"], a["s0_mu_v"])
+    vb.attach(tr, te)
+    vb.init_caches()
+
+    def check_rows(tag):
+        r = vb.rows()
+        for key in ("e", "t"):
+            np.testing.assert_array_equal(r[key], a[tag + "_" + key], err_msg=tag + key)
+
+    check_rows("s0_init")
+    np.testing.assert_array_equal(oc.arr(s.e_test, s.n_test), a["s0_init_test_e"])
+    vb.step("update_w0")
+    check_rows("s1_w0")
+    np.testing.assert_array_equal(vb.params()["scalars"], a["s1_scalars"][:4])
+    vb.step("update_w_all")
+    check_rows("s2_w")
+    np.testing.assert_array_equal(vb.params()["mu_w"], a["s2_mu_w"])
+    np.testing.assert_array_equal(vb.params()["sigma_w"], a["s2_sigma_w"])
+    for f in range(k):
+        vb.step("add_main_q", f)
+        r = vb.rows()
+        for key in ("q", "tq", "tz"):
+            np.testing.assert_array_equal(r[key], a["s3_f%d_q_%s" % (f, key)])
+        vb.step("update_v_all", f)
+        r = vb.rows()
+        for key in ("e", "t", "q", "tq", "tz"):
+            np.testing.assert_array_equal(r[key], a["s4_f%d_v_%s" % (f, key)])
+        p = vb.params()
+        np.testing.assert_array_equal(p["mu_v"], a["s4_f%d_v_mu_v" % f])
+        np.testing.assert_array_equal(p["sigma_v"], a["s4_f%d_v_sigma_v" % f])
+
+
+def _run_vb_trace(case, tr, te, attr_group=None):
+    t, a = load_case(case)
+    m = t["meta"]
+    k0, k1, k = [int(x) for x in m["dim"].split(",")]
+    vb = oc.VB(k0, k1, k, oc.num_all_attribute(tr, te), attr_group)
+    vb.init_params(m["seed"], m["init_stdev"])
+    vb.attach(tr, te)
+    vb.init_caches()
+    got = []
+    for it in range(m["iter"]):
+        rmse, mae, trq = vb.iterate()
+        got.append((rmse, mae, trq, vb.s.alpha, vb.s.last_free_energy, vb.s.mu_0_dash, vb.params()))
+    return t, a, got
+
+
+def _check_trace(t, a, got, exact=True):
+    for it, (rmse, mae, trq, alpha, fe, mu0, p) in enumerate(got):
+        ref = t["trace"][it]
+        cmp = (lambda x, y: x == y) if exact else (lambda x, y: abs(x - y) <= 1e-12 * max(1.0, abs(y)))
+        assert cmp(rmse, ref["rmse"]), (it, rmse, ref["rmse"])
+        assert cmp(mae, ref["mae"]), (it, mae, ref["mae"])
+        assert cmp(trq, ref["train"]), (it, trq, ref["train"])
+        assert cmp(alpha, ref["alpha"]), (it, alpha, ref["alpha"])
+        assert cmp(mu0, ref["mu_0_dash"]), it
+        assert cmp(fe, ref["free_energy"]), (it, fe, ref["free_energy"])
+        key = "iter%d_mu_v" % it
+        if key in a:
+            np.testing.assert_array_equal(p["mu_v"], a[key])
+            np.testing.assert_array_equal(p["sigma_v"], a["iter%d_sigma_v" % it])
+            np.testing.assert_array_equal(p["mu_w"], a["iter%d_mu_w" % it])
+            np.testing.assert_array_equal(p["hyp_sigma_v"], a["iter%d_hyp_sigma_v" % it])
+
+
+@pytest.mark.parametrize("case", ["tiny", "tiny_dup"])
+def test_vb_trace_tiny_bit_exact(case):
+    tr, te = _tiny(case)
+    t, a, got = _run_vb_trace(case + "/vb", tr, te)
+    _check_trace(t, a, got)
+
+
+def test_vb_trace_meta_groups_bit_exact():
+    tr, te = _tiny("tiny")
+    groups = np.loadtxt(os.path.join(GOLDEN, "tiny", "groups.meta"), dtype=np.uint32)
+    t, a, got = _run_vb_trace("tiny/vb_meta", tr, te, groups)
+    _check_trace(t, a, got)
+
+
+def test_vb_trace_synth_bit_exact(synth_files):
+    tr, te = oc.Data(synth_files["train"]), oc.Data(synth_files["test"])
+    t, a, got = _run_vb_trace("synth", tr, te)
+    _check_trace(t, a, got)
+    p = got[-1][-1]
+    np.testing.assert_array_equal(p["mu_v"], a["final_mu_v"])
+    np.testing.assert_array_equal(p["sigma_w"], a["final_sigma_w"])
+
+
+def test_vb_trace_movielens_split_bit_exact(sa_split):
+    tr, te = oc.Data(sa_split["train"]), oc.Data(sa_split["test"])
+    t, a, got = _run_vb_trace("sa_k8", tr, te)
+    _check_trace(t, a, got)
+    np.testing.assert_array_equal(got[-1][-1]["mu_w"], a["final_mu_w"])
+
+
+@pytest.mark.parametrize("case", ["tiny/als", "tiny_dup/als", "synth_als"])
+def test_als_trace_bit_exact(case, synth_files):
+    t, a = load_case(case)
+    m = t["meta"]
+    if case.startswith("synth"):
+        tr, te = oc.Data(synth_files["train"]), oc.Data(synth_files["test"])
+    else:
+        tr, te = _tiny(case.split("/")[0])
+    k0, k1, k = [int(x) for x in m["dim"].split(",")]
+    als = oc.ALS(k0, k1, k, oc.num_all_attribute(tr, te))
+    als.init_params(m["seed"], m["init_stdev"])
+    als.attach(tr, te)
+    for it in range(m["iter"]):
+        rmse_all, rmse_this, train = als.iterate()
+        ref = t["trace"][it]
+        assert rmse_all == ref["rmse_all"], (it, rmse_all, ref["rmse_all"])
+        assert train == ref["train"], (it, train, ref["train"])
+    p = als.params()
+    np.testing.assert_array_equal(p["v"], a["final_fm_v"])
+    np.testing.assert_array_equal(p["w"], a["final_fm_w"])
+    assert p["w0"] == a["final_mcmc_scalars"][0]
