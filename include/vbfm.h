@@ -1,0 +1,182 @@
+/* include/vbfm.h -- C-ABI of libvbfm.so, the MI355X-native VB factorization-machine learner.
+ *
+ * Drop-in boundary for the reference's learner seam: the abstract `fm_learn`
+ * (src/libfm/src/fm_learn.h:38-265) as specialised by `fm_learn_vb` /
+ * `fm_learn_vb_simultaneous` (src/libfm/src/fm_learn_vb.h:25-793,
+ * src/libfm/src/fm_learn_vb_simultaneous.h:15-309) and selected by `-method vb` in
+ * src/libfm/libfm.cpp:306-311. The reference has no FFI; the entry points below are what
+ * a host (the libFM-compatible CLI in host/, or any C/ctypes caller) binds in place of
+ * `new fm_learn_vb_simultaneous()` + `init()` + `learn(train, test)`.
+ *
+ * Conventions
+ *  - plain C types only; every array is caller-owned host memory unless a name says
+ *    `_device`; the library copies what it needs and never keeps a caller pointer.
+ *  - every function returns 0 on success, nonzero on failure; the message is then in
+ *    vbfm_last_error(ctx) (or vbfm_last_error(NULL) for failures without a context).
+ *    The reference signals errors by throwing `const char*` / `std::string`, which main()
+ *    prints as "ERROR: <msg>" (src/libfm/libfm.cpp:521-525); a host maps a nonzero return
+ *    to exactly that.
+ *  - one host thread per context; calls are synchronous (they return after the device
+ *    work they enqueue has completed), like the reference's single-threaded learner.
+ *  - arithmetic is IEEE fp64 for all state, fp32 for design-matrix values and targets
+ *    (FM_FLOAT, src/fm_core/fm_data.h:25), uint32 row / feature ids.
+ */
+#ifndef VBFM_H_
+#define VBFM_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define VBFM_ABI_VERSION 1
+
+typedef struct vbfm_ctx vbfm_ctx;
+
+/* == sparse_entry<float> (src/util/fmatrix.h:36-39): 8 bytes, id then value. In a
+ * transposed (column) matrix `id` is the row index. */
+typedef struct {
+	uint32_t id;
+	float value;
+} vbfm_entry;
+
+/* A data set as the reference's learner sees it: the transposed copy `data_t` built by
+ * Data::create_data_t (src/libfm/src/Data.h:457-509) -- column j lists its rows in
+ * ascending order -- plus the targets (Data::target). */
+typedef struct {
+	uint32_t num_rows;        /* Data::num_cases */
+	uint32_t num_feature;     /* data_t->getNumRows(): max feature id + 1 */
+	uint64_t nnz;
+	const uint64_t *col_ptr;  /* [num_feature + 1] */
+	const vbfm_entry *col_ent;/* [nnz] */
+	const float *target;      /* [num_rows] */
+} vbfm_csc;
+
+/* Learner configuration: the fields main() sets on the model and learner before init()
+ * (src/libfm/libfm.cpp:215-274, 306-311, 331-334). */
+typedef struct {
+	int32_t k0;               /* -dim k0: use bias w0 */
+	int32_t k1;               /* -dim k1: use 1-way interactions w */
+	int32_t num_factor;       /* -dim k2 */
+	uint32_t num_attribute;   /* D = max(train.num_feature, test.num_feature) + 1 (libfm.cpp:215) */
+	uint32_t num_attr_groups; /* DataMetaInfo::num_attr_groups (1 without -meta) */
+	const uint32_t *attr_group; /* [num_attribute] group of each attribute, or NULL = all 0 */
+	float min_target;         /* train.min_target (libfm.cpp:333) */
+	float max_target;         /* train.max_target (libfm.cpp:332) */
+	int32_t device;           /* HIP device ordinal */
+	int32_t task;             /* 0 = regression (the only task the VB learner evaluates) */
+} vbfm_config;
+
+/* Variational and hyper parameters (fm_learn_vb.h:36-46). Arrays are caller-allocated. */
+typedef struct {
+	double *mu_w, *sigma_w;         /* [D]   mu_w_dash, sigma_w_dash            */
+	double *mu_v, *sigma_v;         /* [k*D] mu_v_dash[f][j], sigma_v_dash[f][j] */
+	double *hyp_sigma_w;            /* [G]   sigma_w(g)                          */
+	double *hyp_sigma_v;            /* [G*k] sigma_v(g, f), row-major [g][f]     */
+	double alpha, sigma_0, mu_0_dash, sigma_0_dash;
+} vbfm_params;
+
+/* What one pass of the reference's iteration loop reports
+ * (fm_learn_vb_simultaneous.h:86-222, fm_learn_vb.h:646-681). */
+typedef struct {
+	double rmse, mae;           /* test, on predictions clipped to the train range */
+	double train_quirk;         /* the "Train=" value: sqrt(mean(clip(e)^2)) */
+	double free_energy;         /* F; valid only if free_energy_valid */
+	int32_t free_energy_valid;  /* 0 when update_all returned early on a NaN/inf alpha */
+	int32_t num_levels;         /* dependency levels of the train schedule */
+	double alpha, sigma_0, mu_0_dash, sigma_0_dash;
+	uint32_t nan_mu_w, nan_sigma_w, inf_mu_w;
+	uint32_t nan_mu_v, nan_sigma_v, inf_mu_v;
+	uint32_t nan_alpha, inf_alpha;
+	/* device time of the phases of this iteration (hipEvents on the context stream), ms */
+	double ms_w0, ms_w, ms_qcache, ms_v, ms_hyper, ms_test, ms_total;
+	/* with vbfm_set_profiling(ctx, 1): summed device time of the individual kernel launches
+	 * (an event pair around every launch), and the launch counts */
+	double ms_vlevel_kernels, ms_wlevel_kernels, ms_qcache_kernels;
+	int32_t n_vlevel_launches, n_wlevel_launches, n_qcache_launches;
+	uint64_t nnz_train;         /* nnz of this shard's train data */
+} vbfm_iter_stats;
+
+/* ---- lifecycle ---------------------------------------------------------------------- */
+int vbfm_create(vbfm_ctx **out, const vbfm_config *cfg);   /* fm_learn_vb::init (fm_learn_vb.h:685-743) */
+void vbfm_destroy(vbfm_ctx *ctx);
+const char *vbfm_last_error(const vbfm_ctx *ctx);
+int vbfm_abi_version(void);
+
+/* ---- data (DataSubset hand-over, fm_learn_vb::learn, fm_learn_vb.h:746-786) ----------- */
+int vbfm_set_train(vbfm_ctx *ctx, const vbfm_csc *train);
+int vbfm_set_test(vbfm_ctx *ctx, const vbfm_csc *test);
+/* Field-structured synthetic data generated directly in HBM (tests/synth.py defines it):
+ * rows x n_fields one-hot fields of ids_per_field ids each. which: 0 = train, 1 = test. */
+int vbfm_synth_generate(vbfm_ctx *ctx, int32_t which, uint32_t num_rows, uint32_t n_fields,
+                        uint32_t ids_per_field, uint64_t seed, int32_t xmode);
+/* Copy back the device copy of a data set (parity of the device transpose / generator). */
+int vbfm_get_csc(vbfm_ctx *ctx, int32_t which, uint64_t *col_ptr /*[nf+1]*/, vbfm_entry *col_ent /*[nnz]*/,
+                 float *target /*[rows]*/);
+int vbfm_get_shape(vbfm_ctx *ctx, int32_t which, uint32_t *num_rows, uint32_t *num_feature, uint64_t *nnz);
+/* level of each train feature (1-based; [train.num_feature]) and the number of levels */
+int vbfm_get_levels(vbfm_ctx *ctx, uint32_t *level, uint32_t *num_levels);
+
+/* ---- parameters ----------------------------------------------------------------------- */
+int vbfm_set_params(vbfm_ctx *ctx, const vbfm_params *p);
+int vbfm_get_params(vbfm_ctx *ctx, vbfm_params *p);
+
+/* Bench-scale random init on the device: mu_w_dash, mu_v_dash = 0.1 * N(0,1) from a
+ * counter-based generator (splitmix64 + Box-Muller; NOT the reference's glibc stream),
+ * sigma_* = .02, hyper parameters and scalars at their fm_learn_vb::init values. */
+int vbfm_init_params_device(vbfm_ctx *ctx, uint64_t seed);
+
+/* ---- learning (fm_learn_vb_simultaneous::_learn, fm_learn_vb_simultaneous.h:18-259) ---- */
+int vbfm_init_caches(vbfm_ctx *ctx);                     /* :37-44 */
+int vbfm_iterate(vbfm_ctx *ctx, vbfm_iter_stats *out);   /* one pass of :75-258 */
+int vbfm_get_test_pred(vbfm_ctx *ctx, double *pred /*[test rows]*/); /* pred_this (clipped) */
+
+/* ---- the steps of update_all (fm_learn_vb.h:383-501), for step-level parity ---------- */
+int vbfm_step_w0(vbfm_ctx *ctx);                  /* update_w0, :504-525 */
+int vbfm_step_w(vbfm_ctx *ctx);                   /* the w sweep, :390-406 / :527-574 */
+int vbfm_step_qcache(vbfm_ctx *ctx, int32_t f);   /* zero + add_main_q, :411-418 / :354-381 */
+int vbfm_step_v(vbfm_ctx *ctx, int32_t f);        /* the v sweep of factor f, :420-438 / :577-644 */
+int vbfm_step_hyper(vbfm_ctx *ctx, int32_t *early_return); /* :446-498 */
+int vbfm_free_energy(vbfm_ctx *ctx, double *F);   /* :646-681 (value only, no file) */
+/* row caches: e (cache[].e), t/q/z of cache_t, q of cache (the factor q-cache) */
+int vbfm_get_rows(vbfm_ctx *ctx, double *e, double *t, double *q, double *tq, double *tz);
+int vbfm_get_test_e(vbfm_ctx *ctx, double *e /*[test rows]*/);
+
+/* per-launch event timing of the sweep kernels inside vbfm_iterate (off by default) */
+int vbfm_set_profiling(vbfm_ctx *ctx, int32_t on);
+
+/* ---- the factor sweep alone (the metric's timed unit: q-cache + v sweep, all factors) -- */
+int vbfm_factor_sweep(vbfm_ctx *ctx, double *ms_device);
+
+/* ---- multi-GPU: row-sharded exact mode over RCCL ----------------------------------------
+ * Each rank owns a slice of the train rows; per dependency level the per-feature
+ * sufficient statistics are all-reduced, so every rank computes identical posteriors. */
+int vbfm_comm_unique_id(uint8_t out[128]);
+int vbfm_comm_init(vbfm_ctx *ctx, int32_t nranks, int32_t rank, const uint8_t uid[128]);
+
+/* ---- host side of the reference's CLI path (loader, RNG init) -------------------------- */
+typedef struct {
+	uint32_t num_rows, num_feature;
+	uint64_t nnz;
+	float min_target, max_target;
+	float *target;                  /* [num_rows] */
+	uint64_t *row_ptr; vbfm_entry *row_ent;   /* CSR in file order   (Data.h:233-278) */
+	uint64_t *col_ptr; vbfm_entry *col_ent;   /* transposed copy     (Data.h:457-509) */
+} vbfm_host_data;
+/* Data::load (Data.h:106-283): libfm text, or the binary triple <name>.x/.xt/.y
+ * (fmatrix.h:46-52, matrix.h:296-312) when those files exist. */
+int vbfm_load_data(const char *filename, vbfm_host_data *out);
+void vbfm_free_host_data(vbfm_host_data *d);
+/* srand(seed) then the reference's draw order: fm.v (k*D) ~ N(0, init_stdev)
+ * (fm_model.h:97), fm.w (D) (libfm.cpp:307), mu_w_dash (D), mu_v_dash (k*D) as 0.1*N(0,1)
+ * (fm_learn_vb.h:709-711); sigma_* and hyper parameters at their init values.
+ * fm_v / fm_w may be NULL (they are drawn either way, to keep the stream aligned). */
+int vbfm_init_params_host(uint32_t seed, double init_stdev, int32_t num_factor, uint32_t num_attribute,
+                          uint32_t num_attr_groups, vbfm_params *out, double *fm_v, double *fm_w);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* VBFM_H_ */

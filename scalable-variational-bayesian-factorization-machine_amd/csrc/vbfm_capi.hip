@@ -1,0 +1,1000 @@
+// vbfm_capi.hip -- the C-ABI of include/vbfm.h: a VB learner context on one MI355X.
+//
+// It replaces fm_learn_vb / fm_learn_vb_simultaneous (src/libfm/src/fm_learn_vb.h,
+// src/libfm/src/fm_learn_vb_simultaneous.h): the host keeps the reference's control flow
+// (one iteration = update_all, test prediction, metrics) and the scalar hyper-parameter
+// arithmetic; every O(nnz), O(N) and O(k*D) loop runs as a kernel of vbfm_kernels.hip on
+// the context's stream. Device-side partial sums come back in a fixed order and are added
+// on the host in that order, so results are deterministic run to run.
+#include "vbfm_device.h"
+#include "../../include/vbfm.h"
+
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+extern "C" const char *vbfm_host_last_error(void);
+extern "C" void vbfm_host_set_error(const char *msg);
+
+namespace {
+
+
+struct DevData {
+	uint32_t n = 0, nf = 0;        // rows; columns of the transposed copy (padded to the global nf)
+	uint32_t nf_local = 0;
+	uint64_t nnz = 0;
+	uint64_t *col_ptr = nullptr;   // [nf+1]
+	uint2 *csc = nullptr;          // [nnz]
+	uint64_t *row_ptr = nullptr;   // [n+1]
+	uint2 *csr = nullptr;          // [nnz] feature-sorted rows
+	float *target = nullptr;       // [n]
+	float min_target = 0, max_target = 0;
+};
+
+struct HipError {
+	hipError_t e;
+	const char *what;
+};
+
+#define HIPCHK(x)                                                   \
+	do {                                                            \
+		hipError_t _e = (x);                                        \
+		if (_e != hipSuccess) throw HipError{_e, #x};               \
+	} while (0)
+
+#define NCCLCHK(x)                                                  \
+	do {                                                            \
+		ncclResult_t _r = (x);                                      \
+		if (_r != ncclSuccess) throw std::string("RCCL: ") + ncclGetErrorString(_r) + " in " #x; \
+	} while (0)
+
+template <class T> T *dalloc(size_t n)
+{
+	void *p = nullptr;
+	HIPCHK(hipMalloc(&p, (n ? n : 1) * sizeof(T)));
+	return (T *)p;
+}
+
+template <class T> void dfree(T *&p)
+{
+	if (p) (void)hipFree((void *)p);
+	p = nullptr;
+}
+
+enum { EV_BEGIN, EV_W0, EV_W, EV_V, EV_HYPER, EV_TEST, EV_N };
+
+}  // namespace
+
+struct vbfm_ctx {
+	std::string err;
+	int dev = 0;
+	hipStream_t s = nullptr;
+	int k0 = 1, k1 = 1, k = 0;
+	uint32_t D = 0, G = 1;
+	std::vector<uint32_t> group_h, per_group;
+	uint32_t *group_d = nullptr;
+	float min_target = 0, max_target = 0;
+	DevData tr, te;
+	RowRec *rows = nullptr;
+	double *scratch_n = nullptr;   // yhat of train at init
+	double *e_test = nullptr, *pred_test = nullptr;
+	double2 *ms_v = nullptr, *ms_w = nullptr;
+	double *hyp_w_d = nullptr, *hyp_v_d = nullptr;
+	std::vector<double> hyp_w, hyp_v;
+	double alpha = 1.0, sigma_0 = 1.0, mu0 = 0.0, s0d = 0.02;
+	// schedule
+	std::vector<uint32_t> level_ptr, level_h;
+	uint32_t *level_feats = nullptr;
+	uint8_t *dup = nullptr;
+	bool sched_ready = false;
+	// reductions
+	static constexpr uint32_t RED_BLOCKS = 512;
+	double *red_d = nullptr;
+	std::vector<double> red_h;
+	uint32_t *perm_d = nullptr;
+	vbk::Chunk *chunks_d = nullptr;
+	std::vector<vbk::Chunk> chunks_h;
+	double *chunk_out_d = nullptr;
+	uint32_t *counters = nullptr;
+	// row-sharded multi-GPU
+	int nranks = 1, rank = 0;
+	ncclComm_t comm = nullptr;
+	double2 *stats = nullptr;
+	uint32_t stats_cap = 0;
+	uint64_t n_global = 0;
+	uint32_t test_n_global = 0;
+	hipEvent_t ev[EV_N] = {};
+	// per-launch profiling (vbfm_set_profiling)
+	bool profiling = false;
+	std::vector<hipEvent_t> pev;
+	size_t pev_used = 0;
+	struct Span { size_t a; int kind; };   // kind 0 = v level, 1 = w level, 2 = qcache
+	std::vector<Span> spans;
+};
+
+namespace {
+
+int fail(vbfm_ctx *c, const std::string &m)
+{
+	if (c) c->err = m; else vbfm_host_set_error(m.c_str());
+	return -1;
+}
+
+template <class F> int guarded(vbfm_ctx *c, F &&fn)
+{
+	try {
+		if (c) HIPCHK(hipSetDevice(c->dev));
+		fn();
+		return 0;
+	} catch (const HipError &e) {
+		return fail(c, std::string("HIP error ") + hipGetErrorString(e.e) + " in " + e.what);
+	} catch (const std::string &m) {
+		return fail(c, m);
+	} catch (const char *m) {
+		return fail(c, m);
+	} catch (const std::bad_alloc &) {
+		return fail(c, "host out of memory");
+	}
+}
+
+void sync(vbfm_ctx *c) { HIPCHK(hipStreamSynchronize(c->s)); }
+
+// all-reduce a few host doubles across the row shards (identity with one rank)
+void allreduce_host(vbfm_ctx *c, double *v, int n)
+{
+	if (c->nranks == 1) return;
+	HIPCHK(hipMemcpyAsync(c->red_d, v, n * sizeof(double), hipMemcpyHostToDevice, c->s));
+	NCCLCHK(ncclAllReduce(c->red_d, c->red_d, n, ncclDouble, ncclSum, c->comm, c->s));
+	HIPCHK(hipMemcpyAsync(v, c->red_d, n * sizeof(double), hipMemcpyDeviceToHost, c->s));
+	sync(c);
+}
+
+// block partials of a row reduction, summed on the host in block order
+double finish_sum(vbfm_ctx *c, uint32_t nblocks)
+{
+	HIPCHK(hipMemcpyAsync(c->red_h.data(), c->red_d, nblocks * sizeof(double), hipMemcpyDeviceToHost, c->s));
+	sync(c);
+	double s = 0.0;
+	for (uint32_t i = 0; i < nblocks; i++) s += c->red_h[i];
+	return s;
+}
+
+void free_data(DevData &d)
+{
+	dfree(d.col_ptr); dfree(d.csc); dfree(d.row_ptr); dfree(d.csr); dfree(d.target);
+	d = DevData();
+}
+
+// host CSC -> host CSR sorted by feature: the order the reference's column loops visit a row
+void csc_to_csr(const vbfm_csc *in, std::vector<uint64_t> &row_ptr, std::vector<uint2> &csr)
+{
+	row_ptr.assign((size_t)in->num_rows + 1, 0);
+	for (uint64_t p = 0; p < in->nnz; p++) row_ptr[(size_t)in->col_ent[p].id + 1]++;
+	for (uint32_t r = 0; r < in->num_rows; r++) row_ptr[r + 1] += row_ptr[r];
+	std::vector<uint64_t> pos(row_ptr.begin(), row_ptr.end() - 1);
+	csr.resize(in->nnz);
+	for (uint32_t j = 0; j < in->num_feature; j++)
+		for (uint64_t p = in->col_ptr[j]; p < in->col_ptr[j + 1]; p++) {
+			const vbfm_entry &e = in->col_ent[p];
+			uint2 v;
+			v.x = j;
+			memcpy(&v.y, &e.value, 4);
+			csr[pos[e.id]++] = v;
+		}
+}
+
+void check_csc(const vbfm_csc *in)
+{
+	if (!in) throw std::string("null data set");
+	if (in->nnz && (!in->col_ptr || !in->col_ent)) throw std::string("data set without entries");
+	if (in->num_rows && !in->target) throw std::string("data set without targets");
+	if (!in->col_ptr && in->num_feature) throw std::string("data set without col_ptr");
+	if (in->num_feature && in->col_ptr[in->num_feature] != in->nnz) throw std::string("col_ptr does not end at nnz");
+	for (uint32_t j = 0; j < in->num_feature; j++)
+		if (in->col_ptr[j + 1] < in->col_ptr[j]) throw std::string("col_ptr is not monotone");
+	for (uint64_t p = 0; p < in->nnz; p++)
+		if (in->col_ent[p].id >= in->num_rows) throw std::string("row index out of range in col_ent");
+}
+
+// pad col_ptr to nf_pad columns (trailing empty columns), upload data set
+void upload(vbfm_ctx *c, DevData &d, const vbfm_csc *in, uint32_t nf_pad)
+{
+	free_data(d);
+	d.n = in->num_rows;
+	d.nf_local = in->num_feature;
+	d.nf = std::max(nf_pad, in->num_feature);
+	d.nnz = in->nnz;
+	std::vector<uint64_t> cp((size_t)d.nf + 1, in->nnz);
+	if (in->num_feature) memcpy(cp.data(), in->col_ptr, ((size_t)in->num_feature + 1) * sizeof(uint64_t));
+	else cp[0] = 0;
+	std::vector<uint64_t> row_ptr;
+	std::vector<uint2> csr;
+	csc_to_csr(in, row_ptr, csr);
+	d.col_ptr = dalloc<uint64_t>(cp.size());
+	d.csc = dalloc<uint2>(d.nnz);
+	d.row_ptr = dalloc<uint64_t>(row_ptr.size());
+	d.csr = dalloc<uint2>(d.nnz);
+	d.target = dalloc<float>(d.n);
+	HIPCHK(hipMemcpyAsync(d.col_ptr, cp.data(), cp.size() * 8, hipMemcpyHostToDevice, c->s));
+	if (d.nnz) {
+		HIPCHK(hipMemcpyAsync(d.csc, in->col_ent, d.nnz * 8, hipMemcpyHostToDevice, c->s));
+		HIPCHK(hipMemcpyAsync(d.csr, csr.data(), d.nnz * 8, hipMemcpyHostToDevice, c->s));
+	}
+	HIPCHK(hipMemcpyAsync(d.row_ptr, row_ptr.data(), row_ptr.size() * 8, hipMemcpyHostToDevice, c->s));
+	if (d.n) HIPCHK(hipMemcpyAsync(d.target, in->target, d.n * 4, hipMemcpyHostToDevice, c->s));
+	float mn = 3.40282347e+38f, mx = -3.40282347e+38f;
+	for (uint32_t i = 0; i < d.n; i++) { mn = std::min(in->target[i], mn); mx = std::max(in->target[i], mx); }
+	d.min_target = mn; d.max_target = mx;
+	sync(c);
+}
+
+// Dependency levels of the train features (see vbfm_kernels.hip header). With several
+// row shards every round's levels are max-reduced over the shards, so all ranks share one
+// schedule: the one the un-sharded data set defines.
+void build_schedule(vbfm_ctx *c)
+{
+	DevData &d = c->tr;
+	const uint32_t nf = d.nf;
+	uint32_t *level = dalloc<uint32_t>(nf);
+	uint32_t *changed = dalloc<uint32_t>(1);
+	dfree(c->dup);
+	c->dup = dalloc<uint8_t>(nf);
+	HIPCHK(hipMemsetAsync(c->dup, 0, nf, c->s));
+	HIPCHK(vbk::level_init(level, nf, c->s));
+	HIPCHK(vbk::mark_dups(d.row_ptr, d.csr, d.n, c->dup, c->s));
+	if (c->nranks > 1 && nf) NCCLCHK(ncclAllReduce(c->dup, c->dup, nf, ncclUint8, ncclMax, c->comm, c->s));
+	for (int round = 0;; round++) {
+		uint32_t ch = 0;
+		HIPCHK(hipMemsetAsync(changed, 0, 4, c->s));
+		HIPCHK(vbk::level_relax(d.row_ptr, d.csr, d.n, nf, level, changed, c->s));
+		if (c->nranks > 1) {
+			if (nf) NCCLCHK(ncclAllReduce(level, level, nf, ncclUint32, ncclMax, c->comm, c->s));
+			NCCLCHK(ncclAllReduce(changed, changed, 1, ncclUint32, ncclMax, c->comm, c->s));
+		}
+		HIPCHK(hipMemcpyAsync(&ch, changed, 4, hipMemcpyDeviceToHost, c->s));
+		sync(c);
+		if (!ch) break;
+		if (round > (int)nf + 2) throw std::string("level schedule did not converge");
+	}
+	c->level_h.assign(nf, 0);
+	if (nf) HIPCHK(hipMemcpy(c->level_h.data(), level, nf * 4, hipMemcpyDeviceToHost));
+	dfree(level);
+	dfree(changed);
+	uint32_t L = 0;
+	for (uint32_t j = 0; j < nf; j++) L = std::max(L, c->level_h[j]);
+	c->level_ptr.assign((size_t)L + 1, 0);
+	for (uint32_t j = 0; j < nf; j++) c->level_ptr[c->level_h[j]]++;
+	for (uint32_t l = 0; l < L; l++) c->level_ptr[l + 1] += c->level_ptr[l];
+	std::vector<uint32_t> feats(nf), pos(c->level_ptr.begin(), c->level_ptr.end() - 1);
+	for (uint32_t j = 0; j < nf; j++) feats[pos[c->level_h[j] - 1]++] = j;   // ascending j per level
+	dfree(c->level_feats);
+	c->level_feats = dalloc<uint32_t>(nf);
+	if (nf) HIPCHK(hipMemcpy(c->level_feats, feats.data(), nf * 4, hipMemcpyHostToDevice));
+	uint32_t maxlev = 0;
+	for (uint32_t l = 0; l < L; l++) maxlev = std::max(maxlev, c->level_ptr[l + 1] - c->level_ptr[l]);
+	if (c->nranks > 1 && maxlev > c->stats_cap) {
+		dfree(c->stats);
+		c->stats = dalloc<double2>(maxlev);
+		c->stats_cap = maxlev;
+	}
+	c->sched_ready = true;
+}
+
+// segments of the hyper / free-energy sums: (w or factor f) x group, chunked by 64K attrs
+void build_chunks(vbfm_ctx *c)
+{
+	std::vector<uint32_t> perm(c->D), gptr((size_t)c->G + 1, 0);
+	for (uint32_t i = 0; i < c->D; i++) gptr[c->group_h[i] + 1]++;
+	for (uint32_t g = 0; g < c->G; g++) gptr[g + 1] += gptr[g];
+	std::vector<uint32_t> pos(gptr.begin(), gptr.end() - 1);
+	for (uint32_t i = 0; i < c->D; i++) perm[pos[c->group_h[i]]++] = i;
+	c->chunks_h.clear();
+	const uint32_t CH = 65536;
+	for (int f = -1; f < c->k; f++)
+		for (uint32_t g = 0; g < c->G; g++)
+			for (uint32_t b = gptr[g]; b < gptr[g + 1]; b += CH)
+				c->chunks_h.push_back(vbk::Chunk{b, std::min(b + CH, gptr[g + 1]), f, g});
+	c->perm_d = dalloc<uint32_t>(c->D);
+	if (c->D) HIPCHK(hipMemcpy(c->perm_d, perm.data(), c->D * 4, hipMemcpyHostToDevice));
+	c->chunks_d = dalloc<vbk::Chunk>(c->chunks_h.size());
+	if (!c->chunks_h.empty())
+		HIPCHK(hipMemcpy(c->chunks_d, c->chunks_h.data(), c->chunks_h.size() * sizeof(vbk::Chunk), hipMemcpyHostToDevice));
+	c->chunk_out_d = dalloc<double>(c->chunks_h.size());
+}
+
+// sum of chunk results per segment, in chunk order; seg index = (f+1)*G + g
+std::vector<double> param_sums(vbfm_ctx *c, int mode)
+{
+	const size_t nc = c->chunks_h.size();
+	HIPCHK(vbk::param_sums(c->ms_w, c->ms_v, c->perm_d, c->D, c->chunks_d, (uint32_t)nc, mode, c->hyp_w_d, c->hyp_v_d,
+	                       c->k, c->chunk_out_d, c->s));
+	std::vector<double> out(nc), seg((size_t)(c->k + 1) * c->G, 0.0);
+	if (nc) HIPCHK(hipMemcpyAsync(out.data(), c->chunk_out_d, nc * 8, hipMemcpyDeviceToHost, c->s));
+	sync(c);
+	for (size_t i = 0; i < nc; i++) seg[(size_t)(c->chunks_h[i].f + 1) * c->G + c->chunks_h[i].g] += out[i];
+	return seg;
+}
+
+void upload_hyp(vbfm_ctx *c)
+{
+	HIPCHK(hipMemcpyAsync(c->hyp_w_d, c->hyp_w.data(), c->G * 8, hipMemcpyHostToDevice, c->s));
+	if (c->k) HIPCHK(hipMemcpyAsync(c->hyp_v_d, c->hyp_v.data(), (size_t)c->G * c->k * 8, hipMemcpyHostToDevice, c->s));
+}
+
+void require_train(vbfm_ctx *c)
+{
+	if (!c->rows) throw std::string("no train data set (vbfm_set_train)");
+	if (!c->sched_ready) build_schedule(c);
+}
+
+LevelArgs level_args(vbfm_ctx *c, uint32_t l, bool is_w, int f)
+{
+	LevelArgs a;
+	a.col_ptr = c->tr.col_ptr;
+	a.csc = c->tr.csc;
+	a.feats = c->level_feats + c->level_ptr[l];
+	a.nfeat = c->level_ptr[l + 1] - c->level_ptr[l];
+	a.rows = c->rows;
+	a.ms = is_w ? c->ms_w : c->ms_v + (size_t)f * c->D;
+	a.hyp = is_w ? c->hyp_w_d : c->hyp_v_d + f;
+	a.hyp_stride = is_w ? 1 : (uint32_t)c->k;
+	a.attr_group = c->group_d;
+	a.dup = c->dup;
+	a.alpha = c->alpha;
+	a.counters = c->counters;
+	a.stats = c->stats;
+	return a;
+}
+
+// event pair around one launch when profiling (the pool grows on first use)
+size_t prof_begin(vbfm_ctx *c, int kind)
+{
+	if (!c->profiling) return 0;
+	if (c->pev_used + 2 > c->pev.size()) {
+		const size_t add = std::max<size_t>(256, c->pev.size());
+		for (size_t i = 0; i < add; i++) {
+			hipEvent_t e;
+			HIPCHK(hipEventCreate(&e));
+			c->pev.push_back(e);
+		}
+	}
+	const size_t a = c->pev_used;
+	c->pev_used += 2;
+	HIPCHK(hipEventRecord(c->pev[a], c->s));
+	c->spans.push_back(vbfm_ctx::Span{a, kind});
+	return a;
+}
+
+void prof_end(vbfm_ctx *c, size_t a)
+{
+	if (c->profiling) HIPCHK(hipEventRecord(c->pev[a + 1], c->s));
+}
+
+void sweep_level(vbfm_ctx *c, uint32_t l, bool is_w, int f)
+{
+	LevelArgs a = level_args(c, l, is_w, f);
+	if (a.nfeat == 0) return;
+	if (c->nranks == 1) {
+		const size_t p = prof_begin(c, is_w ? 1 : 0);
+		HIPCHK(is_w ? vbk::w_level_fused(a, c->s) : vbk::v_level_fused(a, c->s));
+		prof_end(c, p);
+		return;
+	}
+	HIPCHK(is_w ? vbk::w_level_stats(a, c->s) : vbk::v_level_stats(a, c->s));
+	NCCLCHK(ncclAllReduce(c->stats, c->stats, 2 * (size_t)a.nfeat, ncclDouble, ncclSum, c->comm, c->s));
+	HIPCHK(is_w ? vbk::w_level_correct(a, c->s) : vbk::v_level_correct(a, c->s));
+}
+
+uint32_t nlevels(vbfm_ctx *c) { return c->level_ptr.empty() ? 0 : (uint32_t)c->level_ptr.size() - 1; }
+
+// ---- the steps of update_all ------------------------------------------------------------
+void step_w0(vbfm_ctx *c)
+{
+	// update_w0 (fm_learn_vb.h:504-525)
+	const double sigma_old = c->s0d;
+	c->s0d = 1.0 / (c->sigma_0 + (double)c->n_global * c->alpha);
+	HIPCHK(vbk::row_sums(c->rows, c->tr.n, 0, c->mu0, c->red_d, c->RED_BLOCKS, c->s));
+	double w0_temp = finish_sum(c, c->RED_BLOCKS);
+	allreduce_host(c, &w0_temp, 1);
+	const double mu_old = c->mu0;
+	c->mu0 = c->s0d * c->alpha * w0_temp;
+	HIPCHK(vbk::w0_apply(c->rows, c->tr.n, mu_old - c->mu0, c->s0d - sigma_old, c->s));
+}
+
+void step_w(vbfm_ctx *c)
+{
+	for (uint32_t l = 0; l < nlevels(c); l++) sweep_level(c, l, true, 0);
+}
+
+void step_qcache(vbfm_ctx *c, int f)
+{
+	const size_t p = prof_begin(c, 2);
+	HIPCHK(vbk::qcache(c->tr.row_ptr, c->tr.csr, c->ms_v + (size_t)f * c->D, c->rows, c->tr.n, c->s));
+	prof_end(c, p);
+}
+
+void step_v(vbfm_ctx *c, int f)
+{
+	for (uint32_t l = 0; l < nlevels(c); l++) sweep_level(c, l, false, f);
+}
+
+double rows_energy(vbfm_ctx *c)
+{
+	HIPCHK(vbk::row_sums(c->rows, c->tr.n, 1, 0.0, c->red_d, c->RED_BLOCKS, c->s));
+	double s = finish_sum(c, c->RED_BLOCKS);
+	allreduce_host(c, &s, 1);
+	return s;
+}
+
+// fm_learn_vb.h:446-498; returns true on the early return of a NaN/inf alpha
+bool step_hyper(vbfm_ctx *c, double *energy_out, uint32_t *nan_alpha, uint32_t *inf_alpha)
+{
+	const double energy = rows_energy(c);
+	if (energy_out) *energy_out = energy;
+	const double alpha_old = c->alpha;
+	c->alpha = (double)c->n_global / energy;
+	if (std::isnan(c->alpha)) { if (nan_alpha) (*nan_alpha)++; c->alpha = alpha_old; return true; }
+	if (std::isinf(c->alpha)) { if (inf_alpha) (*inf_alpha)++; c->alpha = alpha_old; return true; }
+	c->sigma_0 = 1.0 / (c->mu0 * c->mu0 + c->s0d);
+	std::vector<double> seg = param_sums(c, 0);
+	for (uint32_t g = 0; g < c->G; g++) c->hyp_w[g] = (double)c->per_group[g] / seg[g];
+	for (int f = 0; f < c->k; f++)
+		for (uint32_t g = 0; g < c->G; g++)
+			c->hyp_v[(size_t)g * c->k + f] = (double)c->per_group[g] / seg[(size_t)(f + 1) * c->G + g];
+	upload_hyp(c);
+	return false;
+}
+
+// free_energy (fm_learn_vb.h:646-681), given sum(e^2 + t)
+double free_energy(vbfm_ctx *c, double energy)
+{
+	const double temp1 = 2 * 3.14 * (1.0 / c->alpha);
+	double fe = 0.0;
+	fe += -0.5 * c->alpha * energy - .5 * (double)c->n_global * std::log(temp1);
+	fe += -0.5 * c->sigma_0 * (c->mu0 * c->mu0 + c->s0d) + 0.5 * std::log(c->s0d * c->sigma_0) + .5;
+	std::vector<double> seg = param_sums(c, 1);
+	for (double v : seg) fe += v;
+	return fe;
+}
+
+void test_predict(vbfm_ctx *c)
+{
+	HIPCHK(vbk::predict_e(c->te.row_ptr, c->te.csr, c->ms_v, c->ms_w, c->D, c->k, c->k1, c->k0, c->mu0, c->e_test,
+	                      c->te.n, c->s));
+}
+
+void read_counters(vbfm_ctx *c, vbfm_iter_stats *o)
+{
+	uint32_t h[CNT_N];
+	HIPCHK(hipMemcpyAsync(h, c->counters, sizeof(h), hipMemcpyDeviceToHost, c->s));
+	sync(c);
+	o->nan_mu_w = h[CNT_NAN_MU_W]; o->nan_sigma_w = h[CNT_NAN_SIGMA_W]; o->inf_mu_w = h[CNT_INF_MU_W];
+	o->nan_mu_v = h[CNT_NAN_MU_V]; o->nan_sigma_v = h[CNT_NAN_SIGMA_V]; o->inf_mu_v = h[CNT_INF_MU_V];
+}
+
+float ev_ms(vbfm_ctx *c, int a, int b)
+{
+	float ms = 0.f;
+	HIPCHK(hipEventElapsedTime(&ms, c->ev[a], c->ev[b]));
+	return ms;
+}
+
+}  // namespace
+
+// =========================================================================================
+extern "C" {
+
+int vbfm_abi_version(void) { return VBFM_ABI_VERSION; }
+
+const char *vbfm_last_error(const vbfm_ctx *ctx)
+{
+	if (ctx) return ctx->err.c_str();
+	return vbfm_host_last_error();
+}
+
+int vbfm_create(vbfm_ctx **out, const vbfm_config *cfg)
+{
+	if (!out || !cfg) return fail(nullptr, "vbfm_create: null argument");
+	*out = nullptr;
+	if (cfg->task != 0) return fail(nullptr, "task not supported by the VB learner (regression only)");
+	if (cfg->num_factor < 0) return fail(nullptr, "negative number of factors");
+	if (cfg->num_attr_groups == 0) return fail(nullptr, "num_attr_groups must be >= 1");
+	int ndev = 0;
+	if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return fail(nullptr, "no HIP device available");
+	if (cfg->device < 0 || cfg->device >= ndev) return fail(nullptr, "device ordinal out of range");
+	vbfm_ctx *c = new vbfm_ctx();
+	c->dev = cfg->device;
+	c->k0 = cfg->k0 != 0; c->k1 = cfg->k1 != 0; c->k = cfg->num_factor;
+	c->D = cfg->num_attribute; c->G = cfg->num_attr_groups;
+	c->min_target = cfg->min_target; c->max_target = cfg->max_target;
+	int rc = guarded(c, [&] {
+		HIPCHK(hipStreamCreateWithFlags(&c->s, hipStreamNonBlocking));
+		for (int i = 0; i < EV_N; i++) HIPCHK(hipEventCreate(&c->ev[i]));
+		c->group_h.assign(c->D, 0);
+		if (cfg->attr_group)
+			for (uint32_t i = 0; i < c->D; i++) {
+				if (cfg->attr_group[i] >= c->G) throw std::string("attr_group out of range");
+				c->group_h[i] = cfg->attr_group[i];
+			}
+		c->per_group.assign(c->G, 0);
+		for (uint32_t i = 0; i < c->D; i++) c->per_group[c->group_h[i]]++;
+		c->group_d = dalloc<uint32_t>(c->D);
+		if (c->D) HIPCHK(hipMemcpy(c->group_d, c->group_h.data(), c->D * 4, hipMemcpyHostToDevice));
+		c->ms_v = dalloc<double2>((size_t)c->k * c->D);
+		c->ms_w = dalloc<double2>(c->D);
+		c->hyp_w_d = dalloc<double>(c->G);
+		c->hyp_v_d = dalloc<double>((size_t)c->G * c->k);
+		c->hyp_w.assign(c->G, 1.0);               // fm_learn_vb.h:707-708
+		c->hyp_v.assign((size_t)c->G * c->k, 1.0);
+		upload_hyp(c);
+		// fm_learn_vb.h:693-712 defaults: mu 0 until set_params, sigma .02
+		std::vector<double2> init((size_t)std::max<uint64_t>((uint64_t)c->k * c->D, c->D), make_double2(0.0, .02));
+		if ((size_t)c->k * c->D)
+			HIPCHK(hipMemcpy(c->ms_v, init.data(), (size_t)c->k * c->D * 16, hipMemcpyHostToDevice));
+		if (c->D) HIPCHK(hipMemcpy(c->ms_w, init.data(), (size_t)c->D * 16, hipMemcpyHostToDevice));
+		c->red_d = dalloc<double>(2 * vbfm_ctx::RED_BLOCKS);
+		c->red_h.assign(2 * vbfm_ctx::RED_BLOCKS, 0.0);
+		c->counters = dalloc<uint32_t>(CNT_N);
+		HIPCHK(hipMemset(c->counters, 0, CNT_N * 4));
+		build_chunks(c);
+	});
+	if (rc) {
+		vbfm_host_set_error(c->err.c_str());
+		vbfm_destroy(c);
+		return rc;
+	}
+	*out = c;
+	return 0;
+}
+
+void vbfm_destroy(vbfm_ctx *c)
+{
+	if (!c) return;
+	(void)hipSetDevice(c->dev);
+	if (c->s) (void)hipStreamSynchronize(c->s);
+	free_data(c->tr);
+	free_data(c->te);
+	dfree(c->rows); dfree(c->scratch_n); dfree(c->e_test); dfree(c->pred_test);
+	dfree(c->ms_v); dfree(c->ms_w); dfree(c->hyp_w_d); dfree(c->hyp_v_d); dfree(c->group_d);
+	dfree(c->level_feats); dfree(c->dup); dfree(c->red_d); dfree(c->perm_d); dfree(c->chunks_d);
+	dfree(c->chunk_out_d); dfree(c->counters); dfree(c->stats);
+	if (c->comm) ncclCommDestroy(c->comm);
+	for (hipEvent_t e : c->pev) (void)hipEventDestroy(e);
+	for (int i = 0; i < EV_N; i++)
+		if (c->ev[i]) (void)hipEventDestroy(c->ev[i]);
+	if (c->s) (void)hipStreamDestroy(c->s);
+	delete c;
+}
+
+static void alloc_rows(vbfm_ctx *c)
+{
+	dfree(c->rows);
+	dfree(c->scratch_n);
+	c->rows = dalloc<RowRec>(c->tr.n);
+	c->scratch_n = dalloc<double>(c->tr.n);
+	HIPCHK(hipMemsetAsync(c->rows, 0, (size_t)std::max(c->tr.n, 1u) * sizeof(RowRec), c->s));
+	uint64_t n = c->tr.n;
+	c->n_global = n;
+	if (c->nranks > 1) {
+		double v = (double)n;
+		allreduce_host(c, &v, 1);
+		c->n_global = (uint64_t)v;
+	}
+	c->sched_ready = false;
+}
+
+// the train feature count every shard pads to (the max over shards)
+static uint32_t global_nf(vbfm_ctx *c, uint32_t nf)
+{
+	if (c->nranks == 1) return nf;
+	uint32_t *w = dalloc<uint32_t>(1);
+	HIPCHK(hipMemcpyAsync(w, &nf, 4, hipMemcpyHostToDevice, c->s));
+	NCCLCHK(ncclAllReduce(w, w, 1, ncclUint32, ncclMax, c->comm, c->s));
+	uint32_t out = 0;
+	HIPCHK(hipMemcpyAsync(&out, w, 4, hipMemcpyDeviceToHost, c->s));
+	sync(c);
+	dfree(w);
+	return out;
+}
+
+int vbfm_set_train(vbfm_ctx *c, const vbfm_csc *in)
+{
+	if (!c) return fail(nullptr, "null context");
+	return guarded(c, [&] {
+		check_csc(in);
+		const uint32_t nf = global_nf(c, in->num_feature);
+		if (nf > c->D) throw std::string("train num_feature exceeds num_attribute");
+		upload(c, c->tr, in, nf);
+		alloc_rows(c);
+	});
+}
+
+int vbfm_set_test(vbfm_ctx *c, const vbfm_csc *in)
+{
+	if (!c) return fail(nullptr, "null context");
+	return guarded(c, [&] {
+		check_csc(in);
+		if (in->num_feature > c->D) throw std::string("test num_feature exceeds num_attribute");
+		upload(c, c->te, in, in->num_feature);
+		dfree(c->e_test);
+		dfree(c->pred_test);
+		c->e_test = dalloc<double>(c->te.n);
+		c->pred_test = dalloc<double>(c->te.n);
+		double v = c->te.n;
+		allreduce_host(c, &v, 1);
+		c->test_n_global = (uint32_t)v;
+	});
+}
+
+int vbfm_synth_generate(vbfm_ctx *c, int32_t which, uint32_t n, uint32_t F, uint32_t S, uint64_t seed, int32_t xmode)
+{
+	if (!c) return fail(nullptr, "null context");
+	return guarded(c, [&] {
+		if (which != 0 && which != 1) throw std::string("which must be 0 (train) or 1 (test)");
+		const uint64_t nf64 = (uint64_t)F * S;
+		if (nf64 >= 0xFFFFFFFFull || nf64 >= c->D || F == 0 || S == 0)
+			throw std::string("synthetic shape does not fit num_attribute");
+		DevData &d = which ? c->te : c->tr;
+		free_data(d);
+		d.n = n;
+		d.nf_local = (uint32_t)nf64;
+		d.nf = which ? d.nf_local : global_nf(c, d.nf_local);
+		d.nnz = (uint64_t)n * F;
+		d.row_ptr = dalloc<uint64_t>((size_t)n + 1);
+		d.csr = dalloc<uint2>(d.nnz);
+		d.target = dalloc<float>(n);
+		d.col_ptr = dalloc<uint64_t>((size_t)d.nf + 1);
+		d.csc = dalloc<uint2>(d.nnz);
+		HIPCHK(vbk::synth_csr(n, F, S, seed, xmode, d.row_ptr, d.csr, d.target, c->s));
+		// col_ptr: feature histogram + exclusive scan (padded columns stay empty)
+		uint64_t *counts = dalloc<uint64_t>((size_t)d.nf + 1);
+		HIPCHK(hipMemsetAsync(counts, 0, ((size_t)d.nf + 1) * 8, c->s));
+		HIPCHK(vbk::count_features(d.csr, d.nnz, counts, c->s));
+		size_t tb = 0;
+		HIPCHK(vbk::exclusive_scan_u64(nullptr, &tb, counts, d.col_ptr, (size_t)d.nf + 1, c->s));
+		void *tmp = dalloc<uint8_t>(tb);
+		HIPCHK(vbk::exclusive_scan_u64(tmp, &tb, counts, d.col_ptr, (size_t)d.nf + 1, c->s));
+		dfree(tmp);
+		dfree(counts);
+		// CSC per field: stable radix sort of (id within field, row) keeps rows ascending
+		uint32_t *ki = dalloc<uint32_t>(n), *ko = dalloc<uint32_t>(n), *vi = dalloc<uint32_t>(n),
+		         *vo = dalloc<uint32_t>(n);
+		int bits = 1;
+		while ((1ull << bits) < S) bits++;
+		tb = 0;
+		HIPCHK(vbk::sort_pairs_u32(nullptr, &tb, ki, ko, vi, vo, n, bits, c->s));
+		void *stmp = dalloc<uint8_t>(tb);
+		for (uint32_t fl = 0; fl < F; fl++) {
+			HIPCHK(vbk::synth_field_keys(d.csr, n, F, S, fl, ki, vi, c->s));
+			size_t tb2 = tb;
+			HIPCHK(vbk::sort_pairs_u32(stmp, &tb2, ki, ko, vi, vo, n, bits, c->s));
+			HIPCHK(vbk::synth_field_scatter(vo, d.csr, n, F, fl, d.csc + (uint64_t)fl * n, c->s));
+		}
+		sync(c);
+		dfree(stmp); dfree(ki); dfree(ko); dfree(vi); dfree(vo);
+		// target range (min/max over the targets: 1..5 by construction, computed exactly)
+		std::vector<float> t(n);
+		if (n) HIPCHK(hipMemcpy(t.data(), d.target, (size_t)n * 4, hipMemcpyDeviceToHost));
+		float mn = 3.40282347e+38f, mx = -3.40282347e+38f;
+		for (float v : t) { mn = std::min(v, mn); mx = std::max(v, mx); }
+		d.min_target = mn; d.max_target = mx;
+		if (which == 0) alloc_rows(c);
+		else {
+			dfree(c->e_test); dfree(c->pred_test);
+			c->e_test = dalloc<double>(n);
+			c->pred_test = dalloc<double>(n);
+			double v = n;
+			allreduce_host(c, &v, 1);
+			c->test_n_global = (uint32_t)v;
+		}
+	});
+}
+
+int vbfm_get_shape(vbfm_ctx *c, int32_t which, uint32_t *n, uint32_t *nf, uint64_t *nnz)
+{
+	if (!c) return fail(nullptr, "null context");
+	const DevData &d = which ? c->te : c->tr;
+	if (n) *n = d.n;
+	if (nf) *nf = d.nf_local;
+	if (nnz) *nnz = d.nnz;
+	return 0;
+}
+
+int vbfm_get_csc(vbfm_ctx *c, int32_t which, uint64_t *col_ptr, vbfm_entry *col_ent, float *target)
+{
+	if (!c) return fail(nullptr, "null context");
+	return guarded(c, [&] {
+		const DevData &d = which ? c->te : c->tr;
+		if (col_ptr) HIPCHK(hipMemcpy(col_ptr, d.col_ptr, ((size_t)d.nf_local + 1) * 8, hipMemcpyDeviceToHost));
+		if (col_ent && d.nnz) HIPCHK(hipMemcpy(col_ent, d.csc, d.nnz * 8, hipMemcpyDeviceToHost));
+		if (target && d.n) HIPCHK(hipMemcpy(target, d.target, (size_t)d.n * 4, hipMemcpyDeviceToHost));
+	});
+}
+
+int vbfm_get_levels(vbfm_ctx *c, uint32_t *level, uint32_t *num_levels)
+{
+	if (!c) return fail(nullptr, "null context");
+	return guarded(c, [&] {
+		require_train(c);
+		if (level) std::copy(c->level_h.begin(), c->level_h.begin() + c->tr.nf_local, level);
+		if (num_levels) *num_levels = nlevels(c);
+	});
+}
+
+int vbfm_set_params(vbfm_ctx *c, const vbfm_params *p)
+{
+	if (!c || !p) return fail(c, "null argument");
+	return guarded(c, [&] {
+		const size_t kd = (size_t)c->k * c->D;
+		if (!p->mu_w || !p->sigma_w || (kd && (!p->mu_v || !p->sigma_v)))
+			throw std::string("vbfm_set_params: parameter arrays missing");
+		double *tmp = dalloc<double>(2 * std::max(kd, (size_t)c->D));
+		HIPCHK(hipMemcpyAsync(tmp, p->mu_w, c->D * 8, hipMemcpyHostToDevice, c->s));
+		HIPCHK(hipMemcpyAsync(tmp + c->D, p->sigma_w, c->D * 8, hipMemcpyHostToDevice, c->s));
+		HIPCHK(vbk::pack_pairs(tmp, tmp + c->D, c->ms_w, c->D, c->s));
+		sync(c);
+		if (kd) {
+			HIPCHK(hipMemcpyAsync(tmp, p->mu_v, kd * 8, hipMemcpyHostToDevice, c->s));
+			HIPCHK(hipMemcpyAsync(tmp + kd, p->sigma_v, kd * 8, hipMemcpyHostToDevice, c->s));
+			HIPCHK(vbk::pack_pairs(tmp, tmp + kd, c->ms_v, kd, c->s));
+			sync(c);
+		}
+		dfree(tmp);
+		if (p->hyp_sigma_w) std::copy(p->hyp_sigma_w, p->hyp_sigma_w + c->G, c->hyp_w.begin());
+		if (p->hyp_sigma_v) std::copy(p->hyp_sigma_v, p->hyp_sigma_v + (size_t)c->G * c->k, c->hyp_v.begin());
+		upload_hyp(c);
+		c->alpha = p->alpha; c->sigma_0 = p->sigma_0; c->mu0 = p->mu_0_dash; c->s0d = p->sigma_0_dash;
+		sync(c);
+	});
+}
+
+int vbfm_get_params(vbfm_ctx *c, vbfm_params *p)
+{
+	if (!c || !p) return fail(c, "null argument");
+	return guarded(c, [&] {
+		const size_t kd = (size_t)c->k * c->D;
+		double *tmp = dalloc<double>(2 * std::max(kd, (size_t)c->D));
+		HIPCHK(vbk::unpack_pairs(c->ms_w, tmp, tmp + c->D, c->D, c->s));
+		if (p->mu_w) HIPCHK(hipMemcpyAsync(p->mu_w, tmp, c->D * 8, hipMemcpyDeviceToHost, c->s));
+		if (p->sigma_w) HIPCHK(hipMemcpyAsync(p->sigma_w, tmp + c->D, c->D * 8, hipMemcpyDeviceToHost, c->s));
+		sync(c);
+		if (kd) {
+			HIPCHK(vbk::unpack_pairs(c->ms_v, tmp, tmp + kd, kd, c->s));
+			if (p->mu_v) HIPCHK(hipMemcpyAsync(p->mu_v, tmp, kd * 8, hipMemcpyDeviceToHost, c->s));
+			if (p->sigma_v) HIPCHK(hipMemcpyAsync(p->sigma_v, tmp + kd, kd * 8, hipMemcpyDeviceToHost, c->s));
+			sync(c);
+		}
+		dfree(tmp);
+		if (p->hyp_sigma_w) std::copy(c->hyp_w.begin(), c->hyp_w.end(), p->hyp_sigma_w);
+		if (p->hyp_sigma_v) std::copy(c->hyp_v.begin(), c->hyp_v.end(), p->hyp_sigma_v);
+		p->alpha = c->alpha; p->sigma_0 = c->sigma_0; p->mu_0_dash = c->mu0; p->sigma_0_dash = c->s0d;
+	});
+}
+
+int vbfm_init_params_device(vbfm_ctx *c, uint64_t seed)
+{
+	if (!c) return fail(nullptr, "null context");
+	return guarded(c, [&] {
+		HIPCHK(vbk::init_normal_pairs(c->ms_w, c->D, seed, 11, c->s));
+		HIPCHK(vbk::init_normal_pairs(c->ms_v, (size_t)c->k * c->D, seed, 12, c->s));
+		std::fill(c->hyp_w.begin(), c->hyp_w.end(), 1.0);
+		std::fill(c->hyp_v.begin(), c->hyp_v.end(), 1.0);
+		upload_hyp(c);
+		c->alpha = 1.0; c->sigma_0 = 1.0; c->mu0 = 0.0; c->s0d = 0.02;
+		sync(c);
+	});
+}
+
+int vbfm_init_caches(vbfm_ctx *c)
+{
+	if (!c) return fail(nullptr, "null context");
+	return guarded(c, [&] {
+		require_train(c);
+		// fm_learn_vb_simultaneous.h:37-44: yhat of train and test, T of train, e = y - yhat
+		HIPCHK(vbk::predict_e(c->tr.row_ptr, c->tr.csr, c->ms_v, c->ms_w, c->D, c->k, c->k1, c->k0, c->mu0,
+		                      c->scratch_n, c->tr.n, c->s));
+		HIPCHK(vbk::predict_t(c->tr.row_ptr, c->tr.csr, c->ms_v, c->ms_w, c->D, c->k, c->k1, c->k0, c->s0d, c->rows,
+		                      c->tr.n, c->s));
+		HIPCHK(vbk::residual_init(c->rows, c->scratch_n, c->tr.target, c->tr.n, c->s));
+		if (c->e_test) test_predict(c);
+		sync(c);
+	});
+}
+
+int vbfm_step_w0(vbfm_ctx *c)
+{
+	if (!c) return fail(nullptr, "null context");
+	return guarded(c, [&] { require_train(c); if (c->k0) step_w0(c); sync(c); });
+}
+
+int vbfm_step_w(vbfm_ctx *c)
+{
+	if (!c) return fail(nullptr, "null context");
+	return guarded(c, [&] { require_train(c); if (c->k1) step_w(c); sync(c); });
+}
+
+int vbfm_step_qcache(vbfm_ctx *c, int32_t f)
+{
+	if (!c) return fail(nullptr, "null context");
+	return guarded(c, [&] {
+		require_train(c);
+		if (f < 0 || f >= c->k) throw std::string("factor out of range");
+		step_qcache(c, f);
+		sync(c);
+	});
+}
+
+int vbfm_step_v(vbfm_ctx *c, int32_t f)
+{
+	if (!c) return fail(nullptr, "null context");
+	return guarded(c, [&] {
+		require_train(c);
+		if (f < 0 || f >= c->k) throw std::string("factor out of range");
+		step_v(c, f);
+		sync(c);
+	});
+}
+
+int vbfm_step_hyper(vbfm_ctx *c, int32_t *early)
+{
+	if (!c) return fail(nullptr, "null context");
+	return guarded(c, [&] {
+		require_train(c);
+		const bool e = step_hyper(c, nullptr, nullptr, nullptr);
+		if (early) *early = e ? 1 : 0;
+		sync(c);
+	});
+}
+
+int vbfm_free_energy(vbfm_ctx *c, double *F)
+{
+	if (!c || !F) return fail(c, "null argument");
+	return guarded(c, [&] { require_train(c); *F = free_energy(c, rows_energy(c)); });
+}
+
+int vbfm_get_rows(vbfm_ctx *c, double *e, double *t, double *q, double *tq, double *tz)
+{
+	if (!c) return fail(nullptr, "null context");
+	return guarded(c, [&] {
+		std::vector<RowRec> h(c->tr.n);
+		if (c->tr.n) HIPCHK(hipMemcpy(h.data(), c->rows, (size_t)c->tr.n * sizeof(RowRec), hipMemcpyDeviceToHost));
+		for (uint32_t i = 0; i < c->tr.n; i++) {
+			if (e) e[i] = h[i].e;
+			if (t) t[i] = h[i].t;
+			if (q) q[i] = h[i].q;
+			if (tq) tq[i] = h[i].tq;
+			if (tz) tz[i] = h[i].tz;
+		}
+	});
+}
+
+int vbfm_get_test_e(vbfm_ctx *c, double *e)
+{
+	if (!c || !e) return fail(c, "null argument");
+	return guarded(c, [&] {
+		if (c->te.n) HIPCHK(hipMemcpy(e, c->e_test, (size_t)c->te.n * 8, hipMemcpyDeviceToHost));
+	});
+}
+
+int vbfm_get_test_pred(vbfm_ctx *c, double *pred)
+{
+	if (!c || !pred) return fail(c, "null argument");
+	return guarded(c, [&] {
+		if (c->te.n) HIPCHK(hipMemcpy(pred, c->pred_test, (size_t)c->te.n * 8, hipMemcpyDeviceToHost));
+	});
+}
+
+int vbfm_factor_sweep(vbfm_ctx *c, double *ms_device)
+{
+	if (!c) return fail(nullptr, "null context");
+	return guarded(c, [&] {
+		require_train(c);
+		HIPCHK(hipEventRecord(c->ev[EV_BEGIN], c->s));
+		for (int f = 0; f < c->k; f++) { step_qcache(c, f); step_v(c, f); }
+		HIPCHK(hipEventRecord(c->ev[EV_V], c->s));
+		sync(c);
+		if (ms_device) *ms_device = ev_ms(c, EV_BEGIN, EV_V);
+	});
+}
+
+int vbfm_iterate(vbfm_ctx *c, vbfm_iter_stats *o)
+{
+	if (!c) return fail(nullptr, "null context");
+	return guarded(c, [&] {
+		require_train(c);
+		if (!c->e_test) throw std::string("no test data set (vbfm_set_test)");
+		vbfm_iter_stats st;
+		memset(&st, 0, sizeof(st));
+		HIPCHK(hipMemsetAsync(c->counters, 0, CNT_N * 4, c->s));
+		c->pev_used = 0;
+		c->spans.clear();
+		HIPCHK(hipEventRecord(c->ev[EV_BEGIN], c->s));
+		// update_all (fm_learn_vb.h:383-501)
+		if (c->k0) step_w0(c);
+		HIPCHK(hipEventRecord(c->ev[EV_W0], c->s));
+		if (c->k1) step_w(c);
+		HIPCHK(hipEventRecord(c->ev[EV_W], c->s));
+		if (c->D > 0)
+			for (int f = 0; f < c->k; f++) { step_qcache(c, f); step_v(c, f); }
+		HIPCHK(hipEventRecord(c->ev[EV_V], c->s));
+		double energy = 0.0;
+		const bool early = step_hyper(c, &energy, &st.nan_alpha, &st.inf_alpha);
+		st.free_energy_valid = early ? 0 : 1;
+		st.free_energy = early ? NAN : free_energy(c, energy);
+		HIPCHK(hipEventRecord(c->ev[EV_HYPER], c->s));
+		// test prediction and metrics (fm_learn_vb_simultaneous.h:125-222)
+		test_predict(c);
+		const double mn = c->min_target, mx = c->max_target;
+		HIPCHK(vbk::test_metrics(c->e_test, c->te.target, c->te.n, mn, mx, c->pred_test, c->red_d, c->RED_BLOCKS, c->s));
+		HIPCHK(hipMemcpyAsync(c->red_h.data(), c->red_d, 2 * c->RED_BLOCKS * 8, hipMemcpyDeviceToHost, c->s));
+		sync(c);
+		double tm[3] = {0.0, 0.0, 0.0};
+		for (uint32_t i = 0; i < c->RED_BLOCKS; i++) { tm[0] += c->red_h[2 * i]; tm[1] += c->red_h[2 * i + 1]; }
+		HIPCHK(vbk::train_quirk(c->rows, c->tr.n, mn, mx, c->red_d, c->RED_BLOCKS, c->s));
+		tm[2] = finish_sum(c, c->RED_BLOCKS);
+		allreduce_host(c, tm, 3);
+		HIPCHK(hipEventRecord(c->ev[EV_TEST], c->s));
+		sync(c);
+		st.rmse = std::sqrt(tm[0] / c->test_n_global);
+		st.mae = tm[1] / c->test_n_global;
+		st.train_quirk = std::sqrt(tm[2] / (double)c->n_global);
+		st.num_levels = (int32_t)nlevels(c);
+		st.alpha = c->alpha; st.sigma_0 = c->sigma_0; st.mu_0_dash = c->mu0; st.sigma_0_dash = c->s0d;
+		read_counters(c, &st);
+		st.ms_w0 = ev_ms(c, EV_BEGIN, EV_W0);
+		st.ms_w = ev_ms(c, EV_W0, EV_W);
+		st.ms_v = ev_ms(c, EV_W, EV_V);
+		st.ms_qcache = 0.0;
+		st.ms_hyper = ev_ms(c, EV_V, EV_HYPER);
+		st.ms_test = ev_ms(c, EV_HYPER, EV_TEST);
+		st.ms_total = ev_ms(c, EV_BEGIN, EV_TEST);
+		st.nnz_train = c->tr.nnz;
+		for (const auto &sp : c->spans) {
+			float ms = 0.f;
+			HIPCHK(hipEventElapsedTime(&ms, c->pev[sp.a], c->pev[sp.a + 1]));
+			if (sp.kind == 0) { st.ms_vlevel_kernels += ms; st.n_vlevel_launches++; }
+			else if (sp.kind == 1) { st.ms_wlevel_kernels += ms; st.n_wlevel_launches++; }
+			else { st.ms_qcache_kernels += ms; st.n_qcache_launches++; }
+		}
+		st.ms_qcache = st.ms_qcache_kernels;
+		if (o) *o = st;
+	});
+}
+
+int vbfm_set_profiling(vbfm_ctx *c, int32_t on)
+{
+	if (!c) return fail(nullptr, "null context");
+	c->profiling = on != 0;
+	return 0;
+}
+
+int vbfm_comm_unique_id(uint8_t out[128])
+{
+	ncclUniqueId id;
+	if (ncclGetUniqueId(&id) != ncclSuccess) return fail(nullptr, "ncclGetUniqueId failed");
+	static_assert(sizeof(id) == 128, "ncclUniqueId is 128 bytes");
+	memcpy(out, &id, 128);
+	return 0;
+}
+
+int vbfm_comm_init(vbfm_ctx *c, int32_t nranks, int32_t rank, const uint8_t uid[128])
+{
+	if (!c) return fail(nullptr, "null context");
+	return guarded(c, [&] {
+		if (c->rows) throw std::string("vbfm_comm_init must precede vbfm_set_train");
+		if (nranks < 1 || rank < 0 || rank >= nranks) throw std::string("bad rank / nranks");
+		if (nranks == 1) return;
+		ncclUniqueId id;
+		memcpy(&id, uid, 128);
+		NCCLCHK(ncclCommInitRank(&c->comm, nranks, id, rank));
+		c->nranks = nranks;
+		c->rank = rank;
+	});
+}
+
+}  // extern "C"

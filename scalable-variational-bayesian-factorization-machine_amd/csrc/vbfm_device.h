@@ -1,0 +1,104 @@
+// vbfm_device.h -- device-side data layout shared by the kernels and the C-ABI layer.
+//
+// HBM layout (one context = one GPU = one row shard):
+//   RowRec rows[N]      64-B aligned record per train row: the reference's two row caches
+//                       e_q_term{e,q} (fm_learn_mcmc.h:52-55) and t_term{t,q,z}
+//                       (fm_learn_vb.h:17-21) fused so that one 64-B line serves every
+//                       gather of a row (e,q,tq,tz,t = 40 B used).
+//   CSC  col_ptr[nf+1] (u64), csc[nnz] (uint2 = {row, fp32 bits}) == sparse_entry<float>
+//   CSR  row_ptr[N+1]  (u64), csr[nnz] (uint2 = {feature, fp32 bits}), each row sorted by
+//                       feature id: the order in which the reference's column-major loops
+//                       visit a row, so per-row sums are bit-identical to the reference.
+//   ms_v[k*D] (double2 = {mu, sigma}) of mu_v_dash/sigma_v_dash, factor-major;
+//   ms_w[D]   (double2 = {mu, sigma}) of mu_w_dash/sigma_w_dash.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+struct __attribute__((aligned(64))) RowRec {
+	double e;    // cache[i].e      residual y - yhat (fm_learn_vb_simultaneous.h:42-44)
+	double q;    // cache[i].q      q-cache of the current factor: sum mu x
+	double tq;   // cache_t[i].q    sum sigma x^2
+	double tz;   // cache_t[i].z    sum mu^2 x^2
+	double t;    // cache_t[i].t    variance term T_n (paper eq. 26)
+	double pad[3];
+};
+static_assert(sizeof(RowRec) == 64, "RowRec must be one 64-B line");
+
+enum {
+	CNT_NAN_MU_W = 0, CNT_NAN_SIGMA_W, CNT_INF_MU_W,
+	CNT_NAN_MU_V, CNT_NAN_SIGMA_V, CNT_INF_MU_V,
+	CNT_N
+};
+
+// per-level launch description for the v / w sweeps
+struct LevelArgs {
+	const uint64_t *col_ptr;
+	const uint2 *csc;
+	const uint32_t *feats;     // features of this level (ascending id)
+	uint32_t nfeat;
+	RowRec *rows;
+	double2 *ms;               // ms_v + f*D, or ms_w
+	const double *hyp;         // hyper prior: sigma_v(g, f) at hyp[g*stride], or sigma_w(g)
+	uint32_t hyp_stride;
+	const uint32_t *attr_group;
+	const uint8_t *dup;        // column has a repeated row (sequential correction)
+	double alpha;
+	uint32_t *counters;
+	double2 *stats;            // split mode: per-level-feature (sum1, sum2), or nullptr
+};
+
+// kernels launched from the C-ABI layer (vbfm_kernels.hip)
+namespace vbk {
+hipError_t v_level_fused(const LevelArgs &a, hipStream_t s);
+hipError_t w_level_fused(const LevelArgs &a, hipStream_t s);
+hipError_t v_level_stats(const LevelArgs &a, hipStream_t s);
+hipError_t v_level_correct(const LevelArgs &a, hipStream_t s);
+hipError_t w_level_stats(const LevelArgs &a, hipStream_t s);
+hipError_t w_level_correct(const LevelArgs &a, hipStream_t s);
+hipError_t qcache(const uint64_t *row_ptr, const uint2 *csr, const double2 *ms_f, RowRec *rows,
+                  uint32_t n, hipStream_t s);
+hipError_t predict_e(const uint64_t *row_ptr, const uint2 *csr, const double2 *ms_v, const double2 *ms_w,
+                     uint32_t D, int k, int k1, int k0, double mu0, double *out_e, uint32_t n,
+                     hipStream_t s);
+hipError_t predict_t(const uint64_t *row_ptr, const uint2 *csr, const double2 *ms_v, const double2 *ms_w,
+                     uint32_t D, int k, int k1, int k0, double sigma0_dash, RowRec *rows, uint32_t n,
+                     hipStream_t s);
+hipError_t residual_init(RowRec *rows, const double *yhat, const float *target, uint32_t n, hipStream_t s);
+// per-block partial sums over rows; mode 0: e + mu0 ; mode 1: e*e + t ; out[nblocks]
+hipError_t row_sums(const RowRec *rows, uint32_t n, int mode, double mu0, double *out, uint32_t nblocks,
+                    hipStream_t s);
+hipError_t w0_apply(RowRec *rows, uint32_t n, double de, double dt, hipStream_t s);
+// test metrics: per block (sum err^2, sum |err|) of clipped predictions, and pred_this
+hipError_t test_metrics(const double *e_test, const float *target, uint32_t n, double mn, double mx,
+                        double *pred, double *out, uint32_t nblocks, hipStream_t s);
+// train quirk: per block sum clip(e)^2
+hipError_t train_quirk(const RowRec *rows, uint32_t n, double mn, double mx, double *out, uint32_t nblocks,
+                       hipStream_t s);
+// hyper-parameter / free-energy partial sums over attribute chunks (see vbfm_capi.hip)
+struct Chunk { uint32_t begin, end; int32_t f; uint32_t g; };
+hipError_t param_sums(const double2 *ms_w, const double2 *ms_v, const uint32_t *perm, uint32_t D,
+                      const Chunk *chunks, uint32_t nchunks, int mode, const double *hyp_w,
+                      const double *hyp_v, int k, double *out, hipStream_t s);
+// level schedule
+hipError_t level_init(uint32_t *level, uint32_t nf, hipStream_t s);
+hipError_t level_relax(const uint64_t *row_ptr, const uint2 *csr, uint32_t n, uint32_t nf, uint32_t *level,
+                       uint32_t *changed, hipStream_t s);
+hipError_t mark_dups(const uint64_t *row_ptr, const uint2 *csr, uint32_t n, uint8_t *dup, hipStream_t s);
+// synthetic generator (tests/synth.py is the specification)
+hipError_t synth_csr(uint32_t n, uint32_t F, uint32_t S, uint64_t seed, int xmode, uint64_t *row_ptr,
+                     uint2 *csr, float *target, hipStream_t s);
+hipError_t synth_field_keys(const uint2 *csr, uint32_t n, uint32_t F, uint32_t S, uint32_t field,
+                            uint32_t *keys, uint32_t *vals, hipStream_t s);
+hipError_t synth_field_scatter(const uint32_t *sorted_rows, const uint2 *csr, uint32_t n, uint32_t F,
+                               uint32_t field, uint2 *csc_field, hipStream_t s);
+hipError_t count_features(const uint2 *csr, uint64_t nnz, uint64_t *counts, hipStream_t s);
+hipError_t sort_pairs_u32(void *tmp, size_t *tmp_bytes, const uint32_t *ki, uint32_t *ko, const uint32_t *vi,
+                          uint32_t *vo, size_t n, int bits, hipStream_t s);
+hipError_t exclusive_scan_u64(void *tmp, size_t *tmp_bytes, const uint64_t *in, uint64_t *out, size_t n,
+                              hipStream_t s);
+hipError_t init_normal_pairs(double2 *ms, size_t n, uint64_t seed, uint64_t stream, hipStream_t s);
+// layout conversion between the reference's separate mu/sigma arrays and double2 pairs
+hipError_t pack_pairs(const double *a, const double *b, double2 *out, size_t n, hipStream_t s);
+hipError_t unpack_pairs(const double2 *in, double *a, double *b, size_t n, hipStream_t s);
+}  // namespace vbk

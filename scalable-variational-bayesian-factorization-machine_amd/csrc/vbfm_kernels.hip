@@ -1,0 +1,938 @@
+// vbfm_kernels.hip -- CDNA4 (gfx950) kernels of the VB factorization-machine sweep.
+//
+// Every kernel restates one loop of the reference (citations relative to /root/reference)
+// with the reference's arithmetic, expression by expression: x is fp32 and a product of
+// two fp32 values is rounded to fp32 before it meets a double (FM_FLOAT,
+// src/fm_core/fm_data.h:25). Built with -ffp-contract=off so no FMA is formed. Where a
+// sum runs over many independent terms (a column's sufficient statistics, a data set's
+// residual energy) the device sums in a fixed tree order: deterministic run to run, equal
+// to the reference up to summation order (~1e-16 relative). Per-row sums (q-cache,
+// predictions) keep the reference's sequential ascending-feature order and are bit-exact.
+//
+// Parallel schedule: the reference updates features one at a time in ascending id order
+// (Gauss-Seidel). Two features interact only through rows they share, so the features are
+// grouped into dependency levels (level(j) = 1 + max level of an earlier feature sharing a
+// row); all features of one level are updated concurrently, one workgroup per feature
+// column, which reproduces the sequential result exactly (each row is touched by at most
+// one feature per level, in the same relative order as the reference).
+#include "vbfm_device.h"
+#include <rocprim/device/device_radix_sort.hpp>
+#include <rocprim/device/device_scan.hpp>
+
+#define DEVI __device__ __forceinline__
+
+namespace {
+
+DEVI double wave_sum(double v)
+{
+	// xor butterfly: lanes i and i^o add the same two values (a+b == b+a), so every lane
+	// ends with the identical, order-fixed sum
+#pragma unroll
+	for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+	return v;
+}
+
+template <int BLOCK>
+DEVI void block_sum2(double &a, double &b, double *lds /* [2*BLOCK/64] */)
+{
+	a = wave_sum(a);
+	b = wave_sum(b);
+	if constexpr (BLOCK > 64) {
+		const int w = threadIdx.x >> 6;
+		if ((threadIdx.x & 63) == 0) { lds[2 * w] = a; lds[2 * w + 1] = b; }
+		__syncthreads();
+		a = lds[0]; b = lds[1];
+#pragma unroll
+		for (int i = 1; i < BLOCK / 64; ++i) { a += lds[2 * i]; b += lds[2 * i + 1]; }
+	}
+}
+
+template <int BLOCK>
+DEVI double block_sum1(double a, double *lds)
+{
+	a = wave_sum(a);
+	if constexpr (BLOCK > 64) {
+		const int w = threadIdx.x >> 6;
+		__syncthreads();
+		if ((threadIdx.x & 63) == 0) lds[w] = a;
+		__syncthreads();
+		a = lds[0];
+#pragma unroll
+		for (int i = 1; i < BLOCK / 64; ++i) a += lds[i];
+	}
+	return a;
+}
+
+DEVI float ent_x(uint2 ent) { return __uint_as_float(ent.y); }
+
+DEVI bool dnan(double v) { return __builtin_isnan(v); }
+DEVI bool dinf(double v) { return __builtin_isinf(v); }
+
+// ------------------------------------------------------------------------------------
+// v sweep: update_v (src/libfm/src/fm_learn_vb.h:577-644)
+
+// stats term of one entry (fm_learn_vb.h:592-595)
+DEVI void v_stat(float x, double e, double q, double tq, double mo, double so, double &vm, double &vs)
+{
+	const float xx = x * x;
+	const double h = q - x * mo;
+	const double h1 = tq - xx * so;
+	vm += x * h * (e + x * mo * h);
+	vs += xx * h * h + xx * h1;
+}
+
+// posterior + guards (fm_learn_vb.h:597-619); returns false when the correction is skipped
+DEVI bool v_post(double vm, double vs, double sv_g, double alpha, double mo, double so,
+                 double &mu, double &sig, uint32_t *counters, bool leader)
+{
+	sig = (double)1.0 / (sv_g + alpha * vs);
+	mu = sig * alpha * vm;
+	if (dnan(sig) || dinf(sig)) {
+		sig = so;
+		if (leader) atomicAdd(&counters[CNT_NAN_SIGMA_V], 1u);
+	}
+	if (dnan(mu)) {
+		mu = mo;
+		if (leader) atomicAdd(&counters[CNT_NAN_MU_V], 1u);
+		return false;
+	}
+	if (dinf(mu)) {
+		mu = mo;
+		if (leader) atomicAdd(&counters[CNT_INF_MU_V], 1u);
+		return false;
+	}
+	return true;
+}
+
+// correction of one row (fm_learn_vb.h:623-643); e,q,tq,tz,t updated in place
+DEVI void v_corr(float x, double mo, double so, double mu, double sig, double &e, double &q, double &tq,
+                 double &tz, double &t)
+{
+	const float xx = x * x;
+	const double h = x * (q - x * mo);
+	const double h1 = xx * (tq - xx * so);
+	const double h2 = xx * (tz - xx * mo * mo);
+	q += x * (mu - mo);
+	tq += xx * (sig - so);
+	tz += xx * (mu * mu - mo * mo);
+	e += h * (mo - mu);
+	t += (h1 + h2) * (sig - so);
+	t += h1 * (mu * mu - mo * mo);
+}
+
+DEVI void load_row(const RowRec *rows, uint32_t r, double &e, double &q, double &tq, double &tz, double &t)
+{
+	const double2 *p = reinterpret_cast<const double2 *>(rows + r);
+	const double2 a = p[0], b = p[1];
+	e = a.x; q = a.y; tq = b.x; tz = b.y;
+	t = rows[r].t;
+}
+
+DEVI void store_row(RowRec *rows, uint32_t r, double e, double q, double tq, double tz, double t)
+{
+	double2 *p = reinterpret_cast<double2 *>(rows + r);
+	p[0] = make_double2(e, q);
+	p[1] = make_double2(tq, tz);
+	rows[r].t = t;
+}
+
+// sequential correction of a column that lists some row more than once: the reference
+// corrects entry after entry, a repeated row seeing its own earlier update
+DEVI void v_corr_serial(const uint2 *col, uint32_t n, RowRec *rows, double mo, double so, double mu, double sig)
+{
+	for (uint32_t i = 0; i < n; ++i) {
+		const uint2 ent = col[i];
+		double e, q, tq, tz, t;
+		load_row(rows, ent.x, e, q, tq, tz, t);
+		v_corr(ent_x(ent), mo, so, mu, sig, e, q, tq, tz, t);
+		store_row(rows, ent.x, e, q, tq, tz, t);
+	}
+}
+
+// One workgroup per feature column of the level. Entries i = tid + u*BLOCK for u < R are
+// gathered once and kept in registers from the stats pass to the correction pass; longer
+// columns fall back to a second gather for the overflow entries.
+template <int BLOCK, int R>
+__global__ __launch_bounds__(BLOCK) void k_v_level_fused(LevelArgs a)
+{
+	__shared__ double lds[2 * (BLOCK / 64)];
+	const uint32_t j = a.feats[blockIdx.x];
+	const uint64_t cb = a.col_ptr[j];
+	const uint32_t n = (uint32_t)(a.col_ptr[j + 1] - cb);
+	const uint2 *col = a.csc + cb;
+	const double2 msj = a.ms[j];
+	const double mo = msj.x, so = msj.y;
+
+	uint32_t row[R];
+	float xv[R];
+	double re[R], rq[R], rtq[R], rtz[R], rt[R];
+#pragma unroll
+	for (int u = 0; u < R; ++u) {
+		const uint32_t i = threadIdx.x + u * BLOCK;
+		row[u] = 0; xv[u] = 0.f;
+		if (i < n) { const uint2 ent = col[i]; row[u] = ent.x; xv[u] = ent_x(ent); }
+	}
+#pragma unroll
+	for (int u = 0; u < R; ++u) {
+		const uint32_t i = threadIdx.x + u * BLOCK;
+		if (i < n) load_row(a.rows, row[u], re[u], rq[u], rtq[u], rtz[u], rt[u]);
+	}
+	double vm = 0.0, vs = 0.0;
+#pragma unroll
+	for (int u = 0; u < R; ++u) {
+		const uint32_t i = threadIdx.x + u * BLOCK;
+		if (i < n) v_stat(xv[u], re[u], rq[u], rtq[u], mo, so, vm, vs);
+	}
+	for (uint32_t i = threadIdx.x + R * BLOCK; i < n; i += BLOCK) {
+		const uint2 ent = col[i];
+		double e, q, tq, tz, t;
+		load_row(a.rows, ent.x, e, q, tq, tz, t);
+		v_stat(ent_x(ent), e, q, tq, mo, so, vm, vs);
+	}
+	block_sum2<BLOCK>(vm, vs, lds);
+
+	double mu, sig;
+	const double sv_g = a.hyp[(size_t)a.attr_group[j] * a.hyp_stride];
+	const bool go = v_post(vm, vs, sv_g, a.alpha, mo, so, mu, sig, a.counters, threadIdx.x == 0);
+	if (threadIdx.x == 0) a.ms[j] = make_double2(mu, sig);
+	if (!go) return;
+	if (a.dup[j]) {
+		__syncthreads();
+		if (threadIdx.x == 0) v_corr_serial(col, n, a.rows, mo, so, mu, sig);
+		return;
+	}
+#pragma unroll
+	for (int u = 0; u < R; ++u) {
+		const uint32_t i = threadIdx.x + u * BLOCK;
+		if (i < n) {
+			v_corr(xv[u], mo, so, mu, sig, re[u], rq[u], rtq[u], rtz[u], rt[u]);
+			store_row(a.rows, row[u], re[u], rq[u], rtq[u], rtz[u], rt[u]);
+		}
+	}
+	for (uint32_t i = threadIdx.x + R * BLOCK; i < n; i += BLOCK) {
+		const uint2 ent = col[i];
+		double e, q, tq, tz, t;
+		load_row(a.rows, ent.x, e, q, tq, tz, t);
+		v_corr(ent_x(ent), mo, so, mu, sig, e, q, tq, tz, t);
+		store_row(a.rows, ent.x, e, q, tq, tz, t);
+	}
+}
+
+// split form for the row-sharded multi-GPU mode: stats -> (all-reduce) -> correction
+template <int BLOCK>
+__global__ __launch_bounds__(BLOCK) void k_v_level_stats(LevelArgs a)
+{
+	__shared__ double lds[2 * (BLOCK / 64)];
+	const uint32_t j = a.feats[blockIdx.x];
+	const uint64_t cb = a.col_ptr[j];
+	const uint32_t n = (uint32_t)(a.col_ptr[j + 1] - cb);
+	const uint2 *col = a.csc + cb;
+	const double2 msj = a.ms[j];
+	double vm = 0.0, vs = 0.0;
+	for (uint32_t i = threadIdx.x; i < n; i += BLOCK) {
+		const uint2 ent = col[i];
+		double e, q, tq, tz, t;
+		load_row(a.rows, ent.x, e, q, tq, tz, t);
+		v_stat(ent_x(ent), e, q, tq, msj.x, msj.y, vm, vs);
+	}
+	block_sum2<BLOCK>(vm, vs, lds);
+	if (threadIdx.x == 0) a.stats[blockIdx.x] = make_double2(vm, vs);
+}
+
+template <int BLOCK>
+__global__ __launch_bounds__(BLOCK) void k_v_level_correct(LevelArgs a)
+{
+	const uint32_t j = a.feats[blockIdx.x];
+	const uint64_t cb = a.col_ptr[j];
+	const uint32_t n = (uint32_t)(a.col_ptr[j + 1] - cb);
+	const uint2 *col = a.csc + cb;
+	const double2 msj = a.ms[j];
+	const double2 st = a.stats[blockIdx.x];
+	double mu, sig;
+	const double sv_g = a.hyp[(size_t)a.attr_group[j] * a.hyp_stride];
+	const bool go = v_post(st.x, st.y, sv_g, a.alpha, msj.x, msj.y, mu, sig, a.counters, threadIdx.x == 0);
+	__syncthreads();
+	if (threadIdx.x == 0) a.ms[j] = make_double2(mu, sig);
+	if (!go) return;
+	if (a.dup[j]) {
+		if (threadIdx.x == 0) v_corr_serial(col, n, a.rows, msj.x, msj.y, mu, sig);
+		return;
+	}
+	for (uint32_t i = threadIdx.x; i < n; i += BLOCK) {
+		const uint2 ent = col[i];
+		double e, q, tq, tz, t;
+		load_row(a.rows, ent.x, e, q, tq, tz, t);
+		v_corr(ent_x(ent), msj.x, msj.y, mu, sig, e, q, tq, tz, t);
+		store_row(a.rows, ent.x, e, q, tq, tz, t);
+	}
+}
+
+// ------------------------------------------------------------------------------------
+// w sweep: update_w (fm_learn_vb.h:527-574)
+DEVI void w_stat(float x, double e, double mo, double &wm, double &ws)
+{
+	wm += x * (e + x * mo);
+	ws += x * x;   // fp32 product
+}
+
+DEVI bool w_post(double wm, double ws, double sw_g, double alpha, double mo, double so, double &mu,
+                 double &sig, uint32_t *counters, bool leader)
+{
+	sig = (double)1.0 / (sw_g + alpha * ws);
+	mu = sig * alpha * wm;
+	if (dnan(sig) || dinf(sig)) {
+		if (leader) atomicAdd(&counters[CNT_NAN_SIGMA_W], 1u);
+		sig = so;
+	}
+	if (dnan(mu)) {
+		if (leader) atomicAdd(&counters[CNT_NAN_MU_W], 1u);
+		mu = mo;
+		return false;
+	}
+	if (dinf(mu)) {
+		if (leader) atomicAdd(&counters[CNT_INF_MU_W], 1u);
+		mu = mo;
+		return false;
+	}
+	return true;
+}
+
+DEVI void w_corr(float x, double mo, double so, double mu, double sig, double &e, double &t)
+{
+	const double h = x;
+	e += h * (mo - mu);
+	t += h * h * (sig - so);
+}
+
+template <int BLOCK, int R>
+__global__ __launch_bounds__(BLOCK) void k_w_level_fused(LevelArgs a)
+{
+	__shared__ double lds[2 * (BLOCK / 64)];
+	const uint32_t j = a.feats[blockIdx.x];
+	const uint64_t cb = a.col_ptr[j];
+	const uint32_t n = (uint32_t)(a.col_ptr[j + 1] - cb);
+	const uint2 *col = a.csc + cb;
+	const double2 msj = a.ms[j];
+	const double mo = msj.x, so = msj.y;
+	uint32_t row[R];
+	float xv[R];
+	double re[R], rt[R];
+#pragma unroll
+	for (int u = 0; u < R; ++u) {
+		const uint32_t i = threadIdx.x + u * BLOCK;
+		row[u] = 0; xv[u] = 0.f;
+		if (i < n) { const uint2 ent = col[i]; row[u] = ent.x; xv[u] = ent_x(ent); }
+	}
+#pragma unroll
+	for (int u = 0; u < R; ++u) {
+		const uint32_t i = threadIdx.x + u * BLOCK;
+		if (i < n) { re[u] = a.rows[row[u]].e; rt[u] = a.rows[row[u]].t; }
+	}
+	double wm = 0.0, ws = 0.0;
+#pragma unroll
+	for (int u = 0; u < R; ++u) {
+		const uint32_t i = threadIdx.x + u * BLOCK;
+		if (i < n) w_stat(xv[u], re[u], mo, wm, ws);
+	}
+	for (uint32_t i = threadIdx.x + R * BLOCK; i < n; i += BLOCK) {
+		const uint2 ent = col[i];
+		w_stat(ent_x(ent), a.rows[ent.x].e, mo, wm, ws);
+	}
+	block_sum2<BLOCK>(wm, ws, lds);
+	double mu, sig;
+	const double sw_g = a.hyp[(size_t)a.attr_group[j] * a.hyp_stride];
+	const bool go = w_post(wm, ws, sw_g, a.alpha, mo, so, mu, sig, a.counters, threadIdx.x == 0);
+	if (threadIdx.x == 0) a.ms[j] = make_double2(mu, sig);
+	if (!go) return;
+	if (a.dup[j]) {
+		__syncthreads();
+		if (threadIdx.x == 0)
+			for (uint32_t i = 0; i < n; ++i) {
+				const uint2 ent = col[i];
+				double e = a.rows[ent.x].e, t = a.rows[ent.x].t;
+				w_corr(ent_x(ent), mo, so, mu, sig, e, t);
+				a.rows[ent.x].e = e; a.rows[ent.x].t = t;
+			}
+		return;
+	}
+#pragma unroll
+	for (int u = 0; u < R; ++u) {
+		const uint32_t i = threadIdx.x + u * BLOCK;
+		if (i < n) {
+			w_corr(xv[u], mo, so, mu, sig, re[u], rt[u]);
+			a.rows[row[u]].e = re[u];
+			a.rows[row[u]].t = rt[u];
+		}
+	}
+	for (uint32_t i = threadIdx.x + R * BLOCK; i < n; i += BLOCK) {
+		const uint2 ent = col[i];
+		double e = a.rows[ent.x].e, t = a.rows[ent.x].t;
+		w_corr(ent_x(ent), mo, so, mu, sig, e, t);
+		a.rows[ent.x].e = e; a.rows[ent.x].t = t;
+	}
+}
+
+template <int BLOCK>
+__global__ __launch_bounds__(BLOCK) void k_w_level_stats(LevelArgs a)
+{
+	__shared__ double lds[2 * (BLOCK / 64)];
+	const uint32_t j = a.feats[blockIdx.x];
+	const uint64_t cb = a.col_ptr[j];
+	const uint32_t n = (uint32_t)(a.col_ptr[j + 1] - cb);
+	const uint2 *col = a.csc + cb;
+	const double mo = a.ms[j].x;
+	double wm = 0.0, ws = 0.0;
+	for (uint32_t i = threadIdx.x; i < n; i += BLOCK) {
+		const uint2 ent = col[i];
+		w_stat(ent_x(ent), a.rows[ent.x].e, mo, wm, ws);
+	}
+	block_sum2<BLOCK>(wm, ws, lds);
+	if (threadIdx.x == 0) a.stats[blockIdx.x] = make_double2(wm, ws);
+}
+
+template <int BLOCK>
+__global__ __launch_bounds__(BLOCK) void k_w_level_correct(LevelArgs a)
+{
+	const uint32_t j = a.feats[blockIdx.x];
+	const uint64_t cb = a.col_ptr[j];
+	const uint32_t n = (uint32_t)(a.col_ptr[j + 1] - cb);
+	const uint2 *col = a.csc + cb;
+	const double2 msj = a.ms[j];
+	const double2 st = a.stats[blockIdx.x];
+	double mu, sig;
+	const double sw_g = a.hyp[(size_t)a.attr_group[j] * a.hyp_stride];
+	const bool go = w_post(st.x, st.y, sw_g, a.alpha, msj.x, msj.y, mu, sig, a.counters, threadIdx.x == 0);
+	__syncthreads();
+	if (threadIdx.x == 0) a.ms[j] = make_double2(mu, sig);
+	if (!go) return;
+	if (a.dup[j]) {
+		if (threadIdx.x == 0)
+			for (uint32_t i = 0; i < n; ++i) {
+				const uint2 ent = col[i];
+				double e = a.rows[ent.x].e, t = a.rows[ent.x].t;
+				w_corr(ent_x(ent), msj.x, msj.y, mu, sig, e, t);
+				a.rows[ent.x].e = e; a.rows[ent.x].t = t;
+			}
+		return;
+	}
+	for (uint32_t i = threadIdx.x; i < n; i += BLOCK) {
+		const uint2 ent = col[i];
+		double e = a.rows[ent.x].e, t = a.rows[ent.x].t;
+		w_corr(ent_x(ent), msj.x, msj.y, mu, sig, e, t);
+		a.rows[ent.x].e = e; a.rows[ent.x].t = t;
+	}
+}
+
+// ------------------------------------------------------------------------------------
+// q-cache of factor f: add_main_q (fm_learn_vb.h:354-381) after zeroing (:411-415).
+// Row-parallel over the feature-sorted CSR: each row sums its entries in ascending
+// feature order, exactly the order the reference's column loop adds them in.
+__global__ __launch_bounds__(256) void k_qcache(const uint64_t *__restrict__ row_ptr, const uint2 *__restrict__ csr,
+                                                 const double2 *__restrict__ ms_f, RowRec *__restrict__ rows,
+                                                 uint32_t n)
+{
+	const uint32_t r = blockIdx.x * 256u + threadIdx.x;
+	if (r >= n) return;
+	const uint64_t b = row_ptr[r], e = row_ptr[r + 1];
+	double q = 0.0, tq = 0.0, tz = 0.0;
+	for (uint64_t p = b; p < e; ++p) {
+		const uint2 ent = csr[p];
+		const float x = ent_x(ent);
+		const double2 m = ms_f[ent.x];
+		q += m.x * x;
+		tq += m.y * x * x;
+		tz += m.x * m.x * x * x;
+	}
+	rows[r].q = q;
+	reinterpret_cast<double2 *>(rows + r)[1] = make_double2(tq, tz);
+}
+
+// predict_data_and_write_to_eterms for one data set (fm_learn_vb.h:70-203), row-parallel.
+__global__ __launch_bounds__(256) void k_predict_e(const uint64_t *__restrict__ row_ptr, const uint2 *__restrict__ csr,
+                                                    const double2 *__restrict__ ms_v, const double2 *__restrict__ ms_w,
+                                                    uint32_t D, int k, int k1, int k0, double mu0,
+                                                    double *__restrict__ out, uint32_t n)
+{
+	const uint32_t r = blockIdx.x * 256u + threadIdx.x;
+	if (r >= n) return;
+	const uint64_t b = row_ptr[r], en = row_ptr[r + 1];
+	double e = 0.0;
+	for (int f = 0; f < k; ++f) {                          // (1) :93-133
+		const double2 *m = ms_v + (size_t)f * D;
+		double q = 0.0;
+		for (uint64_t p = b; p < en; ++p) { const uint2 ent = csr[p]; q += m[ent.x].x * ent_x(ent); }
+		e += 0.5 * q * q;
+	}
+	double q = 0.0;
+	for (int f = 0; f < k; ++f) {                          // (2) :136-163
+		const double2 *m = ms_v + (size_t)f * D;
+		for (uint64_t p = b; p < en; ++p) {
+			const uint2 ent = csr[p];
+			const double v = m[ent.x].x;
+			const float x = ent_x(ent);
+			q -= 0.5 * v * v * x * x;
+		}
+	}
+	if (k1)                                                // (3) :166-188
+		for (uint64_t p = b; p < en; ++p) { const uint2 ent = csr[p]; q += ms_w[ent.x].x * ent_x(ent); }
+	e = e + q;                                             // merge :190-202
+	if (k0) e += mu0;
+	out[r] = e;
+}
+
+// predict_t_and_write_to_qterms (fm_learn_vb.h:207-312), row-parallel; writes rows[].t
+__global__ __launch_bounds__(256) void k_predict_t(const uint64_t *__restrict__ row_ptr, const uint2 *__restrict__ csr,
+                                                    const double2 *__restrict__ ms_v, const double2 *__restrict__ ms_w,
+                                                    uint32_t D, int k, int k1, int k0, double s0d,
+                                                    RowRec *__restrict__ rows, uint32_t n)
+{
+	const uint32_t r = blockIdx.x * 256u + threadIdx.x;
+	if (r >= n) return;
+	const uint64_t b = row_ptr[r], en = row_ptr[r + 1];
+	double t = 0.0;
+	for (int f = 0; f < k; ++f) {                          // (1) :222-254
+		const double2 *m = ms_v + (size_t)f * D;
+		double q = 0.0, z = 0.0;
+		for (uint64_t p = b; p < en; ++p) {
+			const uint2 ent = csr[p];
+			const double2 vm = m[ent.x];
+			const float x = ent_x(ent);
+			q += vm.x * x * vm.x * x;
+			z += vm.y * x * x;
+		}
+		t += (0.5 * z * z + z * q);
+	}
+	double q = 0.0;
+	for (int f = 0; f < k; ++f) {                          // (2) :257-281
+		const double2 *m = ms_v + (size_t)f * D;
+		for (uint64_t p = b; p < en; ++p) {
+			const uint2 ent = csr[p];
+			const double2 vm = m[ent.x];
+			const float x = ent_x(ent);
+			q -= (vm.x * vm.x * x * x * x * x * vm.y + 0.5 * x * x * x * x * vm.y * vm.y);
+		}
+	}
+	if (k1)                                                // (3) :284-301
+		for (uint64_t p = b; p < en; ++p) {
+			const uint2 ent = csr[p];
+			const float x = ent_x(ent);
+			q += ms_w[ent.x].y * x * x;
+		}
+	t = t + q;                                             // :304-311
+	if (k0) t += s0d;
+	rows[r].t = t;
+}
+
+// e = y - yhat (fm_learn_vb_simultaneous.h:42-44)
+__global__ void k_residual_init(RowRec *rows, const double *yhat, const float *target, uint32_t n)
+{
+	const uint32_t r = blockIdx.x * 256u + threadIdx.x;
+	if (r < n) rows[r].e = target[r] - yhat[r];
+}
+
+template <int BLOCK>
+__global__ __launch_bounds__(BLOCK) void k_row_sums(const RowRec *rows, uint32_t n, int mode, double mu0, double *out)
+{
+	__shared__ double lds[BLOCK / 64];
+	double s = 0.0;
+	for (uint32_t r = blockIdx.x * BLOCK + threadIdx.x; r < n; r += gridDim.x * BLOCK) {
+		const double e = rows[r].e;
+		if (mode == 0) s += e + mu0;                       // update_w0 (fm_learn_vb.h:512-514)
+		else s += e * e + rows[r].t;                       // alpha / free energy (:450-452, :659-661)
+	}
+	s = block_sum1<BLOCK>(s, lds);
+	if (threadIdx.x == 0) out[blockIdx.x] = s;
+}
+
+__global__ void k_w0_apply(RowRec *rows, uint32_t n, double de, double dt)
+{
+	// fm_learn_vb.h:517-520
+	const uint32_t r = blockIdx.x * 256u + threadIdx.x;
+	if (r < n) { rows[r].e = rows[r].e + de; rows[r].t = rows[r].t + dt; }
+}
+
+// std::min(max_target, p) then std::max(min_target, p)
+DEVI double clip(double p, double mn, double mx)
+{
+	p = (p < mx) ? p : mx;
+	p = (mn < p) ? p : mn;
+	return p;
+}
+
+template <int BLOCK>
+__global__ __launch_bounds__(BLOCK) void k_test_metrics(const double *e_test, const float *target, uint32_t n, double mn,
+                                                        double mx, double *pred, double *out)
+{
+	__shared__ double lds[2 * (BLOCK / 64)];
+	double s2 = 0.0, s1 = 0.0;
+	for (uint32_t c = blockIdx.x * BLOCK + threadIdx.x; c < n; c += gridDim.x * BLOCK) {
+		double p = clip(e_test[c], mn, mx);                // fm_learn_vb_simultaneous.h:143-150
+		pred[c] = p;
+		p = clip(p * 1.0, mn, mx);                         // _evaluate (:266-274)
+		const double err = p - target[c];
+		s2 += err * err;
+		s1 += fabs(err);
+	}
+	block_sum2<BLOCK>(s2, s1, lds);
+	if (threadIdx.x == 0) { out[2 * blockIdx.x] = s2; out[2 * blockIdx.x + 1] = s1; }
+}
+
+template <int BLOCK>
+__global__ __launch_bounds__(BLOCK) void k_train_quirk(const RowRec *rows, uint32_t n, double mn, double mx, double *out)
+{
+	__shared__ double lds[BLOCK / 64];
+	double s = 0.0;
+	for (uint32_t c = blockIdx.x * BLOCK + threadIdx.x; c < n; c += gridDim.x * BLOCK) {
+		const double p = clip(rows[c].e, mn, mx);          // :153-161
+		s += p * p;
+	}
+	s = block_sum1<BLOCK>(s, lds);
+	if (threadIdx.x == 0) out[blockIdx.x] = s;
+}
+
+// hyper-parameter sums (mode 0, fm_learn_vb.h:477-497: mu^2 + sigma) and free-energy terms
+// (mode 1, :665-676) over one chunk of attributes of one (factor, group) segment.
+template <int BLOCK>
+__global__ __launch_bounds__(BLOCK) void k_param_sums(const double2 *ms_w, const double2 *ms_v, const uint32_t *perm,
+                                                      uint32_t D, const vbk::Chunk *chunks, int mode,
+                                                      const double *hyp_w, const double *hyp_v, int k, double *out)
+{
+	__shared__ double lds[BLOCK / 64];
+	const vbk::Chunk c = chunks[blockIdx.x];
+	const double2 *ms = c.f < 0 ? ms_w : ms_v + (size_t)c.f * D;
+	const double hs = mode == 0 ? 0.0 : (c.f < 0 ? hyp_w[c.g] : hyp_v[(size_t)c.g * k + c.f]);
+	double s = 0.0;
+	for (uint32_t i = c.begin + threadIdx.x; i < c.end; i += BLOCK) {
+		const double2 m = ms[perm[i]];
+		if (mode == 0) s += m.x * m.x + m.y;
+		else s += -0.5 * hs * (m.x * m.x + m.y) + 0.5 * log(m.y * hs) + .5;
+	}
+	s = block_sum1<BLOCK>(s, lds);
+	if (threadIdx.x == 0) out[blockIdx.x] = s;
+}
+
+// ------------------------------------------------------------------------------------
+// dependency levels: relax level[b] >= level[a] + 1 over consecutive distinct features
+// a < b of every row until nothing changes (least fixed point = longest-path levels).
+__global__ void k_level_init(uint32_t *level, uint32_t nf)
+{
+	const uint32_t j = blockIdx.x * 256u + threadIdx.x;
+	if (j < nf) level[j] = 1;
+}
+
+__global__ void k_level_relax(const uint64_t *row_ptr, const uint2 *csr, uint32_t n, uint32_t *level, uint32_t *changed)
+{
+	const uint32_t r = blockIdx.x * 256u + threadIdx.x;
+	if (r >= n) return;
+	const uint64_t b = row_ptr[r], e = row_ptr[r + 1];
+	if (e - b < 2) return;
+	uint32_t prev = csr[b].x;
+	uint32_t lp = __hip_atomic_load(&level[prev], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+	bool ch = false;
+	for (uint64_t p = b + 1; p < e; ++p) {
+		const uint32_t cur = csr[p].x;
+		if (cur == prev) continue;
+		const uint32_t old = atomicMax(&level[cur], lp + 1);
+		if (old < lp + 1) { ch = true; lp = lp + 1; } else lp = old;
+		prev = cur;
+	}
+	if (ch) atomicOr(changed, 1u);
+}
+
+__global__ void k_mark_dups(const uint64_t *row_ptr, const uint2 *csr, uint32_t n, uint8_t *dup)
+{
+	const uint32_t r = blockIdx.x * 256u + threadIdx.x;
+	if (r >= n) return;
+	const uint64_t b = row_ptr[r], e = row_ptr[r + 1];
+	for (uint64_t p = b + 1; p < e; ++p)
+		if (csr[p].x == csr[p - 1].x) dup[csr[p].x] = 1;
+}
+
+// ------------------------------------------------------------------------------------
+// field-structured synthetic generator (tests/synth.py is the specification)
+DEVI uint64_t splitmix64(uint64_t z)
+{
+	z += 0x9E3779B97F4A7C15ull;
+	z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+	z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+	return z ^ (z >> 31);
+}
+DEVI uint64_t hstream(uint64_t seed, uint64_t stream, uint64_t i)
+{
+	return splitmix64(seed * 0x9E3779B97F4A7C15ull + stream * 0xD1B54A32D192ED03ull + i);
+}
+
+__global__ void k_synth_entries(uint32_t n, uint32_t F, uint32_t S, uint64_t seed, int xmode, uint2 *csr)
+{
+	const uint64_t idx = (uint64_t)blockIdx.x * 256u + threadIdx.x;
+	if (idx >= (uint64_t)n * F) return;
+	const uint32_t fld = (uint32_t)(idx % F);
+	const uint32_t feat = fld * S + (uint32_t)(hstream(seed, 1, idx) % S);
+	float x = 1.0f;
+	if (xmode) x = 0.5f + (float)(hstream(seed, 2, idx) >> 40) * 0x1p-24f;
+	csr[idx] = make_uint2(feat, __float_as_uint(x));
+}
+
+__global__ void k_synth_rows(uint32_t n, uint32_t F, uint64_t seed, const uint2 *csr, uint64_t *row_ptr, float *target)
+{
+	const uint32_t r = blockIdx.x * 256u + threadIdx.x;
+	if (r > n) return;
+	row_ptr[r] = (uint64_t)r * F;
+	if (r == n) return;
+	double s = 0.0;
+	for (uint32_t f = 0; f < F; ++f) {
+		const uint32_t j = csr[(uint64_t)r * F + f].x;
+		s = s + ((double)(hstream(seed, 3, j) >> 11) * 0x1p-53 - 0.5);
+	}
+	const double noise = (double)(hstream(seed, 4, r) >> 11) * 0x1p-53 - 0.5;
+	double y = rint(3.0 + s + 1.5 * noise);
+	y = y < 1.0 ? 1.0 : (y > 5.0 ? 5.0 : y);
+	target[r] = (float)y;
+}
+
+__global__ void k_synth_field_keys(const uint2 *csr, uint32_t n, uint32_t F, uint32_t S, uint32_t field, uint32_t *keys,
+                                   uint32_t *vals)
+{
+	const uint32_t r = blockIdx.x * 256u + threadIdx.x;
+	if (r >= n) return;
+	keys[r] = csr[(uint64_t)r * F + field].x - field * S;
+	vals[r] = r;
+}
+
+__global__ void k_synth_field_scatter(const uint32_t *sorted_rows, const uint2 *csr, uint32_t n, uint32_t F, uint32_t field,
+                                      uint2 *out)
+{
+	const uint32_t p = blockIdx.x * 256u + threadIdx.x;
+	if (p >= n) return;
+	const uint32_t r = sorted_rows[p];
+	out[p] = make_uint2(r, csr[(uint64_t)r * F + field].y);
+}
+
+__global__ void k_count_features(const uint2 *csr, uint64_t nnz, unsigned long long *counts)
+{
+	const uint64_t i = (uint64_t)blockIdx.x * 256u + threadIdx.x;
+	if (i < nnz) atomicAdd(&counts[csr[i].x], 1ull);
+}
+
+// {0.1 * N(0,1), .02}: Box-Muller on two splitmix64 uniforms in (0, 1]
+__global__ void k_init_normal_pairs(double2 *ms, size_t n, uint64_t seed, uint64_t stream)
+{
+	const size_t i = (size_t)blockIdx.x * 256u + threadIdx.x;
+	if (i >= n) return;
+	const double u1 = ((double)(hstream(seed, stream, 2 * i) >> 11) + 1.0) * 0x1p-53;
+	const double u2 = (double)(hstream(seed, stream, 2 * i + 1) >> 11) * 0x1p-53;
+	const double z = sqrt(-2.0 * log(u1)) * cos(6.283185307179586 * u2);
+	ms[i] = make_double2(0.1 * z, .02);
+}
+
+__global__ void k_pack(const double *a, const double *b, double2 *out, size_t n)
+{
+	const size_t i = (size_t)blockIdx.x * 256u + threadIdx.x;
+	if (i < n) out[i] = make_double2(a[i], b[i]);
+}
+
+__global__ void k_unpack(const double2 *in, double *a, double *b, size_t n)
+{
+	const size_t i = (size_t)blockIdx.x * 256u + threadIdx.x;
+	if (i < n) { a[i] = in[i].x; b[i] = in[i].y; }
+}
+
+inline unsigned grid_for(uint64_t n, unsigned block = 256) { return (unsigned)((n + block - 1) / block); }
+
+}  // namespace
+
+// ------------------------------------------------------------------------------------
+namespace vbk {
+
+// Column-length-adaptive launch: one wave per column for short levels, four waves for
+// longer ones (average entries per column of the level decides).
+hipError_t v_level_fused(const LevelArgs &a, hipStream_t s)
+{
+	if (a.nfeat == 0) return hipSuccess;
+	k_v_level_fused<256, 4><<<a.nfeat, 256, 0, s>>>(a);
+	return hipGetLastError();
+}
+hipError_t w_level_fused(const LevelArgs &a, hipStream_t s)
+{
+	if (a.nfeat == 0) return hipSuccess;
+	k_w_level_fused<256, 4><<<a.nfeat, 256, 0, s>>>(a);
+	return hipGetLastError();
+}
+hipError_t v_level_stats(const LevelArgs &a, hipStream_t s)
+{
+	if (a.nfeat == 0) return hipSuccess;
+	k_v_level_stats<256><<<a.nfeat, 256, 0, s>>>(a);
+	return hipGetLastError();
+}
+hipError_t v_level_correct(const LevelArgs &a, hipStream_t s)
+{
+	if (a.nfeat == 0) return hipSuccess;
+	k_v_level_correct<256><<<a.nfeat, 256, 0, s>>>(a);
+	return hipGetLastError();
+}
+hipError_t w_level_stats(const LevelArgs &a, hipStream_t s)
+{
+	if (a.nfeat == 0) return hipSuccess;
+	k_w_level_stats<256><<<a.nfeat, 256, 0, s>>>(a);
+	return hipGetLastError();
+}
+hipError_t w_level_correct(const LevelArgs &a, hipStream_t s)
+{
+	if (a.nfeat == 0) return hipSuccess;
+	k_w_level_correct<256><<<a.nfeat, 256, 0, s>>>(a);
+	return hipGetLastError();
+}
+
+hipError_t qcache(const uint64_t *row_ptr, const uint2 *csr, const double2 *ms_f, RowRec *rows, uint32_t n, hipStream_t s)
+{
+	if (n == 0) return hipSuccess;
+	k_qcache<<<grid_for(n), 256, 0, s>>>(row_ptr, csr, ms_f, rows, n);
+	return hipGetLastError();
+}
+
+hipError_t predict_e(const uint64_t *row_ptr, const uint2 *csr, const double2 *ms_v, const double2 *ms_w, uint32_t D,
+                     int k, int k1, int k0, double mu0, double *out, uint32_t n, hipStream_t s)
+{
+	if (n == 0) return hipSuccess;
+	k_predict_e<<<grid_for(n), 256, 0, s>>>(row_ptr, csr, ms_v, ms_w, D, k, k1, k0, mu0, out, n);
+	return hipGetLastError();
+}
+
+hipError_t predict_t(const uint64_t *row_ptr, const uint2 *csr, const double2 *ms_v, const double2 *ms_w, uint32_t D,
+                     int k, int k1, int k0, double s0d, RowRec *rows, uint32_t n, hipStream_t s)
+{
+	if (n == 0) return hipSuccess;
+	k_predict_t<<<grid_for(n), 256, 0, s>>>(row_ptr, csr, ms_v, ms_w, D, k, k1, k0, s0d, rows, n);
+	return hipGetLastError();
+}
+
+hipError_t residual_init(RowRec *rows, const double *yhat, const float *target, uint32_t n, hipStream_t s)
+{
+	if (n == 0) return hipSuccess;
+	k_residual_init<<<grid_for(n), 256, 0, s>>>(rows, yhat, target, n);
+	return hipGetLastError();
+}
+
+hipError_t row_sums(const RowRec *rows, uint32_t n, int mode, double mu0, double *out, uint32_t nblocks, hipStream_t s)
+{
+	k_row_sums<256><<<nblocks, 256, 0, s>>>(rows, n, mode, mu0, out);
+	return hipGetLastError();
+}
+
+hipError_t w0_apply(RowRec *rows, uint32_t n, double de, double dt, hipStream_t s)
+{
+	if (n == 0) return hipSuccess;
+	k_w0_apply<<<grid_for(n), 256, 0, s>>>(rows, n, de, dt);
+	return hipGetLastError();
+}
+
+hipError_t test_metrics(const double *e_test, const float *target, uint32_t n, double mn, double mx, double *pred,
+                        double *out, uint32_t nblocks, hipStream_t s)
+{
+	k_test_metrics<256><<<nblocks, 256, 0, s>>>(e_test, target, n, mn, mx, pred, out);
+	return hipGetLastError();
+}
+
+hipError_t train_quirk(const RowRec *rows, uint32_t n, double mn, double mx, double *out, uint32_t nblocks, hipStream_t s)
+{
+	k_train_quirk<256><<<nblocks, 256, 0, s>>>(rows, n, mn, mx, out);
+	return hipGetLastError();
+}
+
+hipError_t param_sums(const double2 *ms_w, const double2 *ms_v, const uint32_t *perm, uint32_t D, const Chunk *chunks,
+                      uint32_t nchunks, int mode, const double *hyp_w, const double *hyp_v, int k, double *out,
+                      hipStream_t s)
+{
+	if (nchunks == 0) return hipSuccess;
+	k_param_sums<256><<<nchunks, 256, 0, s>>>(ms_w, ms_v, perm, D, chunks, mode, hyp_w, hyp_v, k, out);
+	return hipGetLastError();
+}
+
+hipError_t level_init(uint32_t *level, uint32_t nf, hipStream_t s)
+{
+	if (nf == 0) return hipSuccess;
+	k_level_init<<<grid_for(nf), 256, 0, s>>>(level, nf);
+	return hipGetLastError();
+}
+
+hipError_t level_relax(const uint64_t *row_ptr, const uint2 *csr, uint32_t n, uint32_t nf, uint32_t *level,
+                       uint32_t *changed, hipStream_t s)
+{
+	(void)nf;
+	if (n == 0) return hipSuccess;
+	k_level_relax<<<grid_for(n), 256, 0, s>>>(row_ptr, csr, n, level, changed);
+	return hipGetLastError();
+}
+
+hipError_t mark_dups(const uint64_t *row_ptr, const uint2 *csr, uint32_t n, uint8_t *dup, hipStream_t s)
+{
+	if (n == 0) return hipSuccess;
+	k_mark_dups<<<grid_for(n), 256, 0, s>>>(row_ptr, csr, n, dup);
+	return hipGetLastError();
+}
+
+hipError_t synth_csr(uint32_t n, uint32_t F, uint32_t S, uint64_t seed, int xmode, uint64_t *row_ptr, uint2 *csr,
+                     float *target, hipStream_t s)
+{
+	const uint64_t nnz = (uint64_t)n * F;
+	if (nnz) k_synth_entries<<<grid_for(nnz), 256, 0, s>>>(n, F, S, seed, xmode, csr);
+	k_synth_rows<<<grid_for((uint64_t)n + 1), 256, 0, s>>>(n, F, seed, csr, row_ptr, target);
+	return hipGetLastError();
+}
+
+hipError_t synth_field_keys(const uint2 *csr, uint32_t n, uint32_t F, uint32_t S, uint32_t field, uint32_t *keys,
+                            uint32_t *vals, hipStream_t s)
+{
+	if (n == 0) return hipSuccess;
+	k_synth_field_keys<<<grid_for(n), 256, 0, s>>>(csr, n, F, S, field, keys, vals);
+	return hipGetLastError();
+}
+
+hipError_t synth_field_scatter(const uint32_t *sorted_rows, const uint2 *csr, uint32_t n, uint32_t F, uint32_t field,
+                               uint2 *out, hipStream_t s)
+{
+	if (n == 0) return hipSuccess;
+	k_synth_field_scatter<<<grid_for(n), 256, 0, s>>>(sorted_rows, csr, n, F, field, out);
+	return hipGetLastError();
+}
+
+hipError_t count_features(const uint2 *csr, uint64_t nnz, uint64_t *counts, hipStream_t s)
+{
+	if (nnz == 0) return hipSuccess;
+	k_count_features<<<grid_for(nnz), 256, 0, s>>>(csr, nnz, reinterpret_cast<unsigned long long *>(counts));
+	return hipGetLastError();
+}
+
+hipError_t sort_pairs_u32(void *tmp, size_t *tmp_bytes, const uint32_t *ki, uint32_t *ko, const uint32_t *vi,
+                          uint32_t *vo, size_t n, int bits, hipStream_t s)
+{
+	return rocprim::radix_sort_pairs(tmp, *tmp_bytes, ki, ko, vi, vo, n, 0, bits, s);
+}
+
+hipError_t exclusive_scan_u64(void *tmp, size_t *tmp_bytes, const uint64_t *in, uint64_t *out, size_t n, hipStream_t s)
+{
+	return rocprim::exclusive_scan(tmp, *tmp_bytes, in, out, (uint64_t)0, n, rocprim::plus<uint64_t>(), s);
+}
+
+hipError_t init_normal_pairs(double2 *ms, size_t n, uint64_t seed, uint64_t stream, hipStream_t s)
+{
+	if (n == 0) return hipSuccess;
+	k_init_normal_pairs<<<grid_for(n), 256, 0, s>>>(ms, n, seed, stream);
+	return hipGetLastError();
+}
+
+hipError_t pack_pairs(const double *a, const double *b, double2 *out, size_t n, hipStream_t s)
+{
+	if (n == 0) return hipSuccess;
+	k_pack<<<grid_for(n), 256, 0, s>>>(a, b, out, n);
+	return hipGetLastError();
+}
+
+hipError_t unpack_pairs(const double2 *in, double *a, double *b, size_t n, hipStream_t s)
+{
+	if (n == 0) return hipSuccess;
+	k_unpack<<<grid_for(n), 256, 0, s>>>(in, a, b, n);
+	return hipGetLastError();
+}
+
+}  // namespace vbk

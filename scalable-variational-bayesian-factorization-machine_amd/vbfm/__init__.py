@@ -1,0 +1,411 @@
+"""vbfm -- Python host side of libvbfm.so (the MI355X VB factorization machine).
+
+Mirrors the reference's learner interface for `-method vb` so that driver code reads like
+the reference's main() (src/libfm/libfm.cpp:137-511):
+
+    train = DataSubset.load("train.libfm")            # Data::load          (Data.h:106-283)
+    test = DataSubset.load("test.libfm")
+    D = num_all_attribute(train, test)                 # libfm.cpp:215
+    fml = FMLearnVB(k0=1, k1=1, num_factor=8, num_attribute=D,
+                    min_target=train.min_target, max_target=train.max_target)
+    fml.init(seed=42, init_stdev=0.1)                  # fm.init + fm_learn_vb::init draws
+    for it, st in enumerate(fml.learn(train, test, num_iter=20)):   # _learn
+        print(it, st.rmse, st.free_energy)
+
+Every numeric step runs in libvbfm.so on the GPU. There is no CPU fallback: without the
+built library (make -C scalable-variational-bayesian-factorization-machine_amd) or without
+a HIP device every call raises.
+"""
+import ctypes as C
+import os
+
+import numpy as np
+
+_PKG = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB_PATH = os.environ.get("VBFM_LIB", os.path.join(_PKG, "lib", "libvbfm.so"))
+
+P_u32, P_u64, P_f32, P_f64, P_u8 = (C.POINTER(C.c_uint32), C.POINTER(C.c_uint64), C.POINTER(C.c_float),
+                                    C.POINTER(C.c_double), C.POINTER(C.c_uint8))
+
+
+class VbfmError(RuntimeError):
+    pass
+
+
+class Entry(C.Structure):
+    _fields_ = [("id", C.c_uint32), ("value", C.c_float)]
+
+
+ENTRY_DTYPE = np.dtype([("id", "<u4"), ("value", "<f4")])
+
+
+class Csc(C.Structure):
+    _fields_ = [("num_rows", C.c_uint32), ("num_feature", C.c_uint32), ("nnz", C.c_uint64),
+                ("col_ptr", P_u64), ("col_ent", C.c_void_p), ("target", P_f32)]
+
+
+class Config(C.Structure):
+    _fields_ = [("k0", C.c_int32), ("k1", C.c_int32), ("num_factor", C.c_int32),
+                ("num_attribute", C.c_uint32), ("num_attr_groups", C.c_uint32), ("attr_group", P_u32),
+                ("min_target", C.c_float), ("max_target", C.c_float), ("device", C.c_int32),
+                ("task", C.c_int32)]
+
+
+class Params(C.Structure):
+    _fields_ = [("mu_w", P_f64), ("sigma_w", P_f64), ("mu_v", P_f64), ("sigma_v", P_f64),
+                ("hyp_sigma_w", P_f64), ("hyp_sigma_v", P_f64), ("alpha", C.c_double),
+                ("sigma_0", C.c_double), ("mu_0_dash", C.c_double), ("sigma_0_dash", C.c_double)]
+
+
+class IterStats(C.Structure):
+    _fields_ = [("rmse", C.c_double), ("mae", C.c_double), ("train_quirk", C.c_double),
+                ("free_energy", C.c_double), ("free_energy_valid", C.c_int32), ("num_levels", C.c_int32),
+                ("alpha", C.c_double), ("sigma_0", C.c_double), ("mu_0_dash", C.c_double),
+                ("sigma_0_dash", C.c_double),
+                ("nan_mu_w", C.c_uint32), ("nan_sigma_w", C.c_uint32), ("inf_mu_w", C.c_uint32),
+                ("nan_mu_v", C.c_uint32), ("nan_sigma_v", C.c_uint32), ("inf_mu_v", C.c_uint32),
+                ("nan_alpha", C.c_uint32), ("inf_alpha", C.c_uint32),
+                ("ms_w0", C.c_double), ("ms_w", C.c_double), ("ms_qcache", C.c_double), ("ms_v", C.c_double),
+                ("ms_hyper", C.c_double), ("ms_test", C.c_double), ("ms_total", C.c_double),
+                ("ms_vlevel_kernels", C.c_double), ("ms_wlevel_kernels", C.c_double),
+                ("ms_qcache_kernels", C.c_double), ("n_vlevel_launches", C.c_int32),
+                ("n_wlevel_launches", C.c_int32), ("n_qcache_launches", C.c_int32), ("nnz_train", C.c_uint64)]
+
+    def as_dict(self):
+        return {k: getattr(self, k) for k, _ in self._fields_}
+
+
+class HostData(C.Structure):
+    _fields_ = [("num_rows", C.c_uint32), ("num_feature", C.c_uint32), ("nnz", C.c_uint64),
+                ("min_target", C.c_float), ("max_target", C.c_float), ("target", P_f32),
+                ("row_ptr", P_u64), ("row_ent", C.c_void_p), ("col_ptr", P_u64), ("col_ent", C.c_void_p)]
+
+
+# every symbol include/vbfm.h declares (checked by tests/test_capi_cpu.py)
+EXPORTS = ["vbfm_abi_version", "vbfm_last_error", "vbfm_create", "vbfm_destroy", "vbfm_set_train",
+           "vbfm_set_test", "vbfm_synth_generate", "vbfm_get_csc", "vbfm_get_shape", "vbfm_get_levels",
+           "vbfm_set_params", "vbfm_get_params", "vbfm_init_params_device", "vbfm_init_caches", "vbfm_iterate", "vbfm_get_test_pred",
+           "vbfm_step_w0", "vbfm_step_w", "vbfm_step_qcache", "vbfm_step_v", "vbfm_step_hyper",
+           "vbfm_free_energy", "vbfm_get_rows", "vbfm_get_test_e", "vbfm_factor_sweep", "vbfm_set_profiling",
+           "vbfm_comm_unique_id", "vbfm_comm_init", "vbfm_load_data", "vbfm_free_host_data",
+           "vbfm_init_params_host"]
+
+_lib = None
+
+
+def lib():
+    """Load libvbfm.so (raises if it is not built: there is no fallback path)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise VbfmError("libvbfm.so not built (expected %s); run `make -C %s`" % (LIB_PATH, _PKG))
+        L = C.CDLL(LIB_PATH)
+        V = C.c_void_p
+        L.vbfm_last_error.argtypes = [V]
+        L.vbfm_last_error.restype = C.c_char_p
+        L.vbfm_create.argtypes = [C.POINTER(V), C.POINTER(Config)]
+        L.vbfm_destroy.argtypes = [V]
+        L.vbfm_destroy.restype = None
+        L.vbfm_set_train.argtypes = [V, C.POINTER(Csc)]
+        L.vbfm_set_test.argtypes = [V, C.POINTER(Csc)]
+        L.vbfm_synth_generate.argtypes = [V, C.c_int32, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint64, C.c_int32]
+        L.vbfm_get_csc.argtypes = [V, C.c_int32, P_u64, V, P_f32]
+        L.vbfm_get_shape.argtypes = [V, C.c_int32, P_u32, P_u32, P_u64]
+        L.vbfm_get_levels.argtypes = [V, P_u32, P_u32]
+        L.vbfm_set_params.argtypes = [V, C.POINTER(Params)]
+        L.vbfm_get_params.argtypes = [V, C.POINTER(Params)]
+        L.vbfm_init_caches.argtypes = [V]
+        L.vbfm_init_params_device.argtypes = [V, C.c_uint64]
+        L.vbfm_iterate.argtypes = [V, C.POINTER(IterStats)]
+        L.vbfm_get_test_pred.argtypes = [V, P_f64]
+        for fn in ("vbfm_step_w0", "vbfm_step_w"):
+            getattr(L, fn).argtypes = [V]
+        L.vbfm_step_qcache.argtypes = [V, C.c_int32]
+        L.vbfm_step_v.argtypes = [V, C.c_int32]
+        L.vbfm_step_hyper.argtypes = [V, C.POINTER(C.c_int32)]
+        L.vbfm_free_energy.argtypes = [V, P_f64]
+        L.vbfm_get_rows.argtypes = [V, P_f64, P_f64, P_f64, P_f64, P_f64]
+        L.vbfm_get_test_e.argtypes = [V, P_f64]
+        L.vbfm_factor_sweep.argtypes = [V, P_f64]
+        L.vbfm_set_profiling.argtypes = [V, C.c_int32]
+        L.vbfm_comm_unique_id.argtypes = [C.POINTER(C.c_uint8)]
+        L.vbfm_comm_init.argtypes = [V, C.c_int32, C.c_int32, C.POINTER(C.c_uint8)]
+        L.vbfm_load_data.argtypes = [C.c_char_p, C.POINTER(HostData)]
+        L.vbfm_free_host_data.argtypes = [C.POINTER(HostData)]
+        L.vbfm_free_host_data.restype = None
+        L.vbfm_init_params_host.argtypes = [C.c_uint32, C.c_double, C.c_int32, C.c_uint32, C.c_uint32,
+                                            C.POINTER(Params), P_f64, P_f64]
+        _lib = L
+    return _lib
+
+
+def _check(rc, ctx=None):
+    if rc != 0:
+        msg = lib().vbfm_last_error(ctx)
+        raise VbfmError(msg.decode() if msg else "libvbfm error %d" % rc)
+
+
+def _ptr(a, typ):
+    return a.ctypes.data_as(typ) if a is not None else None
+
+
+def _copy(ptr, n, dtype):
+    dtype = np.dtype(dtype)
+    if n == 0:
+        return np.zeros(0, dtype=dtype)
+    addr = ptr if isinstance(ptr, int) else C.cast(ptr, C.c_void_p).value
+    buf = (C.c_char * (n * dtype.itemsize)).from_address(addr)
+    return np.frombuffer(buf, dtype=dtype).copy()
+
+
+class DataSubset:
+    """A data set as the learner sees it: transposed copy (CSC) + targets (Data.h:73-104)."""
+
+    def __init__(self, col_ptr, col_ent, target, num_feature=None, row_ptr=None, row_ent=None):
+        self.col_ptr = np.ascontiguousarray(col_ptr, dtype=np.uint64)
+        self.col_ent = np.ascontiguousarray(col_ent, dtype=ENTRY_DTYPE)
+        self.target = np.ascontiguousarray(target, dtype=np.float32)
+        self.num_feature = int(len(self.col_ptr) - 1 if num_feature is None else num_feature)
+        self.num_cases = int(len(self.target))
+        self.row_ptr, self.row_ent = row_ptr, row_ent
+        # Data.h:161-166 (std::min / std::max over fp32 targets)
+        self.min_target = float(np.min(self.target)) if self.num_cases else 3.4028234663852886e38
+        self.max_target = float(np.max(self.target)) if self.num_cases else -3.4028234663852886e38
+
+    @classmethod
+    def load(cls, filename):
+        """Data::load via the library's host loader (libfm text, or .x/.xt/.y binary)."""
+        h = HostData()
+        _check(lib().vbfm_load_data(filename.encode(), C.byref(h)))
+        try:
+            n, nf, z = h.num_rows, h.num_feature, h.nnz
+            ds = cls(_copy(h.col_ptr, nf + 1, np.uint64), _copy(h.col_ent, z, ENTRY_DTYPE),
+                     _copy(h.target, n, np.float32), num_feature=nf,
+                     row_ptr=_copy(h.row_ptr, n + 1, np.uint64), row_ent=_copy(h.row_ent, z, ENTRY_DTYPE))
+            ds.min_target, ds.max_target = float(h.min_target), float(h.max_target)
+        finally:
+            lib().vbfm_free_host_data(C.byref(h))
+        return ds
+
+    @classmethod
+    def from_csr(cls, row_ptr, feat, val, target, num_feature=None):
+        """Build the transposed copy like Data::create_data_t (stable by feature)."""
+        row_ptr = np.asarray(row_ptr, dtype=np.uint64)
+        feat = np.asarray(feat, dtype=np.uint32)
+        n = len(target)
+        nf = int(feat.max()) + 1 if num_feature is None and len(feat) else int(num_feature or 0)
+        rows = np.repeat(np.arange(n, dtype=np.uint32), np.diff(row_ptr.astype(np.int64)))
+        order = np.argsort(feat, kind="stable")
+        col_ptr = np.zeros(nf + 1, dtype=np.uint64)
+        np.cumsum(np.bincount(feat, minlength=nf)[:nf], out=col_ptr[1:])
+        ent = np.empty(len(feat), dtype=ENTRY_DTYPE)
+        ent["id"] = rows[order]
+        ent["value"] = np.asarray(val, dtype=np.float32)[order]
+        return cls(col_ptr, ent, target, num_feature=nf)
+
+    def _csc(self):
+        c = Csc(self.num_cases, self.num_feature, len(self.col_ent), _ptr(self.col_ptr, P_u64),
+                self.col_ent.ctypes.data if len(self.col_ent) else None, _ptr(self.target, P_f32))
+        return c
+
+
+def num_all_attribute(train, test):
+    """libfm.cpp:215"""
+    return max(train.num_feature, test.num_feature) + 1
+
+
+def load_meta(filename, num_attribute):
+    """DataMetaInfo::loadGroupsFromFile (Data.h:49-61): one group id per attribute."""
+    g = np.loadtxt(filename, dtype=np.int64, ndmin=1)
+    out = np.zeros(num_attribute, dtype=np.uint32)
+    m = min(len(g), num_attribute)
+    out[:m] = g[:m]
+    return out
+
+
+class FMLearnVB:
+    """fm_learn_vb_simultaneous on one MI355X (src/libfm/src/fm_learn_vb_simultaneous.h)."""
+
+    def __init__(self, k0=1, k1=1, num_factor=8, num_attribute=0, attr_group=None,
+                 min_target=1.0, max_target=5.0, device=0):
+        self.k0, self.k1, self.k, self.D = int(bool(k0)), int(bool(k1)), int(num_factor), int(num_attribute)
+        self.attr_group = None if attr_group is None else np.ascontiguousarray(attr_group, dtype=np.uint32)
+        self.G = 1 if self.attr_group is None else int(self.attr_group.max()) + 1 if self.D else 1
+        cfg = Config(self.k0, self.k1, self.k, self.D, self.G, _ptr(self.attr_group, P_u32),
+                     min_target, max_target, device, 0)
+        self._ctx = C.c_void_p()
+        _check(lib().vbfm_create(C.byref(self._ctx), C.byref(cfg)))
+        self.num_iter_done = 0
+        self.fm_v = self.fm_w = None
+
+    # -- parameters ---------------------------------------------------------------------
+    def _params_struct(self, arrs):
+        return Params(*[_ptr(arrs[k], P_f64) for k in ("mu_w", "sigma_w", "mu_v", "sigma_v",
+                                                      "hyp_sigma_w", "hyp_sigma_v")],
+                      arrs.get("alpha", 1.0), arrs.get("sigma_0", 1.0), arrs.get("mu_0_dash", 0.0),
+                      arrs.get("sigma_0_dash", 0.02))
+
+    def _empty_params(self):
+        kd = self.k * self.D
+        return {"mu_w": np.zeros(self.D), "sigma_w": np.zeros(self.D), "mu_v": np.zeros(kd),
+                "sigma_v": np.zeros(kd), "hyp_sigma_w": np.zeros(self.G), "hyp_sigma_v": np.zeros(self.G * self.k)}
+
+    def init(self, seed, init_stdev=0.1, keep_model_draws=False):
+        """srand(seed); fm.init(); fm.w.init_normal(); fml->init() (libfm.cpp:123-366)."""
+        p = self._empty_params()
+        fm_v = np.zeros(self.k * self.D) if keep_model_draws else None
+        fm_w = np.zeros(self.D) if keep_model_draws else None
+        ps = self._params_struct(p)
+        _check(lib().vbfm_init_params_host(seed, init_stdev, self.k, self.D, self.G, C.byref(ps),
+                                           _ptr(fm_v, P_f64), _ptr(fm_w, P_f64)))
+        for k in ("alpha", "sigma_0", "mu_0_dash", "sigma_0_dash"):
+            p[k] = getattr(ps, k)
+        self.fm_v, self.fm_w = fm_v, fm_w
+        self.set_params(p)
+        return p
+
+    def init_device(self, seed):
+        """Random init on the device (bench scale; not the reference's RNG stream)."""
+        _check(lib().vbfm_init_params_device(self._ctx, seed), self._ctx)
+
+    def set_params(self, p):
+        full = self._empty_params()
+        full.update({k: np.ascontiguousarray(v, dtype=np.float64) if isinstance(v, np.ndarray) else v
+                     for k, v in p.items()})
+        _check(lib().vbfm_set_params(self._ctx, C.byref(self._params_struct(full))), self._ctx)
+
+    def get_params(self):
+        p = self._empty_params()
+        ps = self._params_struct(p)
+        _check(lib().vbfm_get_params(self._ctx, C.byref(ps)), self._ctx)
+        for k in ("alpha", "sigma_0", "mu_0_dash", "sigma_0_dash"):
+            p[k] = getattr(ps, k)
+        return p
+
+    # -- data ---------------------------------------------------------------------------
+    def set_data(self, train, test):
+        self._train_csc, self._test_csc = train._csc(), test._csc()
+        _check(lib().vbfm_set_train(self._ctx, C.byref(self._train_csc)), self._ctx)
+        _check(lib().vbfm_set_test(self._ctx, C.byref(self._test_csc)), self._ctx)
+        self.n_train, self.n_test = train.num_cases, test.num_cases
+
+    def synth(self, which, num_rows, n_fields, ids_per_field, seed, xmode=0):
+        _check(lib().vbfm_synth_generate(self._ctx, which, num_rows, n_fields, ids_per_field, seed, xmode),
+               self._ctx)
+        if which == 0:
+            self.n_train = num_rows
+        else:
+            self.n_test = num_rows
+
+    def shape(self, which):
+        n, nf, z = C.c_uint32(), C.c_uint32(), C.c_uint64()
+        _check(lib().vbfm_get_shape(self._ctx, which, C.byref(n), C.byref(nf), C.byref(z)), self._ctx)
+        return n.value, nf.value, z.value
+
+    def get_csc(self, which):
+        n, nf, z = self.shape(which)
+        cp = np.zeros(nf + 1, dtype=np.uint64)
+        ent = np.zeros(z, dtype=ENTRY_DTYPE)
+        tg = np.zeros(n, dtype=np.float32)
+        _check(lib().vbfm_get_csc(self._ctx, which, _ptr(cp, P_u64), ent.ctypes.data if z else None,
+                                  _ptr(tg, P_f32)), self._ctx)
+        return cp, ent, tg
+
+    def levels(self):
+        nf = self.shape(0)[1]
+        lv = np.zeros(nf, dtype=np.uint32)
+        L = C.c_uint32()
+        _check(lib().vbfm_get_levels(self._ctx, _ptr(lv, P_u32), C.byref(L)), self._ctx)
+        return lv, L.value
+
+    # -- learning -----------------------------------------------------------------------
+    def init_caches(self):
+        _check(lib().vbfm_init_caches(self._ctx), self._ctx)
+
+    def iterate(self):
+        st = IterStats()
+        _check(lib().vbfm_iterate(self._ctx, C.byref(st)), self._ctx)
+        self.num_iter_done += 1
+        return st
+
+    def learn(self, train, test, num_iter):
+        """fm_learn_vb::learn -> _learn: yields the IterStats of every iteration."""
+        self.set_data(train, test)
+        self.init_caches()
+        for _ in range(num_iter):
+            yield self.iterate()
+
+    def predict(self):
+        """pred_this: clipped test predictions of the last iteration."""
+        out = np.zeros(self.n_test)
+        _check(lib().vbfm_get_test_pred(self._ctx, _ptr(out, P_f64)), self._ctx)
+        return out
+
+    def evaluate(self, data=None):
+        """fm_learn_vb::evaluate returns NaN (fm_learn_vb.h:27)."""
+        return float("nan")
+
+    # -- update_all step by step --------------------------------------------------------
+    def step_w0(self):
+        _check(lib().vbfm_step_w0(self._ctx), self._ctx)
+
+    def step_w(self):
+        _check(lib().vbfm_step_w(self._ctx), self._ctx)
+
+    def step_qcache(self, f):
+        _check(lib().vbfm_step_qcache(self._ctx, f), self._ctx)
+
+    def step_v(self, f):
+        _check(lib().vbfm_step_v(self._ctx, f), self._ctx)
+
+    def step_hyper(self):
+        e = C.c_int32()
+        _check(lib().vbfm_step_hyper(self._ctx, C.byref(e)), self._ctx)
+        return bool(e.value)
+
+    def free_energy(self):
+        F = C.c_double()
+        _check(lib().vbfm_free_energy(self._ctx, C.byref(F)), self._ctx)
+        return F.value
+
+    def set_profiling(self, on=True):
+        _check(lib().vbfm_set_profiling(self._ctx, 1 if on else 0), self._ctx)
+
+    def factor_sweep(self):
+        ms = C.c_double()
+        _check(lib().vbfm_factor_sweep(self._ctx, C.byref(ms)), self._ctx)
+        return ms.value
+
+    def rows(self):
+        n = self.n_train
+        out = {k: np.zeros(n) for k in ("e", "t", "q", "tq", "tz")}
+        _check(lib().vbfm_get_rows(self._ctx, *[_ptr(out[k], P_f64) for k in ("e", "t", "q", "tq", "tz")]),
+               self._ctx)
+        return out
+
+    def test_e(self):
+        out = np.zeros(self.n_test)
+        _check(lib().vbfm_get_test_e(self._ctx, _ptr(out, P_f64)), self._ctx)
+        return out
+
+    # -- multi-GPU ----------------------------------------------------------------------
+    @staticmethod
+    def comm_unique_id():
+        buf = (C.c_uint8 * 128)()
+        _check(lib().vbfm_comm_unique_id(buf))
+        return bytes(buf)
+
+    def comm_init(self, nranks, rank, uid):
+        buf = (C.c_uint8 * 128).from_buffer_copy(uid)
+        _check(lib().vbfm_comm_init(self._ctx, nranks, rank, buf), self._ctx)
+
+    def close(self):
+        if self._ctx:
+            lib().vbfm_destroy(self._ctx)
+            self._ctx = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

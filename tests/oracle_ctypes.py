@@ -162,7 +162,7 @@ class VB:
         lib().or_vb_init_caches(C.byref(self.s), C.byref(self.train.d), C.byref(self.test.d))
 
     def step(self, name, *args):
-        getattr(lib(), "or_vb_" + name)(C.byref(self.s), C.byref(self.train.d), *args)
+        return getattr(lib(), "or_vb_" + name)(C.byref(self.s), C.byref(self.train.d), *args)
 
     def iterate(self):
         r, m, t = C.c_double(), C.c_double(), C.c_double()

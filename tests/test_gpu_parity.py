@@ -1,0 +1,195 @@
+"""Parity of the HIP path (libvbfm.so through its C-ABI) with the oracle and the reference.
+
+Tolerances (north star: 1e-6 relative on free energy and test RMSE at iteration parity):
+  * per-row sums (q-cache, predictions, T) keep the reference's summation order: bit-exact;
+  * everything downstream of a column / data-set reduction (the device sums in a fixed
+    tree order, the reference sequentially) is held to REL = 1e-9 relative -- observed
+    differences are ~1e-13; the 1e-6 gate of the north star is far looser.
+"""
+import os
+
+import numpy as np
+import pytest
+
+import oracle_ctypes as oc
+import synth
+import vbfm
+from conftest import GOLDEN, load_case
+
+pytestmark = pytest.mark.gpu
+REL = 1e-9
+
+
+def rel_err(a, b):
+    a, b = np.asarray(a, dtype=np.float64), np.asarray(b, dtype=np.float64)
+    scale = max(1e-300, float(np.max(np.abs(b))) if b.size else 1.0)
+    return float(np.max(np.abs(a - b))) / scale if b.size else 0.0
+
+
+def close(a, b, tol=REL):
+    assert rel_err(a, b) <= tol, (rel_err(a, b), a, b)
+
+
+def gpu_learner(train, test, dim, seed, init_stdev, attr_group=None):
+    k0, k1, k = [int(x) for x in dim.split(",")]
+    D = vbfm.num_all_attribute(train, test)
+    fml = vbfm.FMLearnVB(k0, k1, k, D, attr_group=attr_group, min_target=train.min_target,
+                         max_target=train.max_target)
+    fml.init(seed, init_stdev)
+    fml.set_data(train, test)
+    return fml
+
+
+def oracle_learner(tr_path, te_path, dim, seed, init_stdev, attr_group=None):
+    tr, te = oc.Data(tr_path), oc.Data(te_path)
+    k0, k1, k = [int(x) for x in dim.split(",")]
+    vb = oc.VB(k0, k1, k, oc.num_all_attribute(tr, te), attr_group)
+    vb.init_params(seed, init_stdev)
+    vb.attach(tr, te)
+    return vb
+
+
+@pytest.mark.parametrize("case", ["tiny", "tiny_dup"])
+def test_update_all_steps_vs_oracle(case):
+    d = os.path.join(GOLDEN, case)
+    trp, tep = os.path.join(d, "train.libfm"), os.path.join(d, "test.libfm")
+    train, test = vbfm.DataSubset.load(trp), vbfm.DataSubset.load(tep)
+    g = gpu_learner(train, test, "1,1,3", 5, 0.1)
+    o = oracle_learner(trp, tep, "1,1,3", 5, 0.1)
+    po, pg = o.params(), g.get_params()
+    for key in ("mu_w", "mu_v", "sigma_v"):
+        np.testing.assert_array_equal(pg[key], po[key])
+    g.init_caches()
+    o.init_caches()
+    rg, ro = g.rows(), o.rows()
+    np.testing.assert_array_equal(rg["e"], ro["e"])       # per-row sums: bit-exact
+    np.testing.assert_array_equal(rg["t"], ro["t"])
+    np.testing.assert_array_equal(g.test_e(), oc.arr(o.s.e_test, o.s.n_test))
+    g.step_w0(); o.step("update_w0")
+    close(g.rows()["e"], o.rows()["e"]); close(g.rows()["t"], o.rows()["t"])
+    g.step_w(); o.step("update_w_all")
+    close(g.get_params()["mu_w"], o.params()["mu_w"]); close(g.rows()["e"], o.rows()["e"])
+    for f in range(3):
+        g.step_qcache(f); o.step("add_main_q", f)
+        for key in ("q", "tq", "tz"):
+            close(g.rows()[key], o.rows()[key])
+        g.step_v(f); o.step("update_v_all", f)
+        rg, ro = g.rows(), o.rows()
+        for key in ("e", "t", "q", "tq", "tz"):
+            close(rg[key], ro[key])
+        close(g.get_params()["mu_v"], o.params()["mu_v"])
+        close(g.get_params()["sigma_v"], o.params()["sigma_v"])
+    early = g.step_hyper()
+    assert early == bool(o.step("hyper") or o.s.hyper_skipped)
+    close(g.get_params()["hyp_sigma_v"], o.params()["hyp_sigma_v"])
+    close([g.free_energy()], [oc.lib().or_vb_free_energy(oc.C.byref(o.s), oc.C.byref(o.train.d))])
+
+
+def run_trace(train, test, meta, attr_group=None):
+    fml = gpu_learner(train, test, meta["dim"], meta["seed"], meta["init_stdev"], attr_group)
+    fml.init_caches()
+    out = [fml.iterate() for _ in range(meta["iter"])]
+    return fml, out
+
+
+def check_trace(stats, trace, tol=REL):
+    for it, (st, ref) in enumerate(zip(stats, trace)):
+        assert st.free_energy_valid
+        close([st.rmse], [ref["rmse"]], tol)
+        close([st.mae], [ref["mae"]], tol)
+        close([st.train_quirk], [ref["train"]], tol)
+        close([st.alpha], [ref["alpha"]], tol)
+        close([st.mu_0_dash], [ref["mu_0_dash"]], tol)
+        close([st.free_energy], [ref["free_energy"]], tol)
+
+
+@pytest.mark.parametrize("case", ["tiny/vb", "tiny_dup/vb", "tiny/vb_meta"])
+def test_trace_tiny_vs_reference(case):
+    t, a = load_case(case)
+    d = os.path.join(GOLDEN, case.split("/")[0])
+    train = vbfm.DataSubset.load(os.path.join(d, "train.libfm"))
+    test = vbfm.DataSubset.load(os.path.join(d, "test.libfm"))
+    groups = None
+    if "meta" in t["meta"]:
+        groups = vbfm.load_meta(os.path.join(d, t["meta"]["meta"]), vbfm.num_all_attribute(train, test))
+    fml, stats = run_trace(train, test, t["meta"], groups)
+    check_trace(stats, t["trace"])
+    p = fml.get_params()
+    last = len(stats) - 1
+    close(p["mu_v"], a["iter%d_mu_v" % last])
+    close(p["sigma_w"], a["iter%d_sigma_w" % last])
+    close(fml.predict(), a["iter%d_pred" % last])
+
+
+def test_trace_synthetic_vs_reference(synth_files):
+    t, a = load_case("synth")
+    train, test = vbfm.DataSubset.load(synth_files["train"]), vbfm.DataSubset.load(synth_files["test"])
+    fml, stats = run_trace(train, test, t["meta"])
+    assert stats[0].num_levels == t["meta"]["n_fields"]
+    check_trace(stats, t["trace"])
+    close(fml.get_params()["mu_v"], a["final_mu_v"])
+
+
+def test_trace_movielens_split_vs_reference(sa_split):
+    t, a = load_case("sa_k8")
+    train, test = vbfm.DataSubset.load(sa_split["train"]), vbfm.DataSubset.load(sa_split["test"])
+    fml, stats = run_trace(train, test, t["meta"])
+    check_trace(stats, t["trace"])
+    close(fml.get_params()["mu_w"], a["final_mu_w"])
+
+
+def test_device_generator_matches_spec():
+    """vbfm_synth_generate (device) == tests/synth.py (numpy), CSC bit-exact."""
+    n, F, S, seed = 5000, 7, 300, 99
+    fml = vbfm.FMLearnVB(1, 1, 2, F * S + 1)
+    fml.synth(0, n, F, S, seed, xmode=1)
+    cp, ent, tg = fml.get_csc(0)
+    rp, f, v, y = synth.generate(n, F, S, seed, 1)
+    ecp, erow, eval_ = synth.csr_to_csc(n, F * S, rp, f, v)
+    np.testing.assert_array_equal(cp, ecp)
+    np.testing.assert_array_equal(ent["id"], erow)
+    np.testing.assert_array_equal(ent["value"], eval_)
+    np.testing.assert_array_equal(tg, y)
+    lv, L = fml.levels()
+    assert L == F
+    present = np.bincount(f, minlength=F * S) > 0
+    np.testing.assert_array_equal(lv[present], (np.arange(F * S) // S + 1)[present])
+
+
+def test_generated_data_vs_oracle_two_iterations():
+    """Device-generated field data (real-valued x) through 2 iterations vs the oracle."""
+    n, F, S, seed, k = 60000, 8, 500, 3, 3
+    D = F * S + 1
+    rp, f, v, y = synth.generate(n, F, S, seed, 1)
+    rpt, ft, vt, yt = synth.generate(2000, F, S, seed + 1, 1)
+    fml = vbfm.FMLearnVB(1, 1, k, D, min_target=float(y.min()), max_target=float(y.max()))
+    fml.init(7, 0.1)
+    fml.synth(0, n, F, S, seed, 1)
+    fml.synth(1, 2000, F, S, seed + 1, 1)
+    fml.init_caches()
+    tr = oc.Data(csr=(n, rp, f, v, y))
+    te = oc.Data(csr=(2000, rpt, ft, vt, yt))
+    o = oc.VB(1, 1, k, D)
+    o.init_params(7, 0.1)
+    o.attach(tr, te)
+    o.init_caches()
+    for _ in range(2):
+        st = fml.iterate()
+        rmse, mae, trq = o.iterate()
+        close([st.rmse], [rmse]); close([st.train_quirk], [trq])
+        close([st.free_energy], [o.s.last_free_energy])
+    close(fml.get_params()["mu_v"], o.params()["mu_v"])
+
+
+def test_deterministic_run_to_run():
+    def run():
+        fml = vbfm.FMLearnVB(1, 1, 4, 10 * 1000 + 1, min_target=1, max_target=5)
+        fml.init(3, 0.1)
+        fml.synth(0, 100000, 10, 1000, 5, 1)
+        fml.synth(1, 5000, 10, 1000, 6, 1)
+        fml.init_caches()
+        st = [fml.iterate() for _ in range(2)]
+        return [s.free_energy for s in st], fml.get_params()["mu_v"]
+    a, b = run(), run()
+    assert a[0] == b[0]
+    np.testing.assert_array_equal(a[1], b[1])
