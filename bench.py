@@ -163,13 +163,15 @@ def main():
     nnz = N * F
     value = world * nnz * k * args.steps / elapsed
     levels = stats[-1].num_levels
-    # roofline of the dominant kernel (k_v_level_fused, one launch per factor and level):
-    # algorithmic bytes per launch = 120 B per nnz of the level (stats 8 CSC + 24 e,q,tq;
-    # correction 8 CSC + 40 read + 40 write) + 32 B per feature (mu, sigma read + write).
+    # roofline of the dominant kernel (k_v_level_fused, one launch per factor and level). It
+    # does the whole factor sweep of its level (stats, posterior, correction and the q-cache
+    # of the next factor), so its algorithmic bytes are SURVEY §8d's per-factor model
+    # B = 128 B/nnz + 24 B/row + 32 B/feature, spread over the level launches of a factor:
+    # 128 = q-build 8 (CSC) + stats 32 (8 CSC + 24 e,q,tq) + correction 88 (8 CSC + 40 + 40).
     n_launch = sum(s.n_vlevel_launches for s in stats)
     ms_launch = sum(s.ms_vlevel_kernels for s in stats)
     avg_ms = ms_launch / max(1, n_launch)
-    bytes_per_launch = (120.0 * nnz + 32.0 * (F * S)) / max(1, levels)
+    bytes_per_launch = (128.0 * nnz + 24.0 * N + 32.0 * (F * S)) / max(1, levels)
     achieved = bytes_per_launch / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else 0.0
     sweep_ms = sum(s.ms_v for s in stats) / len(stats)
     traffic = None
@@ -189,7 +191,7 @@ def main():
                    "parallelism": "row-sharded dp%d" % world},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                     "kernel": "k_v_level_fused<256,4>", "avg_launch_ms": avg_ms,
+                     "kernel": "k_v_level_fused", "avg_launch_ms": avg_ms,
                      "launches": n_launch, "bytes_per_launch": bytes_per_launch},
         "factor_sweep_ms_per_step": sweep_ms,
         "factor_sweep_nnz_k_per_s": world * nnz * k / (sweep_ms * 1e-3),

@@ -13,6 +13,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <cstdio>
 #include <cstring>
 #include <string>
@@ -88,7 +89,9 @@ struct vbfm_ctx {
 	std::vector<double> hyp_w, hyp_v;
 	double alpha = 1.0, sigma_0 = 1.0, mu0 = 0.0, s0d = 0.02;
 	// schedule
-	std::vector<uint32_t> level_ptr, level_h;
+	std::vector<uint32_t> level_ptr, level_h, level_avg;
+	int q_ready[2] = {-1, -1};     // factor whose q-cache each slot holds (-1: none)
+	int qslot = 0;                 // slot reported by vbfm_get_rows
 	uint32_t *level_feats = nullptr;
 	uint8_t *dup = nullptr;
 	bool sched_ready = false;
@@ -275,6 +278,15 @@ void build_schedule(vbfm_ctx *c)
 	dfree(c->level_feats);
 	c->level_feats = dalloc<uint32_t>(nf);
 	if (nf) HIPCHK(hipMemcpy(c->level_feats, feats.data(), nf * 4, hipMemcpyHostToDevice));
+	std::vector<uint64_t> cp((size_t)nf + 1, 0);
+	HIPCHK(hipMemcpy(cp.data(), d.col_ptr, ((size_t)nf + 1) * 8, hipMemcpyDeviceToHost));
+	c->level_avg.assign(L, 0);
+	for (uint32_t l = 0; l < L; l++) {
+		uint64_t z = 0;
+		for (uint32_t i = c->level_ptr[l]; i < c->level_ptr[l + 1]; i++) z += cp[feats[i] + 1] - cp[feats[i]];
+		const uint32_t nfl = c->level_ptr[l + 1] - c->level_ptr[l];
+		c->level_avg[l] = nfl ? (uint32_t)std::min<uint64_t>(z / nfl, 0xFFFFFFFFu) : 0;
+	}
 	uint32_t maxlev = 0;
 	for (uint32_t l = 0; l < L; l++) maxlev = std::max(maxlev, c->level_ptr[l + 1] - c->level_ptr[l]);
 	if (c->nranks > 1 && maxlev > c->stats_cap) {
@@ -340,7 +352,9 @@ LevelArgs level_args(vbfm_ctx *c, uint32_t l, bool is_w, int f)
 	a.feats = c->level_feats + c->level_ptr[l];
 	a.nfeat = c->level_ptr[l + 1] - c->level_ptr[l];
 	a.rows = c->rows;
-	a.ms = is_w ? c->ms_w : c->ms_v + (size_t)f * c->D;
+	a.ms = is_w ? c->ms_w : c->ms_v + f;
+	a.ms_stride = is_w ? 1 : (uint32_t)c->k;
+	a.ms_stride_next = (uint32_t)c->k;
 	a.hyp = is_w ? c->hyp_w_d : c->hyp_v_d + f;
 	a.hyp_stride = is_w ? 1 : (uint32_t)c->k;
 	a.attr_group = c->group_d;
@@ -348,6 +362,14 @@ LevelArgs level_args(vbfm_ctx *c, uint32_t l, bool is_w, int f)
 	a.alpha = c->alpha;
 	a.counters = c->counters;
 	a.stats = c->stats;
+	a.avg_len = c->level_avg[l];
+	if (is_w) {
+		a.slot = 0;                                          // fused q-cache of factor 0
+		a.ms_next = c->k > 0 ? c->ms_v : nullptr;          // factor 0: ms_v[j*k + 0]
+	} else {
+		a.slot = f & 1;
+		a.ms_next = f + 1 < c->k ? c->ms_v + (f + 1) : nullptr;
+	}
 	return a;
 }
 
@@ -406,21 +428,34 @@ void step_w0(vbfm_ctx *c)
 	HIPCHK(vbk::w0_apply(c->rows, c->tr.n, mu_old - c->mu0, c->s0d - sigma_old, c->s));
 }
 
+// the w sweep; with factors it also leaves the q-cache of factor 0 in slot 0
 void step_w(vbfm_ctx *c)
 {
 	for (uint32_t l = 0; l < nlevels(c); l++) sweep_level(c, l, true, 0);
+	if (c->k > 0) c->q_ready[0] = 0;
 }
 
+// make the q-cache of factor f current (zero + add_main_q, fm_learn_vb.h:411-418): a no-op
+// when the previous sweep already accumulated it, else the row-parallel kernel
 void step_qcache(vbfm_ctx *c, int f)
 {
-	const size_t p = prof_begin(c, 2);
-	HIPCHK(vbk::qcache(c->tr.row_ptr, c->tr.csr, c->ms_v + (size_t)f * c->D, c->rows, c->tr.n, c->s));
-	prof_end(c, p);
+	const int slot = f & 1;
+	if (c->q_ready[slot] != f) {
+		const size_t p = prof_begin(c, 2);
+		HIPCHK(vbk::qcache(c->tr.row_ptr, c->tr.csr, c->ms_v + f, (uint32_t)c->k, c->rows, c->tr.n, slot, c->s));
+		prof_end(c, p);
+		c->q_ready[slot] = f;
+	}
+	c->qslot = slot;
 }
 
+// the v sweep of factor f (which also accumulates the q-cache of factor f+1)
 void step_v(vbfm_ctx *c, int f)
 {
 	for (uint32_t l = 0; l < nlevels(c); l++) sweep_level(c, l, false, f);
+	c->qslot = f & 1;
+	if (f + 1 < c->k) c->q_ready[(f + 1) & 1] = f + 1;
+	else c->q_ready[(f + 1) & 1] = -1;
 }
 
 double rows_energy(vbfm_ctx *c)
@@ -462,10 +497,20 @@ double free_energy(vbfm_ctx *c, double energy)
 	return fe;
 }
 
+// the reference's exact summation order for small data sets, the factor-blocked form for
+// large ones (VBFM_PREDICT=exact|blocked overrides)
+int blocked_predict(const vbfm_ctx *c, const DevData &d)
+{
+	const char *env = getenv("VBFM_PREDICT");
+	if (env && !strcmp(env, "exact")) return 0;
+	if (env && !strcmp(env, "blocked")) return 1;
+	return (double)d.nnz * c->k > 5e7 ? 1 : 0;
+}
+
 void test_predict(vbfm_ctx *c)
 {
-	HIPCHK(vbk::predict_e(c->te.row_ptr, c->te.csr, c->ms_v, c->ms_w, c->D, c->k, c->k1, c->k0, c->mu0, c->e_test,
-	                      c->te.n, c->s));
+	HIPCHK(vbk::predict_e(c->te.row_ptr, c->te.csr, c->ms_v, c->ms_w, c->k, c->k1, c->k0, c->mu0, c->e_test, c->te.n,
+	                      blocked_predict(c, c->te), c->s));
 }
 
 void read_counters(vbfm_ctx *c, vbfm_iter_stats *o)
@@ -580,6 +625,7 @@ static void alloc_rows(vbfm_ctx *c)
 	HIPCHK(hipMemsetAsync(c->rows, 0, (size_t)std::max(c->tr.n, 1u) * sizeof(RowRec), c->s));
 	uint64_t n = c->tr.n;
 	c->n_global = n;
+	c->q_ready[0] = c->q_ready[1] = -1;
 	if (c->nranks > 1) {
 		double v = (double)n;
 		allreduce_host(c, &v, 1);
@@ -610,6 +656,8 @@ int vbfm_set_train(vbfm_ctx *c, const vbfm_csc *in)
 		const uint32_t nf = global_nf(c, in->num_feature);
 		if (nf > c->D) throw std::string("train num_feature exceeds num_attribute");
 		upload(c, c->tr, in, nf);
+		if (c->tr.n > ROW_MASK) throw std::string("too many rows for one shard (max 2^31-1)");
+		HIPCHK(vbk::mark_first(c->tr.row_ptr, c->tr.csr, c->tr.col_ptr, c->tr.csc, c->tr.n, c->s));
 		alloc_rows(c);
 	});
 }
@@ -683,8 +731,11 @@ int vbfm_synth_generate(vbfm_ctx *c, int32_t which, uint32_t n, uint32_t F, uint
 		float mn = 3.40282347e+38f, mx = -3.40282347e+38f;
 		for (float v : t) { mn = std::min(v, mn); mx = std::max(v, mx); }
 		d.min_target = mn; d.max_target = mx;
-		if (which == 0) alloc_rows(c);
-		else {
+		if (which == 0) {
+			if (n > ROW_MASK) throw std::string("too many rows for one shard (max 2^31-1)");
+			HIPCHK(vbk::mark_first(d.row_ptr, d.csr, d.col_ptr, d.csc, n, c->s));
+			alloc_rows(c);
+		} else {
 			dfree(c->e_test); dfree(c->pred_test);
 			c->e_test = dalloc<double>(n);
 			c->pred_test = dalloc<double>(n);
@@ -711,7 +762,10 @@ int vbfm_get_csc(vbfm_ctx *c, int32_t which, uint64_t *col_ptr, vbfm_entry *col_
 	return guarded(c, [&] {
 		const DevData &d = which ? c->te : c->tr;
 		if (col_ptr) HIPCHK(hipMemcpy(col_ptr, d.col_ptr, ((size_t)d.nf_local + 1) * 8, hipMemcpyDeviceToHost));
-		if (col_ent && d.nnz) HIPCHK(hipMemcpy(col_ent, d.csc, d.nnz * 8, hipMemcpyDeviceToHost));
+		if (col_ent && d.nnz) {
+			HIPCHK(hipMemcpy(col_ent, d.csc, d.nnz * 8, hipMemcpyDeviceToHost));
+			for (uint64_t p = 0; p < d.nnz; p++) col_ent[p].id &= ROW_MASK;   // first-entry flags
+		}
 		if (target && d.n) HIPCHK(hipMemcpy(target, d.target, (size_t)d.n * 4, hipMemcpyDeviceToHost));
 	});
 }
@@ -736,12 +790,12 @@ int vbfm_set_params(vbfm_ctx *c, const vbfm_params *p)
 		double *tmp = dalloc<double>(2 * std::max(kd, (size_t)c->D));
 		HIPCHK(hipMemcpyAsync(tmp, p->mu_w, c->D * 8, hipMemcpyHostToDevice, c->s));
 		HIPCHK(hipMemcpyAsync(tmp + c->D, p->sigma_w, c->D * 8, hipMemcpyHostToDevice, c->s));
-		HIPCHK(vbk::pack_pairs(tmp, tmp + c->D, c->ms_w, c->D, c->s));
+		HIPCHK(vbk::pack_pairs(tmp, tmp + c->D, c->ms_w, 1, c->D, c->s));
 		sync(c);
 		if (kd) {
 			HIPCHK(hipMemcpyAsync(tmp, p->mu_v, kd * 8, hipMemcpyHostToDevice, c->s));
 			HIPCHK(hipMemcpyAsync(tmp + kd, p->sigma_v, kd * 8, hipMemcpyHostToDevice, c->s));
-			HIPCHK(vbk::pack_pairs(tmp, tmp + kd, c->ms_v, kd, c->s));
+			HIPCHK(vbk::pack_pairs(tmp, tmp + kd, c->ms_v, (uint32_t)c->k, c->D, c->s));
 			sync(c);
 		}
 		dfree(tmp);
@@ -749,6 +803,7 @@ int vbfm_set_params(vbfm_ctx *c, const vbfm_params *p)
 		if (p->hyp_sigma_v) std::copy(p->hyp_sigma_v, p->hyp_sigma_v + (size_t)c->G * c->k, c->hyp_v.begin());
 		upload_hyp(c);
 		c->alpha = p->alpha; c->sigma_0 = p->sigma_0; c->mu0 = p->mu_0_dash; c->s0d = p->sigma_0_dash;
+		c->q_ready[0] = c->q_ready[1] = -1;
 		sync(c);
 	});
 }
@@ -759,12 +814,12 @@ int vbfm_get_params(vbfm_ctx *c, vbfm_params *p)
 	return guarded(c, [&] {
 		const size_t kd = (size_t)c->k * c->D;
 		double *tmp = dalloc<double>(2 * std::max(kd, (size_t)c->D));
-		HIPCHK(vbk::unpack_pairs(c->ms_w, tmp, tmp + c->D, c->D, c->s));
+		HIPCHK(vbk::unpack_pairs(c->ms_w, tmp, tmp + c->D, 1, c->D, c->s));
 		if (p->mu_w) HIPCHK(hipMemcpyAsync(p->mu_w, tmp, c->D * 8, hipMemcpyDeviceToHost, c->s));
 		if (p->sigma_w) HIPCHK(hipMemcpyAsync(p->sigma_w, tmp + c->D, c->D * 8, hipMemcpyDeviceToHost, c->s));
 		sync(c);
 		if (kd) {
-			HIPCHK(vbk::unpack_pairs(c->ms_v, tmp, tmp + kd, kd, c->s));
+			HIPCHK(vbk::unpack_pairs(c->ms_v, tmp, tmp + kd, (uint32_t)c->k, c->D, c->s));
 			if (p->mu_v) HIPCHK(hipMemcpyAsync(p->mu_v, tmp, kd * 8, hipMemcpyDeviceToHost, c->s));
 			if (p->sigma_v) HIPCHK(hipMemcpyAsync(p->sigma_v, tmp + kd, kd * 8, hipMemcpyDeviceToHost, c->s));
 			sync(c);
@@ -786,6 +841,7 @@ int vbfm_init_params_device(vbfm_ctx *c, uint64_t seed)
 		std::fill(c->hyp_v.begin(), c->hyp_v.end(), 1.0);
 		upload_hyp(c);
 		c->alpha = 1.0; c->sigma_0 = 1.0; c->mu0 = 0.0; c->s0d = 0.02;
+		c->q_ready[0] = c->q_ready[1] = -1;
 		sync(c);
 	});
 }
@@ -796,10 +852,11 @@ int vbfm_init_caches(vbfm_ctx *c)
 	return guarded(c, [&] {
 		require_train(c);
 		// fm_learn_vb_simultaneous.h:37-44: yhat of train and test, T of train, e = y - yhat
-		HIPCHK(vbk::predict_e(c->tr.row_ptr, c->tr.csr, c->ms_v, c->ms_w, c->D, c->k, c->k1, c->k0, c->mu0,
-		                      c->scratch_n, c->tr.n, c->s));
-		HIPCHK(vbk::predict_t(c->tr.row_ptr, c->tr.csr, c->ms_v, c->ms_w, c->D, c->k, c->k1, c->k0, c->s0d, c->rows,
-		                      c->tr.n, c->s));
+		const int bl = blocked_predict(c, c->tr);
+		HIPCHK(vbk::predict_e(c->tr.row_ptr, c->tr.csr, c->ms_v, c->ms_w, c->k, c->k1, c->k0, c->mu0, c->scratch_n,
+		                      c->tr.n, bl, c->s));
+		HIPCHK(vbk::predict_t(c->tr.row_ptr, c->tr.csr, c->ms_v, c->ms_w, c->k, c->k1, c->k0, c->s0d, c->rows, c->tr.n,
+		                      bl, c->s));
 		HIPCHK(vbk::residual_init(c->rows, c->scratch_n, c->tr.target, c->tr.n, c->s));
 		if (c->e_test) test_predict(c);
 		sync(c);
@@ -835,6 +892,7 @@ int vbfm_step_v(vbfm_ctx *c, int32_t f)
 	return guarded(c, [&] {
 		require_train(c);
 		if (f < 0 || f >= c->k) throw std::string("factor out of range");
+		if (c->q_ready[f & 1] != f) throw std::string("vbfm_step_v: q-cache of this factor is not current (vbfm_step_qcache)");
 		step_v(c, f);
 		sync(c);
 	});
@@ -863,12 +921,13 @@ int vbfm_get_rows(vbfm_ctx *c, double *e, double *t, double *q, double *tq, doub
 	return guarded(c, [&] {
 		std::vector<RowRec> h(c->tr.n);
 		if (c->tr.n) HIPCHK(hipMemcpy(h.data(), c->rows, (size_t)c->tr.n * sizeof(RowRec), hipMemcpyDeviceToHost));
+		const bool s1 = c->qslot == 1;
 		for (uint32_t i = 0; i < c->tr.n; i++) {
 			if (e) e[i] = h[i].e;
 			if (t) t[i] = h[i].t;
-			if (q) q[i] = h[i].q;
-			if (tq) tq[i] = h[i].tq;
-			if (tz) tz[i] = h[i].tz;
+			if (q) q[i] = s1 ? h[i].q1 : h[i].q;
+			if (tq) tq[i] = s1 ? h[i].tq1 : h[i].tq;
+			if (tz) tz[i] = s1 ? h[i].tz1 : h[i].tz;
 		}
 	});
 }

@@ -4,12 +4,19 @@
 //   RowRec rows[N]      64-B aligned record per train row: the reference's two row caches
 //                       e_q_term{e,q} (fm_learn_mcmc.h:52-55) and t_term{t,q,z}
 //                       (fm_learn_vb.h:17-21) fused so that one 64-B line serves every
-//                       gather of a row (e,q,tq,tz,t = 40 B used).
-//   CSC  col_ptr[nf+1] (u64), csc[nnz] (uint2 = {row, fp32 bits}) == sparse_entry<float>
+//                       gather of a row, plus a second q-cache slot: while factor f is swept
+//                       from slot f%2, the q-cache of factor f+1 is accumulated into slot
+//                       (f+1)%2 (the levels visit a row's features in ascending order, the
+//                       order of add_main_q, so the fused sum is bit-exact).
+//   CSC  col_ptr[nf+1] (u64), csc[nnz] (uint2 = {row, fp32 bits}) == sparse_entry<float>;
+//                       bit 31 of the row id marks the entry that is its row's first
+//                       (smallest-feature) entry: where the fused q-cache sum starts.
 //   CSR  row_ptr[N+1]  (u64), csr[nnz] (uint2 = {feature, fp32 bits}), each row sorted by
 //                       feature id: the order in which the reference's column-major loops
 //                       visit a row, so per-row sums are bit-identical to the reference.
-//   ms_v[k*D] (double2 = {mu, sigma}) of mu_v_dash/sigma_v_dash, factor-major;
+//   ms_v[D*k] (double2 = {mu, sigma}) of mu_v_dash/sigma_v_dash, FEATURE-major:
+//             ms_v[j*k + f]; all factors of a feature are contiguous, so a prediction reads
+//             one run per entry and mu_{f+1}[j] shares the line of mu_f[j];
 //   ms_w[D]   (double2 = {mu, sigma}) of mu_w_dash/sigma_w_dash.
 #pragma once
 #include <hip/hip_runtime.h>
@@ -17,12 +24,14 @@
 
 struct __attribute__((aligned(64))) RowRec {
 	double e;    // cache[i].e      residual y - yhat (fm_learn_vb_simultaneous.h:42-44)
-	double q;    // cache[i].q      q-cache of the current factor: sum mu x
-	double tq;   // cache_t[i].q    sum sigma x^2
-	double tz;   // cache_t[i].z    sum mu^2 x^2
+	double q;    // cache[i].q      q-cache slot 0: sum mu x
+	double tq;   // cache_t[i].q    slot 0: sum sigma x^2
+	double tz;   // cache_t[i].z    slot 0: sum mu^2 x^2
 	double t;    // cache_t[i].t    variance term T_n (paper eq. 26)
-	double pad[3];
+	double q1, tq1, tz1;   // q-cache slot 1
 };
+#define ROW_MASK 0x7FFFFFFFu
+#define ROW_FIRST 0x80000000u
 static_assert(sizeof(RowRec) == 64, "RowRec must be one 64-B line");
 
 enum {
@@ -38,7 +47,8 @@ struct LevelArgs {
 	const uint32_t *feats;     // features of this level (ascending id)
 	uint32_t nfeat;
 	RowRec *rows;
-	double2 *ms;               // ms_v + f*D, or ms_w
+	double2 *ms;               // ms_v + f (stride k), or ms_w (stride 1)
+	uint32_t ms_stride;
 	const double *hyp;         // hyper prior: sigma_v(g, f) at hyp[g*stride], or sigma_w(g)
 	uint32_t hyp_stride;
 	const uint32_t *attr_group;
@@ -46,6 +56,10 @@ struct LevelArgs {
 	double alpha;
 	uint32_t *counters;
 	double2 *stats;            // split mode: per-level-feature (sum1, sum2), or nullptr
+	const double2 *ms_next;    // {mu, sigma} of factor f+1 (fused q-cache, stride ms_stride_next), or nullptr
+	uint32_t ms_stride_next;
+	int slot;                  // q-cache slot of the factor being swept (v) / of factor 0 (w)
+	uint32_t avg_len;          // mean column length of the level (launch shape)
 };
 
 // kernels launched from the C-ABI layer (vbfm_kernels.hip)
@@ -56,13 +70,17 @@ hipError_t v_level_stats(const LevelArgs &a, hipStream_t s);
 hipError_t v_level_correct(const LevelArgs &a, hipStream_t s);
 hipError_t w_level_stats(const LevelArgs &a, hipStream_t s);
 hipError_t w_level_correct(const LevelArgs &a, hipStream_t s);
-hipError_t qcache(const uint64_t *row_ptr, const uint2 *csr, const double2 *ms_f, RowRec *rows,
-                  uint32_t n, hipStream_t s);
+hipError_t qcache(const uint64_t *row_ptr, const uint2 *csr, const double2 *ms_f, uint32_t stride, RowRec *rows,
+                  uint32_t n, int slot, hipStream_t s);
+hipError_t mark_first(const uint64_t *row_ptr, const uint2 *csr, const uint64_t *col_ptr, uint2 *csc,
+                      uint32_t n, hipStream_t s);
+// blocked = 0: the reference's summation order (bit-exact); 1: factors in blocks of 8
+// (exact per-factor sums, the -1/2 sum v^2 x^2 term summed block-major: ~1 ulp apart)
 hipError_t predict_e(const uint64_t *row_ptr, const uint2 *csr, const double2 *ms_v, const double2 *ms_w,
-                     uint32_t D, int k, int k1, int k0, double mu0, double *out_e, uint32_t n,
+                     int k, int k1, int k0, double mu0, double *out_e, uint32_t n, int blocked,
                      hipStream_t s);
 hipError_t predict_t(const uint64_t *row_ptr, const uint2 *csr, const double2 *ms_v, const double2 *ms_w,
-                     uint32_t D, int k, int k1, int k0, double sigma0_dash, RowRec *rows, uint32_t n,
+                     int k, int k1, int k0, double sigma0_dash, RowRec *rows, uint32_t n, int blocked,
                      hipStream_t s);
 hipError_t residual_init(RowRec *rows, const double *yhat, const float *target, uint32_t n, hipStream_t s);
 // per-block partial sums over rows; mode 0: e + mu0 ; mode 1: e*e + t ; out[nblocks]
@@ -98,7 +116,8 @@ hipError_t sort_pairs_u32(void *tmp, size_t *tmp_bytes, const uint32_t *ki, uint
 hipError_t exclusive_scan_u64(void *tmp, size_t *tmp_bytes, const uint64_t *in, uint64_t *out, size_t n,
                               hipStream_t s);
 hipError_t init_normal_pairs(double2 *ms, size_t n, uint64_t seed, uint64_t stream, hipStream_t s);
-// layout conversion between the reference's separate mu/sigma arrays and double2 pairs
-hipError_t pack_pairs(const double *a, const double *b, double2 *out, size_t n, hipStream_t s);
-hipError_t unpack_pairs(const double2 *in, double *a, double *b, size_t n, hipStream_t s);
+// layout conversion between the reference's separate mu/sigma arrays ([f][j], f rows of
+// D) and the device's feature-major double2 pairs ([j][f]); rows = 1 for the w arrays
+hipError_t pack_pairs(const double *a, const double *b, double2 *out, uint32_t rows, size_t D, hipStream_t s);
+hipError_t unpack_pairs(const double2 *in, double *a, double *b, uint32_t rows, size_t D, hipStream_t s);
 }  // namespace vbk

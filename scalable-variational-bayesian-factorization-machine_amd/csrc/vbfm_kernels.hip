@@ -69,6 +69,41 @@ DEVI bool dnan(double v) { return __builtin_isnan(v); }
 DEVI bool dinf(double v) { return __builtin_isinf(v); }
 
 // ------------------------------------------------------------------------------------
+// row record access. v[0] = (e, q0), v[1] = (tq0, tz0), v[2] = (t, q1), v[3] = (tq1, tz1)
+typedef double2 Rec[4];
+
+DEVI void load_rec(const RowRec *rows, uint32_t r, Rec &v)
+{
+	const double2 *p = reinterpret_cast<const double2 *>(rows + r);
+	v[0] = p[0]; v[1] = p[1]; v[2] = p[2]; v[3] = p[3];
+}
+
+DEVI void store_rec(RowRec *rows, uint32_t r, const Rec &v)
+{
+	double2 *p = reinterpret_cast<double2 *>(rows + r);
+	p[0] = v[0]; p[1] = v[1]; p[2] = v[2]; p[3] = v[3];
+}
+
+template <int S> DEVI double &Q(Rec &v) { return S == 0 ? v[0].y : v[2].y; }
+template <int S> DEVI double &TQ(Rec &v) { return S == 0 ? v[1].x : v[3].x; }
+template <int S> DEVI double &TZ(Rec &v) { return S == 0 ? v[1].y : v[3].y; }
+DEVI double &E(Rec &v) { return v[0].x; }
+DEVI double &T(Rec &v) { return v[2].x; }
+
+// add_main_q term of one entry into slot S (fm_learn_vb.h:374-376); `first` marks the
+// row's smallest feature, where the reference's zeroed cache (:411-415) starts the sum
+template <int S>
+DEVI void qacc(Rec &v, float x, bool first, double2 nx)
+{
+	const double a = nx.x * x;
+	const double b = nx.y * x * x;
+	const double c = nx.x * nx.x * x * x;
+	double &q = Q<S>(v), &tq = TQ<S>(v), &tz = TZ<S>(v);
+	if (first) { q = 0.0 + a; tq = 0.0 + b; tz = 0.0 + c; }
+	else { q += a; tq += b; tz += c; }
+}
+
+// ------------------------------------------------------------------------------------
 // v sweep: update_v (src/libfm/src/fm_learn_vb.h:577-644)
 
 // stats term of one entry (fm_learn_vb.h:592-595)
@@ -104,7 +139,7 @@ DEVI bool v_post(double vm, double vs, double sv_g, double alpha, double mo, dou
 	return true;
 }
 
-// correction of one row (fm_learn_vb.h:623-643); e,q,tq,tz,t updated in place
+// correction of one row (fm_learn_vb.h:623-643)
 DEVI void v_corr(float x, double mo, double so, double mu, double sig, double &e, double &q, double &tq,
                  double &tz, double &t)
 {
@@ -120,39 +155,34 @@ DEVI void v_corr(float x, double mo, double so, double mu, double sig, double &e
 	t += h1 * (mu * mu - mo * mo);
 }
 
-DEVI void load_row(const RowRec *rows, uint32_t r, double &e, double &q, double &tq, double &tz, double &t)
+// everything that happens to one row record of the column after the posterior: the
+// correction (when the guards let it run) and the fused q-cache term of factor f+1
+template <int P, bool NEXT>
+DEVI void v_apply(Rec &v, float x, bool first, bool go, double mo, double so, double mu, double sig, double2 nx)
 {
-	const double2 *p = reinterpret_cast<const double2 *>(rows + r);
-	const double2 a = p[0], b = p[1];
-	e = a.x; q = a.y; tq = b.x; tz = b.y;
-	t = rows[r].t;
+	if (go) v_corr(x, mo, so, mu, sig, E(v), Q<P>(v), TQ<P>(v), TZ<P>(v), T(v));
+	if constexpr (NEXT) qacc<1 - P>(v, x, first, nx);
 }
 
-DEVI void store_row(RowRec *rows, uint32_t r, double e, double q, double tq, double tz, double t)
+template <int P, bool NEXT>
+DEVI void v_apply_serial(const uint2 *col, uint32_t n, RowRec *rows, bool go, double mo, double so, double mu,
+                         double sig, double2 nx)
 {
-	double2 *p = reinterpret_cast<double2 *>(rows + r);
-	p[0] = make_double2(e, q);
-	p[1] = make_double2(tq, tz);
-	rows[r].t = t;
-}
-
-// sequential correction of a column that lists some row more than once: the reference
-// corrects entry after entry, a repeated row seeing its own earlier update
-DEVI void v_corr_serial(const uint2 *col, uint32_t n, RowRec *rows, double mo, double so, double mu, double sig)
-{
+	// a column listing some row twice: the reference corrects entry after entry, a repeated
+	// row seeing its own earlier update
 	for (uint32_t i = 0; i < n; ++i) {
 		const uint2 ent = col[i];
-		double e, q, tq, tz, t;
-		load_row(rows, ent.x, e, q, tq, tz, t);
-		v_corr(ent_x(ent), mo, so, mu, sig, e, q, tq, tz, t);
-		store_row(rows, ent.x, e, q, tq, tz, t);
+		Rec v;
+		load_rec(rows, ent.x & ROW_MASK, v);
+		v_apply<P, NEXT>(v, ent_x(ent), (ent.x & ROW_FIRST) != 0, go, mo, so, mu, sig, nx);
+		store_rec(rows, ent.x & ROW_MASK, v);
 	}
 }
 
 // One workgroup per feature column of the level. Entries i = tid + u*BLOCK for u < R are
-// gathered once and kept in registers from the stats pass to the correction pass; longer
-// columns fall back to a second gather for the overflow entries.
-template <int BLOCK, int R>
+// gathered once (one 64-B record each) and kept in registers from the stats pass to the
+// write-back; longer columns re-gather the overflow entries.
+template <int BLOCK, int R, int P, bool NEXT>
 __global__ __launch_bounds__(BLOCK) void k_v_level_fused(LevelArgs a)
 {
 	__shared__ double lds[2 * (BLOCK / 64)];
@@ -160,12 +190,14 @@ __global__ __launch_bounds__(BLOCK) void k_v_level_fused(LevelArgs a)
 	const uint64_t cb = a.col_ptr[j];
 	const uint32_t n = (uint32_t)(a.col_ptr[j + 1] - cb);
 	const uint2 *col = a.csc + cb;
-	const double2 msj = a.ms[j];
+	const double2 msj = a.ms[(size_t)j * a.ms_stride];
 	const double mo = msj.x, so = msj.y;
+	double2 nx = make_double2(0.0, 0.0);
+	if constexpr (NEXT) nx = a.ms_next[(size_t)j * a.ms_stride_next];
 
 	uint32_t row[R];
 	float xv[R];
-	double re[R], rq[R], rtq[R], rtz[R], rt[R];
+	Rec rec[R];
 #pragma unroll
 	for (int u = 0; u < R; ++u) {
 		const uint32_t i = threadIdx.x + u * BLOCK;
@@ -173,53 +205,47 @@ __global__ __launch_bounds__(BLOCK) void k_v_level_fused(LevelArgs a)
 		if (i < n) { const uint2 ent = col[i]; row[u] = ent.x; xv[u] = ent_x(ent); }
 	}
 #pragma unroll
-	for (int u = 0; u < R; ++u) {
-		const uint32_t i = threadIdx.x + u * BLOCK;
-		if (i < n) load_row(a.rows, row[u], re[u], rq[u], rtq[u], rtz[u], rt[u]);
-	}
+	for (int u = 0; u < R; ++u)
+		if (threadIdx.x + u * BLOCK < n) load_rec(a.rows, row[u] & ROW_MASK, rec[u]);
 	double vm = 0.0, vs = 0.0;
 #pragma unroll
-	for (int u = 0; u < R; ++u) {
-		const uint32_t i = threadIdx.x + u * BLOCK;
-		if (i < n) v_stat(xv[u], re[u], rq[u], rtq[u], mo, so, vm, vs);
-	}
+	for (int u = 0; u < R; ++u)
+		if (threadIdx.x + u * BLOCK < n) v_stat(xv[u], E(rec[u]), Q<P>(rec[u]), TQ<P>(rec[u]), mo, so, vm, vs);
 	for (uint32_t i = threadIdx.x + R * BLOCK; i < n; i += BLOCK) {
 		const uint2 ent = col[i];
-		double e, q, tq, tz, t;
-		load_row(a.rows, ent.x, e, q, tq, tz, t);
-		v_stat(ent_x(ent), e, q, tq, mo, so, vm, vs);
+		Rec v;
+		load_rec(a.rows, ent.x & ROW_MASK, v);
+		v_stat(ent_x(ent), E(v), Q<P>(v), TQ<P>(v), mo, so, vm, vs);
 	}
 	block_sum2<BLOCK>(vm, vs, lds);
 
 	double mu, sig;
 	const double sv_g = a.hyp[(size_t)a.attr_group[j] * a.hyp_stride];
 	const bool go = v_post(vm, vs, sv_g, a.alpha, mo, so, mu, sig, a.counters, threadIdx.x == 0);
-	if (threadIdx.x == 0) a.ms[j] = make_double2(mu, sig);
-	if (!go) return;
+	if (threadIdx.x == 0) a.ms[(size_t)j * a.ms_stride] = make_double2(mu, sig);
+	if (!go && !NEXT) return;
 	if (a.dup[j]) {
 		__syncthreads();
-		if (threadIdx.x == 0) v_corr_serial(col, n, a.rows, mo, so, mu, sig);
+		if (threadIdx.x == 0) v_apply_serial<P, NEXT>(col, n, a.rows, go, mo, so, mu, sig, nx);
 		return;
 	}
 #pragma unroll
-	for (int u = 0; u < R; ++u) {
-		const uint32_t i = threadIdx.x + u * BLOCK;
-		if (i < n) {
-			v_corr(xv[u], mo, so, mu, sig, re[u], rq[u], rtq[u], rtz[u], rt[u]);
-			store_row(a.rows, row[u], re[u], rq[u], rtq[u], rtz[u], rt[u]);
+	for (int u = 0; u < R; ++u)
+		if (threadIdx.x + u * BLOCK < n) {
+			v_apply<P, NEXT>(rec[u], xv[u], (row[u] & ROW_FIRST) != 0, go, mo, so, mu, sig, nx);
+			store_rec(a.rows, row[u] & ROW_MASK, rec[u]);
 		}
-	}
 	for (uint32_t i = threadIdx.x + R * BLOCK; i < n; i += BLOCK) {
 		const uint2 ent = col[i];
-		double e, q, tq, tz, t;
-		load_row(a.rows, ent.x, e, q, tq, tz, t);
-		v_corr(ent_x(ent), mo, so, mu, sig, e, q, tq, tz, t);
-		store_row(a.rows, ent.x, e, q, tq, tz, t);
+		Rec v;
+		load_rec(a.rows, ent.x & ROW_MASK, v);
+		v_apply<P, NEXT>(v, ent_x(ent), (ent.x & ROW_FIRST) != 0, go, mo, so, mu, sig, nx);
+		store_rec(a.rows, ent.x & ROW_MASK, v);
 	}
 }
 
 // split form for the row-sharded multi-GPU mode: stats -> (all-reduce) -> correction
-template <int BLOCK>
+template <int BLOCK, int P>
 __global__ __launch_bounds__(BLOCK) void k_v_level_stats(LevelArgs a)
 {
 	__shared__ double lds[2 * (BLOCK / 64)];
@@ -227,48 +253,50 @@ __global__ __launch_bounds__(BLOCK) void k_v_level_stats(LevelArgs a)
 	const uint64_t cb = a.col_ptr[j];
 	const uint32_t n = (uint32_t)(a.col_ptr[j + 1] - cb);
 	const uint2 *col = a.csc + cb;
-	const double2 msj = a.ms[j];
+	const double2 msj = a.ms[(size_t)j * a.ms_stride];
 	double vm = 0.0, vs = 0.0;
 	for (uint32_t i = threadIdx.x; i < n; i += BLOCK) {
 		const uint2 ent = col[i];
-		double e, q, tq, tz, t;
-		load_row(a.rows, ent.x, e, q, tq, tz, t);
-		v_stat(ent_x(ent), e, q, tq, msj.x, msj.y, vm, vs);
+		Rec v;
+		load_rec(a.rows, ent.x & ROW_MASK, v);
+		v_stat(ent_x(ent), E(v), Q<P>(v), TQ<P>(v), msj.x, msj.y, vm, vs);
 	}
 	block_sum2<BLOCK>(vm, vs, lds);
 	if (threadIdx.x == 0) a.stats[blockIdx.x] = make_double2(vm, vs);
 }
 
-template <int BLOCK>
+template <int BLOCK, int P, bool NEXT>
 __global__ __launch_bounds__(BLOCK) void k_v_level_correct(LevelArgs a)
 {
 	const uint32_t j = a.feats[blockIdx.x];
 	const uint64_t cb = a.col_ptr[j];
 	const uint32_t n = (uint32_t)(a.col_ptr[j + 1] - cb);
 	const uint2 *col = a.csc + cb;
-	const double2 msj = a.ms[j];
+	const double2 msj = a.ms[(size_t)j * a.ms_stride];
 	const double2 st = a.stats[blockIdx.x];
+	double2 nx = make_double2(0.0, 0.0);
+	if constexpr (NEXT) nx = a.ms_next[(size_t)j * a.ms_stride_next];
 	double mu, sig;
 	const double sv_g = a.hyp[(size_t)a.attr_group[j] * a.hyp_stride];
 	const bool go = v_post(st.x, st.y, sv_g, a.alpha, msj.x, msj.y, mu, sig, a.counters, threadIdx.x == 0);
-	__syncthreads();
-	if (threadIdx.x == 0) a.ms[j] = make_double2(mu, sig);
-	if (!go) return;
+	if (threadIdx.x == 0) a.ms[(size_t)j * a.ms_stride] = make_double2(mu, sig);
+	if (!go && !NEXT) return;
 	if (a.dup[j]) {
-		if (threadIdx.x == 0) v_corr_serial(col, n, a.rows, msj.x, msj.y, mu, sig);
+		if (threadIdx.x == 0) v_apply_serial<P, NEXT>(col, n, a.rows, go, msj.x, msj.y, mu, sig, nx);
 		return;
 	}
 	for (uint32_t i = threadIdx.x; i < n; i += BLOCK) {
 		const uint2 ent = col[i];
-		double e, q, tq, tz, t;
-		load_row(a.rows, ent.x, e, q, tq, tz, t);
-		v_corr(ent_x(ent), msj.x, msj.y, mu, sig, e, q, tq, tz, t);
-		store_row(a.rows, ent.x, e, q, tq, tz, t);
+		Rec v;
+		load_rec(a.rows, ent.x & ROW_MASK, v);
+		v_apply<P, NEXT>(v, ent_x(ent), (ent.x & ROW_FIRST) != 0, go, msj.x, msj.y, mu, sig, nx);
+		store_rec(a.rows, ent.x & ROW_MASK, v);
 	}
 }
 
 // ------------------------------------------------------------------------------------
-// w sweep: update_w (fm_learn_vb.h:527-574)
+// w sweep: update_w (fm_learn_vb.h:527-574). With NEXT the sweep also accumulates the
+// q-cache of factor 0 into slot 0 (add_main_q(train, 0), fm_learn_vb.h:354-381).
 DEVI void w_stat(float x, double e, double mo, double &wm, double &ws)
 {
 	wm += x * (e + x * mo);
@@ -297,14 +325,31 @@ DEVI bool w_post(double wm, double ws, double sw_g, double alpha, double mo, dou
 	return true;
 }
 
-DEVI void w_corr(float x, double mo, double so, double mu, double sig, double &e, double &t)
+template <bool NEXT>
+DEVI void w_apply(Rec &v, float x, bool first, bool go, double mo, double so, double mu, double sig, double2 nx)
 {
-	const double h = x;
-	e += h * (mo - mu);
-	t += h * h * (sig - so);
+	if (go) {
+		const double h = x;
+		E(v) += h * (mo - mu);
+		T(v) += h * h * (sig - so);
+	}
+	if constexpr (NEXT) qacc<0>(v, x, first, nx);
 }
 
-template <int BLOCK, int R>
+template <bool NEXT>
+DEVI void w_apply_serial(const uint2 *col, uint32_t n, RowRec *rows, bool go, double mo, double so, double mu,
+                         double sig, double2 nx)
+{
+	for (uint32_t i = 0; i < n; ++i) {
+		const uint2 ent = col[i];
+		Rec v;
+		load_rec(rows, ent.x & ROW_MASK, v);
+		w_apply<NEXT>(v, ent_x(ent), (ent.x & ROW_FIRST) != 0, go, mo, so, mu, sig, nx);
+		store_rec(rows, ent.x & ROW_MASK, v);
+	}
+}
+
+template <int BLOCK, int R, bool NEXT>
 __global__ __launch_bounds__(BLOCK) void k_w_level_fused(LevelArgs a)
 {
 	__shared__ double lds[2 * (BLOCK / 64)];
@@ -312,11 +357,13 @@ __global__ __launch_bounds__(BLOCK) void k_w_level_fused(LevelArgs a)
 	const uint64_t cb = a.col_ptr[j];
 	const uint32_t n = (uint32_t)(a.col_ptr[j + 1] - cb);
 	const uint2 *col = a.csc + cb;
-	const double2 msj = a.ms[j];
+	const double2 msj = a.ms[(size_t)j * a.ms_stride];
 	const double mo = msj.x, so = msj.y;
+	double2 nx = make_double2(0.0, 0.0);
+	if constexpr (NEXT) nx = a.ms_next[(size_t)j * a.ms_stride_next];
 	uint32_t row[R];
 	float xv[R];
-	double re[R], rt[R];
+	Rec rec[R];
 #pragma unroll
 	for (int u = 0; u < R; ++u) {
 		const uint32_t i = threadIdx.x + u * BLOCK;
@@ -324,51 +371,39 @@ __global__ __launch_bounds__(BLOCK) void k_w_level_fused(LevelArgs a)
 		if (i < n) { const uint2 ent = col[i]; row[u] = ent.x; xv[u] = ent_x(ent); }
 	}
 #pragma unroll
-	for (int u = 0; u < R; ++u) {
-		const uint32_t i = threadIdx.x + u * BLOCK;
-		if (i < n) { re[u] = a.rows[row[u]].e; rt[u] = a.rows[row[u]].t; }
-	}
+	for (int u = 0; u < R; ++u)
+		if (threadIdx.x + u * BLOCK < n) load_rec(a.rows, row[u] & ROW_MASK, rec[u]);
 	double wm = 0.0, ws = 0.0;
 #pragma unroll
-	for (int u = 0; u < R; ++u) {
-		const uint32_t i = threadIdx.x + u * BLOCK;
-		if (i < n) w_stat(xv[u], re[u], mo, wm, ws);
-	}
+	for (int u = 0; u < R; ++u)
+		if (threadIdx.x + u * BLOCK < n) w_stat(xv[u], E(rec[u]), mo, wm, ws);
 	for (uint32_t i = threadIdx.x + R * BLOCK; i < n; i += BLOCK) {
 		const uint2 ent = col[i];
-		w_stat(ent_x(ent), a.rows[ent.x].e, mo, wm, ws);
+		w_stat(ent_x(ent), a.rows[ent.x & ROW_MASK].e, mo, wm, ws);
 	}
 	block_sum2<BLOCK>(wm, ws, lds);
 	double mu, sig;
 	const double sw_g = a.hyp[(size_t)a.attr_group[j] * a.hyp_stride];
 	const bool go = w_post(wm, ws, sw_g, a.alpha, mo, so, mu, sig, a.counters, threadIdx.x == 0);
-	if (threadIdx.x == 0) a.ms[j] = make_double2(mu, sig);
-	if (!go) return;
+	if (threadIdx.x == 0) a.ms[(size_t)j * a.ms_stride] = make_double2(mu, sig);
+	if (!go && !NEXT) return;
 	if (a.dup[j]) {
 		__syncthreads();
-		if (threadIdx.x == 0)
-			for (uint32_t i = 0; i < n; ++i) {
-				const uint2 ent = col[i];
-				double e = a.rows[ent.x].e, t = a.rows[ent.x].t;
-				w_corr(ent_x(ent), mo, so, mu, sig, e, t);
-				a.rows[ent.x].e = e; a.rows[ent.x].t = t;
-			}
+		if (threadIdx.x == 0) w_apply_serial<NEXT>(col, n, a.rows, go, mo, so, mu, sig, nx);
 		return;
 	}
 #pragma unroll
-	for (int u = 0; u < R; ++u) {
-		const uint32_t i = threadIdx.x + u * BLOCK;
-		if (i < n) {
-			w_corr(xv[u], mo, so, mu, sig, re[u], rt[u]);
-			a.rows[row[u]].e = re[u];
-			a.rows[row[u]].t = rt[u];
+	for (int u = 0; u < R; ++u)
+		if (threadIdx.x + u * BLOCK < n) {
+			w_apply<NEXT>(rec[u], xv[u], (row[u] & ROW_FIRST) != 0, go, mo, so, mu, sig, nx);
+			store_rec(a.rows, row[u] & ROW_MASK, rec[u]);
 		}
-	}
 	for (uint32_t i = threadIdx.x + R * BLOCK; i < n; i += BLOCK) {
 		const uint2 ent = col[i];
-		double e = a.rows[ent.x].e, t = a.rows[ent.x].t;
-		w_corr(ent_x(ent), mo, so, mu, sig, e, t);
-		a.rows[ent.x].e = e; a.rows[ent.x].t = t;
+		Rec v;
+		load_rec(a.rows, ent.x & ROW_MASK, v);
+		w_apply<NEXT>(v, ent_x(ent), (ent.x & ROW_FIRST) != 0, go, mo, so, mu, sig, nx);
+		store_rec(a.rows, ent.x & ROW_MASK, v);
 	}
 }
 
@@ -380,46 +415,42 @@ __global__ __launch_bounds__(BLOCK) void k_w_level_stats(LevelArgs a)
 	const uint64_t cb = a.col_ptr[j];
 	const uint32_t n = (uint32_t)(a.col_ptr[j + 1] - cb);
 	const uint2 *col = a.csc + cb;
-	const double mo = a.ms[j].x;
+	const double mo = a.ms[(size_t)j * a.ms_stride].x;
 	double wm = 0.0, ws = 0.0;
 	for (uint32_t i = threadIdx.x; i < n; i += BLOCK) {
 		const uint2 ent = col[i];
-		w_stat(ent_x(ent), a.rows[ent.x].e, mo, wm, ws);
+		w_stat(ent_x(ent), a.rows[ent.x & ROW_MASK].e, mo, wm, ws);
 	}
 	block_sum2<BLOCK>(wm, ws, lds);
 	if (threadIdx.x == 0) a.stats[blockIdx.x] = make_double2(wm, ws);
 }
 
-template <int BLOCK>
+template <int BLOCK, bool NEXT>
 __global__ __launch_bounds__(BLOCK) void k_w_level_correct(LevelArgs a)
 {
 	const uint32_t j = a.feats[blockIdx.x];
 	const uint64_t cb = a.col_ptr[j];
 	const uint32_t n = (uint32_t)(a.col_ptr[j + 1] - cb);
 	const uint2 *col = a.csc + cb;
-	const double2 msj = a.ms[j];
+	const double2 msj = a.ms[(size_t)j * a.ms_stride];
 	const double2 st = a.stats[blockIdx.x];
+	double2 nx = make_double2(0.0, 0.0);
+	if constexpr (NEXT) nx = a.ms_next[(size_t)j * a.ms_stride_next];
 	double mu, sig;
 	const double sw_g = a.hyp[(size_t)a.attr_group[j] * a.hyp_stride];
 	const bool go = w_post(st.x, st.y, sw_g, a.alpha, msj.x, msj.y, mu, sig, a.counters, threadIdx.x == 0);
-	__syncthreads();
-	if (threadIdx.x == 0) a.ms[j] = make_double2(mu, sig);
-	if (!go) return;
+	if (threadIdx.x == 0) a.ms[(size_t)j * a.ms_stride] = make_double2(mu, sig);
+	if (!go && !NEXT) return;
 	if (a.dup[j]) {
-		if (threadIdx.x == 0)
-			for (uint32_t i = 0; i < n; ++i) {
-				const uint2 ent = col[i];
-				double e = a.rows[ent.x].e, t = a.rows[ent.x].t;
-				w_corr(ent_x(ent), msj.x, msj.y, mu, sig, e, t);
-				a.rows[ent.x].e = e; a.rows[ent.x].t = t;
-			}
+		if (threadIdx.x == 0) w_apply_serial<NEXT>(col, n, a.rows, go, msj.x, msj.y, mu, sig, nx);
 		return;
 	}
 	for (uint32_t i = threadIdx.x; i < n; i += BLOCK) {
 		const uint2 ent = col[i];
-		double e = a.rows[ent.x].e, t = a.rows[ent.x].t;
-		w_corr(ent_x(ent), msj.x, msj.y, mu, sig, e, t);
-		a.rows[ent.x].e = e; a.rows[ent.x].t = t;
+		Rec v;
+		load_rec(a.rows, ent.x & ROW_MASK, v);
+		w_apply<NEXT>(v, ent_x(ent), (ent.x & ROW_FIRST) != 0, go, msj.x, msj.y, mu, sig, nx);
+		store_rec(a.rows, ent.x & ROW_MASK, v);
 	}
 }
 
@@ -428,8 +459,8 @@ __global__ __launch_bounds__(BLOCK) void k_w_level_correct(LevelArgs a)
 // Row-parallel over the feature-sorted CSR: each row sums its entries in ascending
 // feature order, exactly the order the reference's column loop adds them in.
 __global__ __launch_bounds__(256) void k_qcache(const uint64_t *__restrict__ row_ptr, const uint2 *__restrict__ csr,
-                                                 const double2 *__restrict__ ms_f, RowRec *__restrict__ rows,
-                                                 uint32_t n)
+                                                 const double2 *__restrict__ ms_f, uint32_t stride,
+                                                 RowRec *__restrict__ rows, uint32_t n, int slot)
 {
 	const uint32_t r = blockIdx.x * 256u + threadIdx.x;
 	if (r >= n) return;
@@ -438,37 +469,57 @@ __global__ __launch_bounds__(256) void k_qcache(const uint64_t *__restrict__ row
 	for (uint64_t p = b; p < e; ++p) {
 		const uint2 ent = csr[p];
 		const float x = ent_x(ent);
-		const double2 m = ms_f[ent.x];
+		const double2 m = ms_f[(size_t)ent.x * stride];
 		q += m.x * x;
 		tq += m.y * x * x;
 		tz += m.x * m.x * x * x;
 	}
-	rows[r].q = q;
-	reinterpret_cast<double2 *>(rows + r)[1] = make_double2(tq, tz);
+	if (slot == 0) {
+		rows[r].q = q;
+		reinterpret_cast<double2 *>(rows + r)[1] = make_double2(tq, tz);
+	} else {
+		rows[r].q1 = q;
+		reinterpret_cast<double2 *>(rows + r)[3] = make_double2(tq, tz);
+	}
+}
+
+// flag the CSC entry of each row's first (smallest-feature) CSR entry: binary search for the
+// row in that column (rows ascend within a column; the first of repeated rows is taken)
+__global__ void k_mark_first(const uint64_t *row_ptr, const uint2 *csr, const uint64_t *col_ptr, uint2 *csc, uint32_t n)
+{
+	const uint32_t r = blockIdx.x * 256u + threadIdx.x;
+	if (r >= n) return;
+	const uint64_t b = row_ptr[r];
+	if (row_ptr[r + 1] == b) return;
+	const uint32_t j = csr[b].x;
+	uint64_t lo = col_ptr[j], hi = col_ptr[j + 1];
+	while (lo < hi) {
+		const uint64_t mid = (lo + hi) >> 1;
+		if ((csc[mid].x & ROW_MASK) < r) lo = mid + 1; else hi = mid;
+	}
+	csc[lo].x |= ROW_FIRST;
 }
 
 // predict_data_and_write_to_eterms for one data set (fm_learn_vb.h:70-203), row-parallel.
+// Exact form: the reference's order (factor-major sums, each over the row's ascending ids).
 __global__ __launch_bounds__(256) void k_predict_e(const uint64_t *__restrict__ row_ptr, const uint2 *__restrict__ csr,
                                                     const double2 *__restrict__ ms_v, const double2 *__restrict__ ms_w,
-                                                    uint32_t D, int k, int k1, int k0, double mu0,
-                                                    double *__restrict__ out, uint32_t n)
+                                                    int k, int k1, int k0, double mu0, double *__restrict__ out, uint32_t n)
 {
 	const uint32_t r = blockIdx.x * 256u + threadIdx.x;
 	if (r >= n) return;
 	const uint64_t b = row_ptr[r], en = row_ptr[r + 1];
 	double e = 0.0;
 	for (int f = 0; f < k; ++f) {                          // (1) :93-133
-		const double2 *m = ms_v + (size_t)f * D;
 		double q = 0.0;
-		for (uint64_t p = b; p < en; ++p) { const uint2 ent = csr[p]; q += m[ent.x].x * ent_x(ent); }
+		for (uint64_t p = b; p < en; ++p) { const uint2 ent = csr[p]; q += ms_v[(size_t)ent.x * k + f].x * ent_x(ent); }
 		e += 0.5 * q * q;
 	}
 	double q = 0.0;
 	for (int f = 0; f < k; ++f) {                          // (2) :136-163
-		const double2 *m = ms_v + (size_t)f * D;
 		for (uint64_t p = b; p < en; ++p) {
 			const uint2 ent = csr[p];
-			const double v = m[ent.x].x;
+			const double v = ms_v[(size_t)ent.x * k + f].x;
 			const float x = ent_x(ent);
 			q -= 0.5 * v * v * x * x;
 		}
@@ -480,22 +531,62 @@ __global__ __launch_bounds__(256) void k_predict_e(const uint64_t *__restrict__ 
 	out[r] = e;
 }
 
+// Blocked form for large data sets: one pass over the row per block of C factors reading
+// C contiguous {mu, sigma} pairs per entry; every per-factor sum keeps the reference's
+// order, the -1/2 sum v^2 x^2 term is summed block-major.
+template <int C>
+__global__ __launch_bounds__(256) void k_predict_e_blocked(const uint64_t *__restrict__ row_ptr,
+                                                            const uint2 *__restrict__ csr,
+                                                            const double2 *__restrict__ ms_v,
+                                                            const double2 *__restrict__ ms_w, int k, int k1, int k0,
+                                                            double mu0, double *__restrict__ out, uint32_t n)
+{
+	const uint32_t r = blockIdx.x * 256u + threadIdx.x;
+	if (r >= n) return;
+	const uint64_t b = row_ptr[r], en = row_ptr[r + 1];
+	double e = 0.0, qq = 0.0;
+	for (int f0 = 0; f0 < k; f0 += C) {
+		double q[C];
+#pragma unroll
+		for (int c = 0; c < C; ++c) q[c] = 0.0;
+		for (uint64_t p = b; p < en; ++p) {
+			const uint2 ent = csr[p];
+			const float x = ent_x(ent);
+			const double2 *m = ms_v + (size_t)ent.x * k + f0;
+#pragma unroll
+			for (int c = 0; c < C; ++c)
+				if (f0 + c < k) {
+					const double v = m[c].x;
+					q[c] += v * x;
+					qq -= 0.5 * v * v * x * x;
+				}
+		}
+#pragma unroll
+		for (int c = 0; c < C; ++c)
+			if (f0 + c < k) e += 0.5 * q[c] * q[c];
+	}
+	if (k1)
+		for (uint64_t p = b; p < en; ++p) { const uint2 ent = csr[p]; qq += ms_w[ent.x].x * ent_x(ent); }
+	e = e + qq;
+	if (k0) e += mu0;
+	out[r] = e;
+}
+
 // predict_t_and_write_to_qterms (fm_learn_vb.h:207-312), row-parallel; writes rows[].t
 __global__ __launch_bounds__(256) void k_predict_t(const uint64_t *__restrict__ row_ptr, const uint2 *__restrict__ csr,
                                                     const double2 *__restrict__ ms_v, const double2 *__restrict__ ms_w,
-                                                    uint32_t D, int k, int k1, int k0, double s0d,
-                                                    RowRec *__restrict__ rows, uint32_t n)
+                                                    int k, int k1, int k0, double s0d, RowRec *__restrict__ rows,
+                                                    uint32_t n)
 {
 	const uint32_t r = blockIdx.x * 256u + threadIdx.x;
 	if (r >= n) return;
 	const uint64_t b = row_ptr[r], en = row_ptr[r + 1];
 	double t = 0.0;
 	for (int f = 0; f < k; ++f) {                          // (1) :222-254
-		const double2 *m = ms_v + (size_t)f * D;
 		double q = 0.0, z = 0.0;
 		for (uint64_t p = b; p < en; ++p) {
 			const uint2 ent = csr[p];
-			const double2 vm = m[ent.x];
+			const double2 vm = ms_v[(size_t)ent.x * k + f];
 			const float x = ent_x(ent);
 			q += vm.x * x * vm.x * x;
 			z += vm.y * x * x;
@@ -504,10 +595,9 @@ __global__ __launch_bounds__(256) void k_predict_t(const uint64_t *__restrict__ 
 	}
 	double q = 0.0;
 	for (int f = 0; f < k; ++f) {                          // (2) :257-281
-		const double2 *m = ms_v + (size_t)f * D;
 		for (uint64_t p = b; p < en; ++p) {
 			const uint2 ent = csr[p];
-			const double2 vm = m[ent.x];
+			const double2 vm = ms_v[(size_t)ent.x * k + f];
 			const float x = ent_x(ent);
 			q -= (vm.x * vm.x * x * x * x * x * vm.y + 0.5 * x * x * x * x * vm.y * vm.y);
 		}
@@ -519,6 +609,49 @@ __global__ __launch_bounds__(256) void k_predict_t(const uint64_t *__restrict__ 
 			q += ms_w[ent.x].y * x * x;
 		}
 	t = t + q;                                             // :304-311
+	if (k0) t += s0d;
+	rows[r].t = t;
+}
+
+template <int C>
+__global__ __launch_bounds__(256) void k_predict_t_blocked(const uint64_t *__restrict__ row_ptr,
+                                                            const uint2 *__restrict__ csr,
+                                                            const double2 *__restrict__ ms_v,
+                                                            const double2 *__restrict__ ms_w, int k, int k1, int k0,
+                                                            double s0d, RowRec *__restrict__ rows, uint32_t n)
+{
+	const uint32_t r = blockIdx.x * 256u + threadIdx.x;
+	if (r >= n) return;
+	const uint64_t b = row_ptr[r], en = row_ptr[r + 1];
+	double t = 0.0, qq = 0.0;
+	for (int f0 = 0; f0 < k; f0 += C) {
+		double q[C], z[C];
+#pragma unroll
+		for (int c = 0; c < C; ++c) { q[c] = 0.0; z[c] = 0.0; }
+		for (uint64_t p = b; p < en; ++p) {
+			const uint2 ent = csr[p];
+			const float x = ent_x(ent);
+			const double2 *m = ms_v + (size_t)ent.x * k + f0;
+#pragma unroll
+			for (int c = 0; c < C; ++c)
+				if (f0 + c < k) {
+					const double2 vm = m[c];
+					q[c] += vm.x * x * vm.x * x;
+					z[c] += vm.y * x * x;
+					qq -= (vm.x * vm.x * x * x * x * x * vm.y + 0.5 * x * x * x * x * vm.y * vm.y);
+				}
+		}
+#pragma unroll
+		for (int c = 0; c < C; ++c)
+			if (f0 + c < k) t += (0.5 * z[c] * z[c] + z[c] * q[c]);
+	}
+	if (k1)
+		for (uint64_t p = b; p < en; ++p) {
+			const uint2 ent = csr[p];
+			const float x = ent_x(ent);
+			qq += ms_w[ent.x].y * x * x;
+		}
+	t = t + qq;
 	if (k0) t += s0d;
 	rows[r].t = t;
 }
@@ -599,11 +732,12 @@ __global__ __launch_bounds__(BLOCK) void k_param_sums(const double2 *ms_w, const
 {
 	__shared__ double lds[BLOCK / 64];
 	const vbk::Chunk c = chunks[blockIdx.x];
-	const double2 *ms = c.f < 0 ? ms_w : ms_v + (size_t)c.f * D;
+	const double2 *ms = c.f < 0 ? ms_w : ms_v + c.f;       // ms_v is feature-major: [j*k + f]
+	const size_t stride = c.f < 0 ? 1 : (size_t)k;
 	const double hs = mode == 0 ? 0.0 : (c.f < 0 ? hyp_w[c.g] : hyp_v[(size_t)c.g * k + c.f]);
 	double s = 0.0;
 	for (uint32_t i = c.begin + threadIdx.x; i < c.end; i += BLOCK) {
-		const double2 m = ms[perm[i]];
+		const double2 m = ms[(size_t)perm[i] * stride];
 		if (mode == 0) s += m.x * m.x + m.y;
 		else s += -0.5 * hs * (m.x * m.x + m.y) + 0.5 * log(m.y * hs) + .5;
 	}
@@ -725,16 +859,22 @@ __global__ void k_init_normal_pairs(double2 *ms, size_t n, uint64_t seed, uint64
 	ms[i] = make_double2(0.1 * z, .02);
 }
 
-__global__ void k_pack(const double *a, const double *b, double2 *out, size_t n)
+// out[j*rows + f] = {a[f*D + j], b[f*D + j]}
+__global__ void k_pack(const double *a, const double *b, double2 *out, uint32_t rows, size_t D)
 {
 	const size_t i = (size_t)blockIdx.x * 256u + threadIdx.x;
-	if (i < n) out[i] = make_double2(a[i], b[i]);
+	if (i >= (size_t)rows * D) return;
+	const size_t j = i / rows, f = i % rows;
+	out[i] = make_double2(a[f * D + j], b[f * D + j]);
 }
 
-__global__ void k_unpack(const double2 *in, double *a, double *b, size_t n)
+__global__ void k_unpack(const double2 *in, double *a, double *b, uint32_t rows, size_t D)
 {
 	const size_t i = (size_t)blockIdx.x * 256u + threadIdx.x;
-	if (i < n) { a[i] = in[i].x; b[i] = in[i].y; }
+	if (i >= (size_t)rows * D) return;
+	const size_t j = i / rows, f = i % rows;
+	a[f * D + j] = in[i].x;
+	b[f * D + j] = in[i].y;
 }
 
 inline unsigned grid_for(uint64_t n, unsigned block = 256) { return (unsigned)((n + block - 1) / block); }
@@ -744,30 +884,58 @@ inline unsigned grid_for(uint64_t n, unsigned block = 256) { return (unsigned)((
 // ------------------------------------------------------------------------------------
 namespace vbk {
 
-// Column-length-adaptive launch: one wave per column for short levels, four waves for
-// longer ones (average entries per column of the level decides).
+// Column-length-adaptive launch shape: threads per column and entries held per thread
+// from the level's mean column length.
+template <int P, bool NEXT>
+hipError_t launch_v_fused(const LevelArgs &a, hipStream_t s)
+{
+	if (a.avg_len <= 96) k_v_level_fused<64, 2, P, NEXT><<<a.nfeat, 64, 0, s>>>(a);
+	else if (a.avg_len <= 320) k_v_level_fused<256, 1, P, NEXT><<<a.nfeat, 256, 0, s>>>(a);
+	else if (a.avg_len <= 640) k_v_level_fused<256, 2, P, NEXT><<<a.nfeat, 256, 0, s>>>(a);
+	else k_v_level_fused<512, 2, P, NEXT><<<a.nfeat, 512, 0, s>>>(a);
+	return hipGetLastError();
+}
+
+template <bool NEXT>
+hipError_t launch_w_fused(const LevelArgs &a, hipStream_t s)
+{
+	if (a.avg_len <= 96) k_w_level_fused<64, 2, NEXT><<<a.nfeat, 64, 0, s>>>(a);
+	else if (a.avg_len <= 320) k_w_level_fused<256, 1, NEXT><<<a.nfeat, 256, 0, s>>>(a);
+	else if (a.avg_len <= 640) k_w_level_fused<256, 2, NEXT><<<a.nfeat, 256, 0, s>>>(a);
+	else k_w_level_fused<512, 2, NEXT><<<a.nfeat, 512, 0, s>>>(a);
+	return hipGetLastError();
+}
+
 hipError_t v_level_fused(const LevelArgs &a, hipStream_t s)
 {
 	if (a.nfeat == 0) return hipSuccess;
-	k_v_level_fused<256, 4><<<a.nfeat, 256, 0, s>>>(a);
-	return hipGetLastError();
+	const bool nx = a.ms_next != nullptr;
+	if (a.slot == 0) return nx ? launch_v_fused<0, true>(a, s) : launch_v_fused<0, false>(a, s);
+	return nx ? launch_v_fused<1, true>(a, s) : launch_v_fused<1, false>(a, s);
 }
 hipError_t w_level_fused(const LevelArgs &a, hipStream_t s)
 {
 	if (a.nfeat == 0) return hipSuccess;
-	k_w_level_fused<256, 4><<<a.nfeat, 256, 0, s>>>(a);
-	return hipGetLastError();
+	return a.ms_next ? launch_w_fused<true>(a, s) : launch_w_fused<false>(a, s);
 }
 hipError_t v_level_stats(const LevelArgs &a, hipStream_t s)
 {
 	if (a.nfeat == 0) return hipSuccess;
-	k_v_level_stats<256><<<a.nfeat, 256, 0, s>>>(a);
+	if (a.slot == 0) k_v_level_stats<256, 0><<<a.nfeat, 256, 0, s>>>(a);
+	else k_v_level_stats<256, 1><<<a.nfeat, 256, 0, s>>>(a);
 	return hipGetLastError();
 }
 hipError_t v_level_correct(const LevelArgs &a, hipStream_t s)
 {
 	if (a.nfeat == 0) return hipSuccess;
-	k_v_level_correct<256><<<a.nfeat, 256, 0, s>>>(a);
+	const bool nx = a.ms_next != nullptr;
+	if (a.slot == 0) {
+		if (nx) k_v_level_correct<256, 0, true><<<a.nfeat, 256, 0, s>>>(a);
+		else k_v_level_correct<256, 0, false><<<a.nfeat, 256, 0, s>>>(a);
+	} else {
+		if (nx) k_v_level_correct<256, 1, true><<<a.nfeat, 256, 0, s>>>(a);
+		else k_v_level_correct<256, 1, false><<<a.nfeat, 256, 0, s>>>(a);
+	}
 	return hipGetLastError();
 }
 hipError_t w_level_stats(const LevelArgs &a, hipStream_t s)
@@ -779,30 +947,42 @@ hipError_t w_level_stats(const LevelArgs &a, hipStream_t s)
 hipError_t w_level_correct(const LevelArgs &a, hipStream_t s)
 {
 	if (a.nfeat == 0) return hipSuccess;
-	k_w_level_correct<256><<<a.nfeat, 256, 0, s>>>(a);
+	if (a.ms_next) k_w_level_correct<256, true><<<a.nfeat, 256, 0, s>>>(a);
+	else k_w_level_correct<256, false><<<a.nfeat, 256, 0, s>>>(a);
 	return hipGetLastError();
 }
 
-hipError_t qcache(const uint64_t *row_ptr, const uint2 *csr, const double2 *ms_f, RowRec *rows, uint32_t n, hipStream_t s)
+hipError_t qcache(const uint64_t *row_ptr, const uint2 *csr, const double2 *ms_f, uint32_t stride, RowRec *rows,
+                  uint32_t n, int slot, hipStream_t s)
 {
 	if (n == 0) return hipSuccess;
-	k_qcache<<<grid_for(n), 256, 0, s>>>(row_ptr, csr, ms_f, rows, n);
+	k_qcache<<<grid_for(n), 256, 0, s>>>(row_ptr, csr, ms_f, stride, rows, n, slot);
 	return hipGetLastError();
 }
 
-hipError_t predict_e(const uint64_t *row_ptr, const uint2 *csr, const double2 *ms_v, const double2 *ms_w, uint32_t D,
-                     int k, int k1, int k0, double mu0, double *out, uint32_t n, hipStream_t s)
+hipError_t mark_first(const uint64_t *row_ptr, const uint2 *csr, const uint64_t *col_ptr, uint2 *csc, uint32_t n,
+                      hipStream_t s)
 {
 	if (n == 0) return hipSuccess;
-	k_predict_e<<<grid_for(n), 256, 0, s>>>(row_ptr, csr, ms_v, ms_w, D, k, k1, k0, mu0, out, n);
+	k_mark_first<<<grid_for(n), 256, 0, s>>>(row_ptr, csr, col_ptr, csc, n);
 	return hipGetLastError();
 }
 
-hipError_t predict_t(const uint64_t *row_ptr, const uint2 *csr, const double2 *ms_v, const double2 *ms_w, uint32_t D,
-                     int k, int k1, int k0, double s0d, RowRec *rows, uint32_t n, hipStream_t s)
+hipError_t predict_e(const uint64_t *row_ptr, const uint2 *csr, const double2 *ms_v, const double2 *ms_w, int k, int k1,
+                     int k0, double mu0, double *out, uint32_t n, int blocked, hipStream_t s)
 {
 	if (n == 0) return hipSuccess;
-	k_predict_t<<<grid_for(n), 256, 0, s>>>(row_ptr, csr, ms_v, ms_w, D, k, k1, k0, s0d, rows, n);
+	if (blocked) k_predict_e_blocked<8><<<grid_for(n), 256, 0, s>>>(row_ptr, csr, ms_v, ms_w, k, k1, k0, mu0, out, n);
+	else k_predict_e<<<grid_for(n), 256, 0, s>>>(row_ptr, csr, ms_v, ms_w, k, k1, k0, mu0, out, n);
+	return hipGetLastError();
+}
+
+hipError_t predict_t(const uint64_t *row_ptr, const uint2 *csr, const double2 *ms_v, const double2 *ms_w, int k, int k1,
+                     int k0, double s0d, RowRec *rows, uint32_t n, int blocked, hipStream_t s)
+{
+	if (n == 0) return hipSuccess;
+	if (blocked) k_predict_t_blocked<8><<<grid_for(n), 256, 0, s>>>(row_ptr, csr, ms_v, ms_w, k, k1, k0, s0d, rows, n);
+	else k_predict_t<<<grid_for(n), 256, 0, s>>>(row_ptr, csr, ms_v, ms_w, k, k1, k0, s0d, rows, n);
 	return hipGetLastError();
 }
 
@@ -921,17 +1101,19 @@ hipError_t init_normal_pairs(double2 *ms, size_t n, uint64_t seed, uint64_t stre
 	return hipGetLastError();
 }
 
-hipError_t pack_pairs(const double *a, const double *b, double2 *out, size_t n, hipStream_t s)
+hipError_t pack_pairs(const double *a, const double *b, double2 *out, uint32_t rows, size_t D, hipStream_t s)
 {
+	const size_t n = (size_t)rows * D;
 	if (n == 0) return hipSuccess;
-	k_pack<<<grid_for(n), 256, 0, s>>>(a, b, out, n);
+	k_pack<<<grid_for(n), 256, 0, s>>>(a, b, out, rows, D);
 	return hipGetLastError();
 }
 
-hipError_t unpack_pairs(const double2 *in, double *a, double *b, size_t n, hipStream_t s)
+hipError_t unpack_pairs(const double2 *in, double *a, double *b, uint32_t rows, size_t D, hipStream_t s)
 {
+	const size_t n = (size_t)rows * D;
 	if (n == 0) return hipSuccess;
-	k_unpack<<<grid_for(n), 256, 0, s>>>(in, a, b, n);
+	k_unpack<<<grid_for(n), 256, 0, s>>>(in, a, b, rows, D);
 	return hipGetLastError();
 }
 

@@ -49,13 +49,16 @@ def oracle_learner(tr_path, te_path, dim, seed, init_stdev, attr_group=None):
     return vb
 
 
-@pytest.mark.parametrize("case", ["tiny", "tiny_dup"])
-def test_update_all_steps_vs_oracle(case):
+@pytest.mark.parametrize("case,dim", [("tiny", "1,1,3"), ("tiny_dup", "1,1,3"), ("tiny", "1,0,3"),
+                                      ("tiny_dup", "0,0,3")])
+def test_update_all_steps_vs_oracle(case, dim):
+    """update_all step by step. The q-cache of factor f is accumulated inside the previous
+    sweep (w sweep for f = 0 when k1, else the row-parallel kernel): bit-exact."""
     d = os.path.join(GOLDEN, case)
     trp, tep = os.path.join(d, "train.libfm"), os.path.join(d, "test.libfm")
     train, test = vbfm.DataSubset.load(trp), vbfm.DataSubset.load(tep)
-    g = gpu_learner(train, test, "1,1,3", 5, 0.1)
-    o = oracle_learner(trp, tep, "1,1,3", 5, 0.1)
+    g = gpu_learner(train, test, dim, 5, 0.1)
+    o = oracle_learner(trp, tep, dim, 5, 0.1)
     po, pg = o.params(), g.get_params()
     for key in ("mu_w", "mu_v", "sigma_v"):
         np.testing.assert_array_equal(pg[key], po[key])
@@ -65,14 +68,17 @@ def test_update_all_steps_vs_oracle(case):
     np.testing.assert_array_equal(rg["e"], ro["e"])       # per-row sums: bit-exact
     np.testing.assert_array_equal(rg["t"], ro["t"])
     np.testing.assert_array_equal(g.test_e(), oc.arr(o.s.e_test, o.s.n_test))
-    g.step_w0(); o.step("update_w0")
+    g.step_w0()
+    if int(dim.split(",")[0]):                    # update_all calls update_w0 only with k0
+        o.step("update_w0")
     close(g.rows()["e"], o.rows()["e"]); close(g.rows()["t"], o.rows()["t"])
     g.step_w(); o.step("update_w_all")
     close(g.get_params()["mu_w"], o.params()["mu_w"]); close(g.rows()["e"], o.rows()["e"])
     for f in range(3):
         g.step_qcache(f); o.step("add_main_q", f)
+        rg, ro = g.rows(), o.rows()
         for key in ("q", "tq", "tz"):
-            close(g.rows()[key], o.rows()[key])
+            np.testing.assert_array_equal(rg[key], ro[key], err_msg="f%d %s" % (f, key))
         g.step_v(f); o.step("update_v_all", f)
         rg, ro = g.rows(), o.rows()
         for key in ("e", "t", "q", "tq", "tz"):
@@ -156,9 +162,12 @@ def test_device_generator_matches_spec():
     np.testing.assert_array_equal(lv[present], (np.arange(F * S) // S + 1)[present])
 
 
-def test_generated_data_vs_oracle_two_iterations():
-    """Device-generated field data (real-valued x) through 2 iterations vs the oracle."""
-    n, F, S, seed, k = 60000, 8, 500, 3, 3
+@pytest.mark.parametrize("predict", ["exact", "blocked"])
+def test_generated_data_vs_oracle_two_iterations(predict, monkeypatch):
+    """Device-generated field data (real-valued x) through 2 iterations vs the oracle, with
+    both forms of the prediction kernels (blocked: ~1 ulp from the reference's order)."""
+    monkeypatch.setenv("VBFM_PREDICT", predict)
+    n, F, S, seed, k = 60000, 8, 500, 3, 11
     D = F * S + 1
     rp, f, v, y = synth.generate(n, F, S, seed, 1)
     rpt, ft, vt, yt = synth.generate(2000, F, S, seed + 1, 1)
@@ -173,6 +182,13 @@ def test_generated_data_vs_oracle_two_iterations():
     o.init_params(7, 0.1)
     o.attach(tr, te)
     o.init_caches()
+    rg, ro = fml.rows(), o.rows()
+    if predict == "exact":
+        np.testing.assert_array_equal(rg["e"], ro["e"])
+        np.testing.assert_array_equal(rg["t"], ro["t"])
+    else:
+        close(rg["e"], ro["e"], 1e-13)
+        close(rg["t"], ro["t"], 1e-13)
     for _ in range(2):
         st = fml.iterate()
         rmse, mae, trq = o.iterate()
