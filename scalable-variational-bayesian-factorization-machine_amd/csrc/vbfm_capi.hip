@@ -106,6 +106,7 @@ struct vbfm_ctx {
 	uint32_t *counters = nullptr;
 	// row-sharded multi-GPU
 	int nranks = 1, rank = 0;
+	bool force_split = false;      // VBFM_FORCE_SPLIT=1: the multi-rank kernels on one rank
 	ncclComm_t comm = nullptr;
 	double2 *stats = nullptr;
 	uint32_t stats_cap = 0;
@@ -289,7 +290,7 @@ void build_schedule(vbfm_ctx *c)
 	}
 	uint32_t maxlev = 0;
 	for (uint32_t l = 0; l < L; l++) maxlev = std::max(maxlev, c->level_ptr[l + 1] - c->level_ptr[l]);
-	if (c->nranks > 1 && maxlev > c->stats_cap) {
+	if ((c->nranks > 1 || c->force_split) && maxlev > c->stats_cap) {
 		dfree(c->stats);
 		c->stats = dalloc<double2>(maxlev);
 		c->stats_cap = maxlev;
@@ -401,15 +402,19 @@ void sweep_level(vbfm_ctx *c, uint32_t l, bool is_w, int f)
 {
 	LevelArgs a = level_args(c, l, is_w, f);
 	if (a.nfeat == 0) return;
-	if (c->nranks == 1) {
-		const size_t p = prof_begin(c, is_w ? 1 : 0);
+	const size_t p = prof_begin(c, is_w ? 1 : 0);
+	if (c->nranks == 1 && !c->force_split) {
 		HIPCHK(is_w ? vbk::w_level_fused(a, c->s) : vbk::v_level_fused(a, c->s));
 		prof_end(c, p);
 		return;
 	}
+	// row-sharded form: per-feature sufficient statistics of this shard's rows, summed over
+	// the shards, then every shard applies the identical posterior to its own rows
 	HIPCHK(is_w ? vbk::w_level_stats(a, c->s) : vbk::v_level_stats(a, c->s));
-	NCCLCHK(ncclAllReduce(c->stats, c->stats, 2 * (size_t)a.nfeat, ncclDouble, ncclSum, c->comm, c->s));
+	if (c->nranks > 1)
+		NCCLCHK(ncclAllReduce(c->stats, c->stats, 2 * (size_t)a.nfeat, ncclDouble, ncclSum, c->comm, c->s));
 	HIPCHK(is_w ? vbk::w_level_correct(a, c->s) : vbk::v_level_correct(a, c->s));
+	prof_end(c, p);
 }
 
 uint32_t nlevels(vbfm_ctx *c) { return c->level_ptr.empty() ? 0 : (uint32_t)c->level_ptr.size() - 1; }
@@ -557,6 +562,10 @@ int vbfm_create(vbfm_ctx **out, const vbfm_config *cfg)
 	c->k0 = cfg->k0 != 0; c->k1 = cfg->k1 != 0; c->k = cfg->num_factor;
 	c->D = cfg->num_attribute; c->G = cfg->num_attr_groups;
 	c->min_target = cfg->min_target; c->max_target = cfg->max_target;
+	{
+		const char *fs = getenv("VBFM_FORCE_SPLIT");
+		c->force_split = fs && fs[0] == '1';
+	}
 	int rc = guarded(c, [&] {
 		HIPCHK(hipStreamCreateWithFlags(&c->s, hipStreamNonBlocking));
 		for (int i = 0; i < EV_N; i++) HIPCHK(hipEventCreate(&c->ev[i]));

@@ -1,0 +1,316 @@
+// host/libfm_main.cpp -- drop-in for the reference's `bin/libFM -method vb` on MI355X.
+//
+// Mirrors main() of src/libfm/libfm.cpp (flag surface, defaults, RNG order, output lines and
+// files) and the iteration loop of fm_learn_vb_simultaneous::_learn
+// (src/libfm/src/fm_learn_vb_simultaneous.h:18-259); the learner itself is libvbfm.so
+// (include/vbfm.h). Deliberate differences, all documented in INTEGRATION.md:
+//   * -seed is honoured (the reference seeds with time(NULL) and ignores it, libfm.cpp:123);
+//   * -out writes the clipped test predictions of the last iteration (the reference's VB
+//     predict() body is commented out and leaves the vector uninitialised, fm_learn_vb.h:321);
+//   * -method mcmc/als/sgd/... and -task c are rejected with an error instead of running
+//     other learners; -relation is not supported;
+//   * extra flags: -device (HIP ordinal), -vfile 0 (skip writing v_file.txt).
+#include "../../include/vbfm.h"
+
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <ctime>
+#include <fstream>
+#include <iomanip>
+#include <iostream>
+#include <map>
+#include <sstream>
+#include <string>
+#include <sys/resource.h>
+#include <vector>
+
+namespace {
+
+// CMDLine (src/util/cmdline.h:29-197): "-name value", "--name", lists split on ";,".
+class CmdLine {
+public:
+	std::map<std::string, std::string> help, value;
+	CmdLine(int argc, char **argv)
+	{
+		int i = 1;
+		while (i < argc) {
+			std::string s(argv[i]);
+			if (!parse_name(s)) throw std::string("cannot parse " + s);
+			if (value.count(s)) throw std::string("the parameter " + s + " is already specified");
+			if (i + 1 < argc) {
+				std::string nx(argv[i + 1]);
+				if (!parse_name(nx)) { value[s] = argv[i + 1]; i++; }
+				else value[s] = "";
+			} else value[s] = "";
+			i++;
+		}
+	}
+	static bool parse_name(std::string &s)
+	{
+		if (s.size() > 0 && s[0] == '-') {
+			s = (s.size() > 1 && s[1] == '-') ? s.substr(2) : s.substr(1);
+			return true;
+		}
+		return false;
+	}
+	const std::string &reg(const std::string &p, const std::string &h) { help[p] = h; return p; }
+	bool has(const std::string &p) const { return value.count(p) > 0; }
+	void check() const
+	{
+		for (const auto &kv : value)
+			if (!help.count(kv.first)) throw std::string("the parameter " + kv.first + " does not exist");
+	}
+	std::string get(const std::string &p, const std::string &d = "") const { return has(p) ? value.at(p) : d; }
+	double getd(const std::string &p, double d) const { return has(p) ? atof(value.at(p).c_str()) : d; }
+	long geti(const std::string &p, long d) const { return has(p) ? atoi(value.at(p).c_str()) : d; }
+	std::vector<std::string> list(const std::string &p) const
+	{
+		std::vector<std::string> out;
+		const std::string s = get(p);
+		size_t a = s.find_first_not_of(";,");
+		while (a != std::string::npos) {
+			size_t b = s.find_first_of(";,", a);
+			out.push_back(s.substr(a, b == std::string::npos ? std::string::npos : b - a));
+			a = s.find_first_not_of(";,", b);
+		}
+		return out;
+	}
+	void print_help() const
+	{
+		for (const auto &kv : help) {
+			std::cout << "-" << kv.first;
+			for (size_t i = kv.first.size() + 1; i < 16; i++) std::cout << " ";
+			std::cout << kv.second << std::endl;
+		}
+	}
+};
+
+// RLog (src/util/rlog.h:29-91): TSV of registered fields, one line per iteration
+class RLog {
+public:
+	explicit RLog(std::ostream *o) : out(o) {}
+	void add(const std::string &f) { header.push_back(f); value[f] = NAN; }
+	void log(const std::string &f, double d) { value[f] = d; }
+	void init()
+	{
+		for (size_t i = 0; i < header.size(); i++) *out << header[i] << (i + 1 < header.size() ? "\t" : "\n");
+		out->flush();
+	}
+	void newline()
+	{
+		for (size_t i = 0; i < header.size(); i++) *out << value[header[i]] << (i + 1 < header.size() ? "\t" : "\n");
+		out->flush();
+		for (auto &kv : value) kv.second = NAN;
+	}
+private:
+	std::ostream *out;
+	std::vector<std::string> header;
+	std::map<std::string, double> value;
+};
+
+double usertime()
+{
+	struct rusage ru;
+	getrusage(RUSAGE_SELF, &ru);
+	return (double)ru.ru_utime.tv_sec + (double)ru.ru_utime.tv_usec / 1000000.0;
+}
+
+struct Data {
+	vbfm_host_data h{};
+	~Data() { vbfm_free_host_data(&h); }
+	vbfm_csc csc() const { return vbfm_csc{h.num_rows, h.num_feature, h.nnz, h.col_ptr, h.col_ent, h.target}; }
+};
+
+void check(int rc, vbfm_ctx *ctx)
+{
+	if (rc != 0) throw std::string(vbfm_last_error(ctx));
+}
+
+void load(const std::string &fn, Data &d, const char *what)
+{
+	std::cout << "Loading " << what << "...\t" << std::endl;
+	if (vbfm_load_data(fn.c_str(), &d.h) != 0) throw std::string(vbfm_last_error(nullptr));
+	std::cout << "num_rows=" << d.h.num_rows << "\tnum_values=" << d.h.nnz << "\tnum_features=" << d.h.num_feature
+	          << "\tmin_target=" << d.h.min_target << "\tmax_target=" << d.h.max_target << std::endl;
+}
+
+}  // namespace
+
+int main(int argc, char **argv)
+{
+	vbfm_ctx *ctx = nullptr;
+	try {
+		CmdLine cmd(argc, argv);
+		std::cout << "----------------------------------------------------------------------------" << std::endl;
+		std::cout << "libFM (VB learner on MI355X, libvbfm ABI " << vbfm_abi_version() << ")" << std::endl;
+		std::cout << "  Version: 1.4.2 (reference CLI surface)" << std::endl;
+		std::cout << "----------------------------------------------------------------------------" << std::endl;
+		const std::string p_task = cmd.reg("task", "r=regression, c=binary classification [MANDATORY]");
+		const std::string p_meta = cmd.reg("meta", "filename for meta information about data set");
+		const std::string p_train = cmd.reg("train", "filename for training data [MANDATORY]");
+		const std::string p_test = cmd.reg("test", "filename for test data [MANDATORY]");
+		cmd.reg("validation", "filename for validation data (only for SGDA)");
+		const std::string p_out = cmd.reg("out", "filename for output");
+		const std::string p_dim = cmd.reg("dim", "'k0,k1,k2': k0=use bias, k1=use 1-way interactions, k2=dim of 2-way interactions; default=1,1,8");
+		cmd.reg("regular", "'r0,r1,r2' for SGD and ALS: r0=bias regularization, r1=1-way regularization, r2=2-way regularization");
+		const std::string p_init = cmd.reg("init_stdev", "stdev for initialization of 2-way factors; default=0.1");
+		cmd.reg("stdev", "standard deviation for the model; default=1");
+		const std::string p_iter = cmd.reg("iter", "number of iterations; default=100");
+		cmd.reg("learn_rate", "learn_rate for SGD; default=0.1");
+		const std::string p_method = cmd.reg("method", "learning method (SGD, SGDA, ALS, MCMC, VB); default=MCMC");
+		const std::string p_verb = cmd.reg("verbosity", "how much infos to print; default=0");
+		const std::string p_rlog = cmd.reg("rlog", "write measurements within iterations to a file; default=''");
+		const std::string p_seed = cmd.reg("seed", "integer value, default=time(NULL)");
+		const std::string p_help = cmd.reg("help", "this screen");
+		const std::string p_rel = cmd.reg("relation", "BS: filenames for the relations, default=''");
+		cmd.reg("cache_size", "cache size for data storage (only applicable if data is in binary format), default=infty");
+		cmd.reg("batch", "How many batches for online algorithm");
+		const std::string p_dev = cmd.reg("device", "HIP device ordinal; default=0");
+		const std::string p_vfile = cmd.reg("vfile", "write v_file.txt like the reference (1) or not (0); default=1");
+		if (cmd.has(p_help) || argc == 1) { cmd.print_help(); return 0; }
+		cmd.check();
+
+		const uint32_t seed = cmd.has(p_seed) ? (uint32_t)cmd.geti(p_seed, 0) : (uint32_t)time(NULL);
+		const std::string method = cmd.get(p_method, "mcmc");
+		if (method != "vb") throw std::string("method " + method + " is not provided by this build (use -method vb)");
+		if (cmd.get(p_task) != "r") throw std::string("unknown task");   // VB regression only
+		if (!cmd.list(p_rel).empty()) throw std::string("-relation is not supported by the VB learner");
+
+		Data train, test;
+		load(cmd.get(p_train), train, "train");
+		load(cmd.get(p_test), test, "test");
+		if (cmd.geti(p_verb, 0) > 0) std::cout << "seed=" << seed << std::endl;
+
+		// libfm.cpp:215-256: attributes and groups
+		const uint32_t D = std::max(train.h.num_feature, test.h.num_feature) + 1;
+		std::vector<uint32_t> groups(D, 0);
+		uint32_t G = 1;
+		if (cmd.has(p_meta)) {
+			std::ifstream in(cmd.get(p_meta));
+			if (!in.is_open()) throw std::string("Unable to open file " + cmd.get(p_meta));
+			G = 0;
+			for (uint32_t i = 0; i < D; i++) {
+				long g = 0;
+				in >> g;
+				groups[i] = (uint32_t)g;
+				G = std::max(G, groups[i] + 1);
+			}
+		}
+		// -dim (libfm.cpp:266-271)
+		std::vector<std::string> dim = cmd.list(p_dim);
+		if (dim.empty()) dim = {"1", "1", "8"};
+		if (dim.size() != 3) throw std::string("-dim needs three values");
+		const int k0 = atoi(dim[0].c_str()) != 0, k1 = atoi(dim[1].c_str()) != 0, k = atoi(dim[2].c_str());
+		const double init_stdev = cmd.getd(p_init, 0.1);
+		const uint32_t num_iter = (uint32_t)cmd.geti(p_iter, 100);
+
+		// fm.init + fm.w.init_normal + fml->init draws (libfm.cpp:123-366) on the host
+		const size_t kd = (size_t)k * D;
+		std::vector<double> mu_w(D), sig_w(D), mu_v(kd), sig_v(kd), hw(G), hv((size_t)G * k), fm_v(kd);
+		vbfm_params p{mu_w.data(), sig_w.data(), mu_v.data(), sig_v.data(), hw.data(), hv.data(), 0, 0, 0, 0};
+		check(vbfm_init_params_host(seed, init_stdev, k, D, G, &p, fm_v.data(), nullptr), nullptr);
+		if (cmd.geti(p_vfile, 1)) {   // fm_model.h:98 (DMatrix::save, matrix.h:129-152)
+			std::ofstream vf("v_file.txt");
+			for (int f = 0; f < k; f++) {
+				for (uint32_t j = 0; j < D; j++) vf << (j ? "\t" : "") << fm_v[(size_t)f * D + j];
+				vf << std::endl;
+			}
+		}
+		fm_v.clear();
+		fm_v.shrink_to_fit();
+
+		vbfm_config cfg{k0, k1, k, D, G, cmd.has(p_meta) ? groups.data() : nullptr, train.h.min_target,
+		                train.h.max_target, (int32_t)cmd.geti(p_dev, 0), 0};
+		check(vbfm_create(&ctx, &cfg), nullptr);
+		const vbfm_csc tr = train.csc(), te = test.csc();
+		check(vbfm_set_train(ctx, &tr), ctx);
+		check(vbfm_set_test(ctx, &te), ctx);
+		check(vbfm_set_params(ctx, &p), ctx);
+		mu_v.clear(); sig_v.clear(); mu_v.shrink_to_fit(); sig_v.shrink_to_fit();
+
+		// -rlog (libfm.cpp:353-363; fields of fm_learn::init and fm_learn_vb::init)
+		std::ofstream *rlog_out = nullptr;
+		RLog *rlog = nullptr;
+		if (cmd.has(p_rlog)) {
+			rlog_out = new std::ofstream(cmd.get(p_rlog).c_str());
+			if (!rlog_out->is_open()) throw std::string("Unable to open file " + cmd.get(p_rlog));
+			std::cout << "logging to " << cmd.get(p_rlog) << std::endl;
+			rlog = new RLog(rlog_out);
+			for (const char *f : {"rmse", "mae", "time_pred", "time_learn", "time_learn2", "time_learn4", "alpha",
+			                      "rmse_mcmc_this", "rmse_mcmc_all"})
+				rlog->add(f);
+			for (uint32_t g = 0; g < G; g++) {
+				std::ostringstream ss;
+				ss << "wmu[" << g << "]"; rlog->add(ss.str()); ss.str("");
+				ss << "wlambda[" << g << "]"; rlog->add(ss.str()); ss.str("");
+				for (int f = 0; f < k; f++) {
+					ss << "vmu[" << g << "," << f << "]"; rlog->add(ss.str()); ss.str("");
+					ss << "vlambda[" << g << "," << f << "]"; rlog->add(ss.str()); ss.str("");
+				}
+			}
+			rlog->init();
+		}
+
+		// fm_learn_vb_simultaneous::_learn
+		check(vbfm_init_caches(ctx), ctx);
+		std::ostringstream tag;
+		tag << k0 << k1 << k;
+		const std::string f_rmse = "test_rmse_" + tag.str() + "_vb", f_fe = "free_energy_" + tag.str() + "_vb";
+		{ std::ofstream a(f_rmse.c_str()); std::ofstream b(f_fe.c_str()); }   // truncate (:58-73)
+		for (uint32_t it = 0; it < num_iter; it++) {
+			time_t now = time(0);
+			std::cout << ctime(&now) << std::endl;
+			const double t_user = usertime();
+			const clock_t t_clock = clock();
+			const double t_wall = (double)time(NULL);
+			vbfm_iter_stats st;
+			check(vbfm_iterate(ctx, &st), ctx);
+			if (st.free_energy_valid) {   // fm_learn_vb.h:678-680
+				std::ofstream fe(f_fe.c_str(), std::ios_base::app);
+				fe << -st.free_energy << "\n";
+				std::cout << "free energy " << st.free_energy << std::endl;
+			}
+			// the reference's NaN reports (fm_learn_vb_simultaneous.h:89-118; labels as printed there)
+			if (st.nan_alpha > 0 || st.inf_alpha > 0)
+				std::cout << "#nans in alpha:\t" << st.nan_alpha << "\t#inf_in_alpha:\t" << st.inf_alpha << std::endl;
+			if (st.nan_mu_w > 0 || st.inf_mu_w > 0)
+				std::cout << "#nans in alpha:\t" << st.nan_mu_w << "\t#inf_in_alpha:\t" << st.inf_mu_w << std::endl;
+			if (st.nan_sigma_w > 0)
+				std::cout << "#nans in alpha:\t" << st.nan_sigma_w << "\t#inf_in_alpha:\t" << 0 << std::endl;
+			if (st.nan_mu_v > 0 || st.inf_mu_v > 0)
+				std::cout << "#nans in alpha:\t" << st.nan_mu_v << "\t#inf_in_alpha:\t" << st.inf_mu_v << std::endl;
+			if (st.nan_sigma_v > 0)
+				std::cout << "#nans in alpha:\t" << st.nan_sigma_v << "\t#inf_in_alpha:\t" << 0 << std::endl;
+			if (rlog) {
+				rlog->log("time_learn", usertime() - t_user);
+				rlog->log("time_learn2", (double)(clock() - t_clock) / CLOCKS_PER_SEC);
+				rlog->log("time_learn4", (double)time(NULL) - t_wall);
+				rlog->log("rmse_mcmc_this", st.rmse);
+				rlog->newline();
+			}
+			std::ofstream fr(f_rmse.c_str(), std::ios_base::app);
+			fr << st.rmse << "\n";
+			std::cout << "#Iter=" << std::setw(3) << it << "\tTrain=" << st.train_quirk << "\tTest=" << st.rmse << std::endl;
+		}
+		// libfm.cpp:509-511: fm_learn_vb::evaluate returns NaN
+		std::cout << "Final\tTrain=" << NAN << "\tTest=" << NAN << std::endl;
+		if (cmd.has(p_out)) {   // libfm.cpp:514-519, DVector::save (matrix.h:284-295)
+			std::vector<double> pred(test.h.num_rows);
+			check(vbfm_get_test_pred(ctx, pred.data()), ctx);
+			std::ofstream o(cmd.get(p_out).c_str());
+			for (double v : pred) o << v << std::endl;
+		}
+		delete rlog;
+		delete rlog_out;
+		vbfm_destroy(ctx);
+		ctx = nullptr;
+	} catch (std::string &e) {
+		std::cerr << std::endl << "ERROR: " << e << std::endl;   // libfm.cpp:521-525 (exit code 0 there too)
+		if (ctx) vbfm_destroy(ctx);
+	} catch (char const *e) {
+		std::cerr << std::endl << "ERROR: " << e << std::endl;
+		if (ctx) vbfm_destroy(ctx);
+	}
+	return 0;
+}

@@ -127,7 +127,11 @@ def test_trace_tiny_vs_reference(case):
     close(fml.predict(), a["iter%d_pred" % last])
 
 
-def test_trace_synthetic_vs_reference(synth_files):
+@pytest.mark.parametrize("split", ["fused", "split"])
+def test_trace_synthetic_vs_reference(synth_files, split, monkeypatch):
+    """split: the row-sharded kernels (stats -> all-reduce -> correct) on one rank."""
+    if split == "split":
+        monkeypatch.setenv("VBFM_FORCE_SPLIT", "1")
     t, a = load_case("synth")
     train, test = vbfm.DataSubset.load(synth_files["train"]), vbfm.DataSubset.load(synth_files["test"])
     fml, stats = run_trace(train, test, t["meta"])
@@ -136,7 +140,10 @@ def test_trace_synthetic_vs_reference(synth_files):
     close(fml.get_params()["mu_v"], a["final_mu_v"])
 
 
-def test_trace_movielens_split_vs_reference(sa_split):
+@pytest.mark.parametrize("split", ["fused", "split"])
+def test_trace_movielens_split_vs_reference(sa_split, split, monkeypatch):
+    if split == "split":
+        monkeypatch.setenv("VBFM_FORCE_SPLIT", "1")
     t, a = load_case("sa_k8")
     train, test = vbfm.DataSubset.load(sa_split["train"]), vbfm.DataSubset.load(sa_split["test"])
     fml, stats = run_trace(train, test, t["meta"])
