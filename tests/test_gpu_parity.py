@@ -140,13 +140,27 @@ def test_trace_synthetic_vs_reference(synth_files, split, monkeypatch):
     close(fml.get_params()["mu_v"], a["final_mu_v"])
 
 
-@pytest.mark.parametrize("split", ["fused", "split"])
+@pytest.mark.parametrize("split", ["fused", "split", "rccl"])
 def test_trace_movielens_split_vs_reference(sa_split, split, monkeypatch):
-    if split == "split":
+    """split: the row-sharded kernels on one rank; rccl: the same through a real 1-rank RCCL
+    communicator (every ncclAllReduce of the multi-GPU path runs)."""
+    if split != "fused":
         monkeypatch.setenv("VBFM_FORCE_SPLIT", "1")
     t, a = load_case("sa_k8")
     train, test = vbfm.DataSubset.load(sa_split["train"]), vbfm.DataSubset.load(sa_split["test"])
-    fml, stats = run_trace(train, test, t["meta"])
+    if split == "rccl":
+        monkeypatch.setenv("VBFM_FORCE_COMM", "1")
+        m = t["meta"]
+        k0, k1, k = [int(x) for x in m["dim"].split(",")]
+        fml = vbfm.FMLearnVB(k0, k1, k, vbfm.num_all_attribute(train, test), min_target=train.min_target,
+                             max_target=train.max_target)
+        fml.comm_init(1, 0, vbfm.FMLearnVB.comm_unique_id())
+        fml.init(m["seed"], m["init_stdev"])
+        fml.set_data(train, test)
+        fml.init_caches()
+        stats = [fml.iterate() for _ in range(m["iter"])]
+    else:
+        fml, stats = run_trace(train, test, t["meta"])
     check_trace(stats, t["trace"])
     close(fml.get_params()["mu_w"], a["final_mu_w"])
 
