@@ -156,6 +156,71 @@ int vbfm_factor_sweep(vbfm_ctx *ctx, double *ms_device);
 int vbfm_comm_unique_id(uint8_t out[128]);
 int vbfm_comm_init(vbfm_ctx *ctx, int32_t nranks, int32_t rank, const uint8_t uid[128]);
 
+/* ---- MCMC / ALS learner (-method mcmc | als) -------------------------------------------
+ * Replaces fm_learn_mcmc / fm_learn_mcmc_simultaneous (src/libfm/src/fm_learn_mcmc.h,
+ * src/libfm/src/fm_learn_mcmc_simultaneous.h), regression, without relation blocks.
+ * vbfm_mcmc_init turns a context made by vbfm_create into an MCMC/ALS learner; the data
+ * hand-over (vbfm_set_train / vbfm_set_test / vbfm_synth_generate), vbfm_comm_init and the
+ * level schedule are the VB learner's. State is the model's point values fm.w0 / fm.w /
+ * fm.v and the hyper-priors; the row cache holds e = yhat - y (the MCMC sign, :76-80). */
+#define VBFM_RNG_REFERENCE 0  /* every draw from the reference's stream: srand(seed), glibc
+                                 rand(), Leva normals, Marsaglia-Tsang gammas (random.h),
+                                 consumed in the reference's order: the draws the reference
+                                 makes on the same inputs */
+#define VBFM_RNG_DEVICE 1     /* hyper-prior draws from that stream; the per-attribute
+                                 normals of draw_w / draw_v from a counter-based generator
+                                 keyed (seed, iteration, factor, attribute), identical on
+                                 every shard; fm.w / fm.v initialised on the device */
+
+typedef struct {
+	int32_t do_sample;        /* fm_learn_mcmc::do_sample: 1 mcmc, 0 als (libfm.cpp:131-135, 303) */
+	int32_t do_multilevel;    /* fm_learn_mcmc::do_multilevel (libfm.cpp:304) */
+	int32_t rng;              /* VBFM_RNG_* */
+	uint32_t seed;            /* srand(seed) (libfm.cpp:123-124) */
+	double init_stdev;        /* -init_stdev: fm.v, fm.w ~ N(0, init_stdev) (fm_model.h:97, libfm.cpp:298) */
+	const double *regular;    /* -regular values: 0, 1, 3 or 1 + 2*num_attr_groups of them (libfm.cpp:367-411) */
+	int32_t num_regular;
+} vbfm_mcmc_config;
+
+typedef struct {
+	double *w;                /* [D]   fm.w */
+	double *v;                /* [k*D] fm.v[f][j] */
+	double *w_mu, *w_lambda;  /* [G]   fm_learn_mcmc::w_mu, w_lambda */
+	double *v_mu, *v_lambda;  /* [G*k] v_mu(g, f), v_lambda(g, f), row-major [g][f] */
+	double w0, alpha, reg0;   /* fm.w0, fm_learn_mcmc::alpha, fm.reg0 */
+} vbfm_mcmc_params;
+
+typedef struct {
+	double rmse_all, mae_all;   /* test, on the running mean of the clipped predictions: "Test=" */
+	double rmse_this, mae_this; /* test, this iteration's predictions */
+	double train_rmse;          /* "Train=" (fm_learn_mcmc_simultaneous.h:153-162) */
+	double alpha, w0;
+	uint32_t nan_alpha, inf_alpha, nan_w0, inf_w0, nan_w, inf_w, nan_v, inf_v;
+	uint32_t nan_w_mu, inf_w_mu, nan_w_lambda, inf_w_lambda, nan_v_mu, inf_v_mu, nan_v_lambda, inf_v_lambda;
+	uint32_t rng_skipped;       /* VBFM_RNG_REFERENCE: attributes whose draw / no-draw decision
+	                               (the reference draws no normal for a zero or non-finite
+	                               variance) differed from the host's, i.e. 0 while the stream
+	                               is the reference's; VBFM_RNG_DEVICE: such attributes */
+	int32_t num_levels;
+	/* device time of the phases (hipEvents), ms; per-launch sums with vbfm_set_profiling */
+	double ms_hyper, ms_w, ms_v, ms_predict, ms_total;
+	double ms_vlevel_kernels;
+	int32_t n_vlevel_launches;
+	uint64_t nnz_train;
+} vbfm_mcmc_stats;
+
+int vbfm_mcmc_init(vbfm_ctx *ctx, const vbfm_mcmc_config *cfg);  /* fm_learn_mcmc::init (fm_learn_mcmc.h:1092-1151),
+                                                                    parameter draws and -regular (libfm.cpp:123-124, 273-304, 367-411) */
+int vbfm_mcmc_set_params(vbfm_ctx *ctx, const vbfm_mcmc_params *p);
+int vbfm_mcmc_get_params(vbfm_ctx *ctx, vbfm_mcmc_params *p);      /* NULL arrays are skipped */
+int vbfm_mcmc_init_caches(vbfm_ctx *ctx);                          /* _learn prologue, fm_learn_mcmc_simultaneous.h:64-81 */
+int vbfm_mcmc_iterate(vbfm_ctx *ctx, vbfm_mcmc_stats *out);        /* one pass of :83-304: draw_all, re-predict, evaluate */
+/* fm_learn_mcmc::predict (fm_learn_mcmc.h:355-381): sampling -> pred_sum_all / num_iter,
+ * else the last iteration's predictions; clipped to the train target range */
+int vbfm_mcmc_get_test_pred(vbfm_ctx *ctx, int32_t num_iter, double *pred /*[test rows]*/);
+/* the v draws of all factors alone (q-cache + draw_v sweeps, :501-621), for the bench */
+int vbfm_mcmc_factor_sweep(vbfm_ctx *ctx, double *ms_device);
+
 /* ---- host side of the reference's CLI path (loader, RNG init) -------------------------- */
 typedef struct {
 	uint32_t num_rows, num_feature;

@@ -245,7 +245,7 @@ static std::string arg(int argc, char** argv, const std::string& key, const std:
 
 int main(int argc, char** argv) {
 	if (argc < 2) {
-		fprintf(stderr, "usage: ref_driver vb|steps|sweep|als|mcmc --train F --test F --dim k0,k1,k --iter N --seed S [--init_stdev x] [--meta F] [--dump DIR] [--sweep_factors n]\n");
+		fprintf(stderr, "usage: ref_driver vb|steps|sweep|als|mcmc --train F --test F --dim k0,k1,k --iter N --seed S [--init_stdev x] [--meta F] [--regular r0,rw,rv] [--dump DIR] [--sweep_factors n]\n");
 		return 2;
 	}
 	std::cout.precision(17);
@@ -326,10 +326,29 @@ int main(int argc, char** argv) {
 		fml->log = NULL;
 		fml->init();
 		if (is_mcmc) {
-			// -regular absent => all zero (libfm.cpp:370-377)
-			fm.reg0 = 0.0; fm.regw = 0.0; fm.regv = 0.0;
-			((fm_learn_mcmc*)fml)->w_lambda.init(fm.regw);
-			((fm_learn_mcmc*)fml)->v_lambda.init(fm.regv);
+			// -regular as libfm.cpp:367-411 (absent => all zero)
+			std::vector<double> reg;
+			{
+				std::stringstream ss(arg(argc, argv, "--regular", ""));
+				std::string tok;
+				while (std::getline(ss, tok, ',')) if (!tok.empty()) reg.push_back(atof(tok.c_str()));
+			}
+			fm_learn_mcmc* m = (fm_learn_mcmc*)fml;
+			if (reg.size() == 0) { fm.reg0 = 0.0; fm.regw = 0.0; fm.regv = 0.0; }
+			else if (reg.size() == 1) { fm.reg0 = reg[0]; fm.regw = reg[0]; fm.regv = reg[0]; }
+			else if (reg.size() == 3) { fm.reg0 = reg[0]; fm.regw = reg[1]; fm.regv = reg[2]; }
+			if (reg.size() == 1 + 2 * (size_t)meta.num_attr_groups && reg.size() != 3 && reg.size() != 1) {
+				fm.reg0 = reg[0]; fm.regw = 0.0; fm.regv = 0.0;
+				size_t j = 1;
+				for (uint g = 0; g < meta.num_attr_groups; g++) m->w_lambda(g) = reg[j++];
+				for (uint g = 0; g < meta.num_attr_groups; g++) {
+					for (int f = 0; f < fm.num_factor; f++) m->v_lambda(g, f) = reg[j];
+					j++;
+				}
+			} else {
+				m->w_lambda.init(fm.regw);
+				m->v_lambda.init(fm.regv);
+			}
 		} else {
 			vb->dump_params("init");
 		}
@@ -340,6 +359,12 @@ int main(int argc, char** argv) {
 			dump_arr("final_fm_w", fm.w.value, fm.w.dim);
 			double sc[2] = {fm.w0, m->alpha};
 			dump_arr("final_mcmc_scalars", sc, 2);
+			dump_arr("final_w_mu", m->w_mu.value, m->w_mu.dim);
+			dump_arr("final_w_lambda", m->w_lambda.value, m->w_lambda.dim);
+			if (fm.num_factor > 0) {
+				dump_arr("final_v_mu", m->v_mu.value[0], (size_t)m->v_mu.dim1 * m->v_mu.dim2);
+				dump_arr("final_v_lambda", m->v_lambda.value[0], (size_t)m->v_lambda.dim1 * m->v_lambda.dim2);
+			}
 		}
 		std::cout << "DONE" << std::endl;
 	} catch (std::string& e) {

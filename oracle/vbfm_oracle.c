@@ -1,7 +1,6 @@
 /* oracle/vbfm_oracle.c -- TEST INFRASTRUCTURE ONLY (the checker; never the product).
  *
- * Plain-C restatement of the reference's libFM VB path (and the deterministic ALS variant
- * of the MCMC learner). Every function follows the reference's arithmetic expression by
+ * Plain-C restatement of the reference's libFM VB path and of its MCMC / ALS learner. Every function follows the reference's arithmetic expression by
  * expression, in the reference's loop order, so that on the same inputs it reproduces the
  * reference bit for bit (pinned by tests/test_oracle_golden.py against dumps of the
  * compiled reference, oracle/_ref/ref_driver).
@@ -733,7 +732,32 @@ void or_vb_update_all_sharded(or_vb *st, const or_data *train, uint32_t n_global
 }
 
 /* ------------------------------------------------------------------------------------ */
-/* ALS: fm_learn_mcmc with do_sample = do_multilevel = 0 (libfm.cpp:131-135,304-305)     */
+/* MCMC / ALS: fm_learn_mcmc + fm_learn_mcmc_simultaneous (regression, no relations).
+ * ALS is the same learner with do_sample = do_multilevel = 0 (libfm.cpp:131-135).        */
+
+/* random.h:118-148: Marsaglia-Tsang for a >= 1, the U^(1/a) boost below 1 */
+double or_ran_gamma(double a)
+{
+	if (a < 1.0) {
+		double u;
+		do { u = or_uniform(); } while (u == 0.0);
+		return or_ran_gamma(a + 1.0) * pow(u, 1.0 / a);
+	} else {
+		double d = a - 1.0 / 3.0, c = 1.0 / sqrt(9.0 * d), x, v, u;
+		do {
+			do {
+				x = or_ran_gaussian();
+				v = 1.0 + c * x;
+			} while (v <= 0.0);
+			v = v * v * v;
+			u = or_uniform();
+		} while ((u >= (1.0 - 0.0331 * (x * x) * (x * x))) && (log(u) >= (0.5 * x * x + d * (1.0 - v + log(v)))));
+		return d * v;
+	}
+}
+
+double or_ran_gamma_ab(double a, double b) { return or_ran_gamma(a) / b; } /* random.h:146-148 */
+
 int or_als_create(or_als *st, int k0, int k1, int k, uint32_t D, const uint32_t *attr_group)
 {
 	uint32_t i;
@@ -758,7 +782,13 @@ int or_als_create(or_als *st, int k0, int k1, int k, uint32_t D, const uint32_t 
 	st->v_mu = (double *)xcalloc((size_t)st->G * k, sizeof(double));
 	st->alpha = 1;   /* fm_learn_mcmc::init (fm_learn_mcmc.h:1100-1117) */
 	st->w0 = 0;
+	st->do_sample = 0; st->do_multilevel = 0; st->reg0 = 0.0;
 	return 0;
+}
+
+void or_als_configure(or_als *st, int do_sample, int do_multilevel, double reg0)
+{
+	st->do_sample = do_sample; st->do_multilevel = do_multilevel; st->reg0 = reg0;
 }
 
 void or_als_destroy(or_als *st)
@@ -766,7 +796,7 @@ void or_als_destroy(or_als *st)
 	free(st->attr_group); free(st->num_attr_per_group); free(st->w); free(st->v);
 	free(st->w_lambda); free(st->w_mu); free(st->v_lambda); free(st->v_mu);
 	free(st->e); free(st->q); free(st->e_test); free(st->q_test);
-	free(st->pred_sum_all); free(st->pred_this);
+	free(st->pred_sum_all); free(st->pred_this); free(st->tmp_g);
 	memset(st, 0, sizeof(*st));
 }
 
@@ -820,7 +850,7 @@ int or_als_attach(or_als *st, const or_data *train, const or_data *test)
 	st->pred_sum_all = (double *)xcalloc(test->num_rows, sizeof(double));
 	st->pred_this = (double *)xcalloc(test->num_rows, sizeof(double));
 	st->min_target = train->min_target; st->max_target = train->max_target;
-	/* fm_learn_mcmc_simultaneous.h:75-81: e = yhat - y */
+	/* fm_learn_mcmc_simultaneous.h:71-80: predict train and test, e = yhat - y */
 	als_predict(st, train, st->e, st->q);
 	als_predict(st, test, st->e_test, st->q_test);
 	for (c = 0; c < train->num_rows; c++) st->e[c] = st->e[c] - train->target[c];
@@ -828,7 +858,7 @@ int or_als_attach(or_als *st, const or_data *train, const or_data *test)
 	return 0;
 }
 
-/* draw_w / draw_v without sampling (fm_learn_mcmc.h:671-718, 780-835) */
+/* draw_w (fm_learn_mcmc.h:671-718) */
 static void als_draw_w(or_als *st, double *w, double w_mu, double w_lambda,
                        const uint32_t *rows, const float *vals, uint64_t n)
 {
@@ -842,14 +872,17 @@ static void als_draw_w(or_als *st, double *w, double w_mu, double w_lambda,
 	w_sigma_sqr = (double)1.0 / (w_lambda + st->alpha * w_sigma_sqr);
 	w_mean = -w_sigma_sqr * (st->alpha * w_mean - w_mu * w_lambda);
 	w_old = *w;
-	if (isnan(w_sigma_sqr) || isinf(w_sigma_sqr)) *w = 0.0; else *w = w_mean;
-	if (isnan(*w) || isinf(*w)) { *w = w_old; return; }
+	if (isnan(w_sigma_sqr) || isinf(w_sigma_sqr)) *w = 0.0;
+	else *w = st->do_sample ? or_ran_gaussian_ms(w_mean, sqrt(w_sigma_sqr)) : w_mean;
+	if (isnan(*w)) { st->nan_w++; *w = w_old; return; }
+	if (isinf(*w)) { st->inf_w++; *w = w_old; return; }
 	for (p = 0; p < n; p++) {
 		double h = vals[p];
 		st->e[rows[p]] -= h * (w_old - *w);
 	}
 }
 
+/* draw_v (fm_learn_mcmc.h:780-835) */
 static void als_draw_v(or_als *st, double *v, double v_mu, double v_lambda,
                        const uint32_t *rows, const float *vals, uint64_t n)
 {
@@ -866,14 +899,118 @@ static void als_draw_v(or_als *st, double *v, double v_mu, double v_lambda,
 	v_sigma_sqr = (double)1.0 / (v_lambda + st->alpha * v_sigma_sqr);
 	v_mean = -v_sigma_sqr * (st->alpha * v_mean - v_mu * v_lambda);
 	v_old = *v;
-	if (isnan(v_sigma_sqr) || isinf(v_sigma_sqr)) *v = 0.0; else *v = v_mean;
-	if (isnan(*v) || isinf(*v)) { *v = v_old; return; }
+	if (isnan(v_sigma_sqr) || isinf(v_sigma_sqr)) *v = 0.0;
+	else *v = st->do_sample ? or_ran_gaussian_ms(v_mean, sqrt(v_sigma_sqr)) : v_mean;
+	if (isnan(*v)) { st->nan_v++; *v = v_old; return; }
+	if (isinf(*v)) { st->inf_v++; *v = v_old; return; }
 	for (p = 0; p < n; p++) {
 		uint32_t r = rows[p];
 		float x = vals[p];
 		double h = x * (st->q[r] - x * v_old);
 		st->q[r] -= x * (v_old - *v);
 		st->e[r] -= h * (v_old - *v);
+	}
+}
+
+/* hyper-prior constants of fm_learn_mcmc::init (fm_learn_mcmc.h:1100-1103) */
+#define MC_ALPHA_0 1.0
+#define MC_GAMMA_0 1.0
+#define MC_BETA_0 1.0
+#define MC_MU_0 0.0
+
+/* draw_alpha (fm_learn_mcmc.h:901-929) */
+static void mc_draw_alpha(or_als *st, uint32_t n)
+{
+	double alpha_n, gamma_n, alpha_old;
+	uint32_t i;
+	if (!st->do_multilevel) { st->alpha = MC_ALPHA_0; return; }
+	alpha_n = MC_ALPHA_0 + n;
+	gamma_n = MC_GAMMA_0;
+	for (i = 0; i < n; i++) gamma_n += st->e[i] * st->e[i];
+	alpha_old = st->alpha;
+	st->alpha = or_ran_gamma_ab(alpha_n / 2.0, gamma_n / 2.0);
+	if (isnan(st->alpha) || isinf(st->alpha)) st->alpha = alpha_old;
+}
+
+/* draw_w_lambda / draw_w_mu (fm_learn_mcmc.h:931-1008); the early `return` on a NaN/inf
+ * draw skips the remaining groups, as in the reference */
+static void mc_draw_w_lambda(or_als *st)
+{
+	double *gam = st->tmp_g;
+	uint32_t g, i;
+	if (!st->do_multilevel) return;
+	for (g = 0; g < st->G; g++) gam[g] = MC_BETA_0 * (st->w_mu[g] - MC_MU_0) * (st->w_mu[g] - MC_MU_0) + MC_GAMMA_0;
+	for (i = 0; i < st->D; i++) {
+		g = st->attr_group[i];
+		gam[g] += (st->w[i] - st->w_mu[g]) * (st->w[i] - st->w_mu[g]);
+	}
+	for (g = 0; g < st->G; g++) {
+		double a = MC_ALPHA_0 + st->num_attr_per_group[g] + 1, old = st->w_lambda[g];
+		st->w_lambda[g] = st->do_sample ? or_ran_gamma_ab(a / 2.0, gam[g] / 2.0) : a / gam[g];
+		if (isnan(st->w_lambda[g]) || isinf(st->w_lambda[g])) { st->w_lambda[g] = old; return; }
+	}
+}
+
+static void mc_draw_w_mu(or_als *st)
+{
+	double *mean = st->tmp_g;
+	uint32_t g, i;
+	if (!st->do_multilevel) { for (g = 0; g < st->G; g++) st->w_mu[g] = MC_MU_0; return; }
+	for (g = 0; g < st->G; g++) mean[g] = 0.0;
+	for (i = 0; i < st->D; i++) mean[st->attr_group[i]] += st->w[i];
+	for (g = 0; g < st->G; g++) {
+		double s2, old = st->w_mu[g];
+		mean[g] = (mean[g] + MC_BETA_0 * MC_MU_0) / (st->num_attr_per_group[g] + MC_BETA_0);
+		s2 = (double)1.0 / ((st->num_attr_per_group[g] + MC_BETA_0) * st->w_lambda[g]);
+		st->w_mu[g] = st->do_sample ? or_ran_gaussian_ms(mean[g], sqrt(s2)) : mean[g];
+		if (isnan(st->w_mu[g]) || isinf(st->w_mu[g])) { st->w_mu[g] = old; return; }
+	}
+}
+
+/* draw_v_lambda / draw_v_mu (fm_learn_mcmc.h:1011-1089); v_mu, v_lambda at [g*k + f] */
+static void mc_draw_v_lambda(or_als *st)
+{
+	double *gam = st->tmp_g;
+	uint32_t g, i;
+	int f, k = st->k;
+	if (!st->do_multilevel) return;
+	for (f = 0; f < k; f++) {
+		const double *v = st->v + (size_t)f * st->D;
+		for (g = 0; g < st->G; g++) {
+			double m = st->v_mu[(size_t)g * k + f];
+			gam[g] = MC_BETA_0 * (m - MC_MU_0) * (m - MC_MU_0) + MC_GAMMA_0;
+		}
+		for (i = 0; i < st->D; i++) {
+			double m;
+			g = st->attr_group[i];
+			m = st->v_mu[(size_t)g * k + f];
+			gam[g] += (v[i] - m) * (v[i] - m);
+		}
+		for (g = 0; g < st->G; g++) {
+			double a = MC_ALPHA_0 + st->num_attr_per_group[g] + 1, *lam = &st->v_lambda[(size_t)g * k + f], old = *lam;
+			*lam = st->do_sample ? or_ran_gamma_ab(a / 2.0, gam[g] / 2.0) : a / gam[g];
+			if (isnan(*lam) || isinf(*lam)) { *lam = old; return; }
+		}
+	}
+}
+
+static void mc_draw_v_mu(or_als *st)
+{
+	double *mean = st->tmp_g;
+	uint32_t g, i;
+	int f, k = st->k;
+	if (!st->do_multilevel) { for (i = 0; i < st->G * (uint32_t)k; i++) st->v_mu[i] = MC_MU_0; return; }
+	for (f = 0; f < k; f++) {
+		const double *v = st->v + (size_t)f * st->D;
+		for (g = 0; g < st->G; g++) mean[g] = 0.0;
+		for (i = 0; i < st->D; i++) mean[st->attr_group[i]] += v[i];
+		for (g = 0; g < st->G; g++) {
+			double s2, *mu = &st->v_mu[(size_t)g * k + f], old = *mu;
+			mean[g] = (mean[g] + MC_BETA_0 * MC_MU_0) / (st->num_attr_per_group[g] + MC_BETA_0);
+			s2 = (double)1.0 / ((st->num_attr_per_group[g] + MC_BETA_0) * st->v_lambda[(size_t)g * k + f]);
+			*mu = st->do_sample ? or_ran_gaussian_ms(mean[g], sqrt(s2)) : mean[g];
+			if (isnan(*mu) || isinf(*mu)) { *mu = old; return; }
+		}
 	}
 }
 
@@ -884,19 +1021,21 @@ void or_als_iterate(or_als *st, const or_data *train, const or_data *test,
 	uint64_t p;
 	int f;
 	double mx = st->max_target, mn = st->min_target, s = 0.0, s1 = 0.0, s2 = 0.0;
-	/* draw_all (fm_learn_mcmc.h:411-623), do_multilevel = 0: alpha = alpha_0 = 1, mu = 0 */
-	st->alpha = 1.0;
-	if (st->k0) {   /* draw_w0 (fm_learn_mcmc.h:628-668) with reg0 = 0 */
+	if (!st->tmp_g) st->tmp_g = (double *)xcalloc(st->G, sizeof(double));
+	/* draw_all (fm_learn_mcmc.h:411-623) */
+	mc_draw_alpha(st, train->num_rows);
+	if (st->k0) {   /* draw_w0 (fm_learn_mcmc.h:628-668), w0_mean_0 = 0 */
 		double w0_mean = 0, w0_sigma_sqr, w0_old = st->w0;
 		for (c = 0; c < train->num_rows; c++) w0_mean += st->e[c] - st->w0;
-		w0_sigma_sqr = (double)1.0 / (0.0 + st->alpha * train->num_rows);
-		w0_mean = -w0_sigma_sqr * (st->alpha * w0_mean - 0.0 * 0.0);
-		st->w0 = w0_mean;
+		w0_sigma_sqr = (double)1.0 / (st->reg0 + st->alpha * train->num_rows);
+		w0_mean = -w0_sigma_sqr * (st->alpha * w0_mean - 0.0 * st->reg0);
+		st->w0 = st->do_sample ? or_ran_gaussian_ms(w0_mean, sqrt(w0_sigma_sqr)) : w0_mean;
 		if (isnan(st->w0) || isinf(st->w0)) st->w0 = w0_old;
 		else for (c = 0; c < train->num_rows; c++) st->e[c] -= (w0_old - st->w0);
 	}
 	if (st->k1) {
-		for (i = 0; i < st->G; i++) st->w_mu[i] = 0.0;
+		mc_draw_w_lambda(st);
+		mc_draw_w_mu(st);
 		for (i = 0; i < train->num_feature; i++) {
 			uint32_t g = st->attr_group[i];
 			uint64_t b = train->col_ptr[i];
@@ -908,7 +1047,10 @@ void or_als_iterate(or_als *st, const or_data *train, const or_data *test,
 			als_draw_w(st, &st->w[i], st->w_mu[g], st->w_lambda[g], NULL, NULL, 0);
 		}
 	}
-	if (st->k > 0) for (i = 0; i < st->G * (uint32_t)st->k; i++) st->v_mu[i] = 0.0;
+	if (st->k > 0) {
+		mc_draw_v_lambda(st);
+		mc_draw_v_mu(st);
+	}
 	for (f = 0; f < st->k; f++) {
 		double *v = st->v + (size_t)f * st->D;
 		for (c = 0; c < train->num_rows; c++) st->q[c] = 0.0;
@@ -933,26 +1075,26 @@ void or_als_iterate(or_als *st, const or_data *train, const or_data *test,
 	for (c = 0; c < test->num_rows; c++) {
 		double pp = st->e_test[c];
 		st->pred_this[c] = pp;
-		pp = pp < mx ? pp : mx;
-		pp = mn > pp ? mn : pp;
+		pp = pp < mx ? pp : mx;      /* std::min(max_target, p) */
+		pp = mn < pp ? pp : mn;      /* std::max(min_target, p) */
 		st->pred_sum_all[c] += pp;
 	}
 	for (c = 0; c < train->num_rows; c++) {
 		double pp = st->e[c], err;
 		pp = pp < mx ? pp : mx;
-		pp = mn > pp ? mn : pp;
+		pp = mn < pp ? pp : mn;
 		err = pp - train->target[c];
 		s += err * err;
 		st->e[c] = st->e[c] - train->target[c];
 	}
 	*train_rmse = sqrt(s / train->num_rows);
-	for (c = 0; c < test->num_rows; c++) {
+	for (c = 0; c < test->num_rows; c++) {   /* _evaluate (fm_learn_mcmc_simultaneous.h:261-279) */
 		double pp = st->pred_this[c] * 1.0, err;
-		pp = pp < mx ? pp : mx; pp = mn > pp ? mn : pp;
+		pp = pp < mx ? pp : mx; pp = mn < pp ? pp : mn;
 		err = pp - test->target[c];
 		s1 += err * err;
 		pp = st->pred_sum_all[c] * (1.0 / (st->iter_done + 1));
-		pp = pp < mx ? pp : mx; pp = mn > pp ? mn : pp;
+		pp = pp < mx ? pp : mx; pp = mn < pp ? pp : mn;
 		err = pp - test->target[c];
 		s2 += err * err;
 	}

@@ -92,7 +92,8 @@ typedef void (*or_allreduce_fn)(double *buf, int n, void *user);
 void or_vb_update_all_sharded(or_vb *st, const or_data *train, uint32_t n_train_global,
                               uint32_t nf_train_global, or_allreduce_fn allreduce, void *user);
 
-/* ALS (= mcmc without sampling / multilevel, libfm.cpp:131-135) state */
+/* MCMC / ALS learner state (fm_learn_mcmc.h); ALS = mcmc without sampling / multilevel
+ * (libfm.cpp:131-135). Draws come from the or_srand stream, as the reference's rand(). */
 typedef struct {
 	int k0, k1, k;
 	uint32_t D, G;
@@ -105,10 +106,17 @@ typedef struct {
 	double *pred_sum_all, *pred_this;
 	float min_target, max_target;
 	uint32_t iter_done;
+	int do_sample, do_multilevel;   /* fm_learn_mcmc.h:92-93 */
+	double reg0;                    /* fm.reg0 (libfm.cpp:367-411) */
+	uint32_t nan_w, inf_w, nan_v, inf_v;
+	double *tmp_g;                  /* cache_for_group_values */
 } or_als;
 
 int or_als_create(or_als *st, int k0, int k1, int k, uint32_t D, const uint32_t *attr_group);
 void or_als_destroy(or_als *st);
+void or_als_configure(or_als *st, int do_sample, int do_multilevel, double reg0);
+double or_ran_gamma(double a);                 /* random.h:118-144 */
+double or_ran_gamma_ab(double a, double b);    /* random.h:146-148 */
 void or_als_init_params(or_als *st, uint32_t seed, double init_stdev); /* libfm.cpp:123,273,298 */
 int or_als_attach(or_als *st, const or_data *train, const or_data *test);
 void or_als_iterate(or_als *st, const or_data *train, const or_data *test,

@@ -6,10 +6,7 @@
 // arithmetic; every O(nnz), O(N) and O(k*D) loop runs as a kernel of vbfm_kernels.hip on
 // the context's stream. Device-side partial sums come back in a fixed order and are added
 // on the host in that order, so results are deterministic run to run.
-#include "vbfm_device.h"
-#include "../../include/vbfm.h"
-
-#include <rccl/rccl.h>
+#include "vbfm_ctx.h"
 
 #include <algorithm>
 #include <cmath>
@@ -19,131 +16,14 @@
 #include <string>
 #include <vector>
 
-extern "C" const char *vbfm_host_last_error(void);
-extern "C" void vbfm_host_set_error(const char *msg);
+using namespace vbi;
 
-namespace {
-
-
-struct DevData {
-	uint32_t n = 0, nf = 0;        // rows; columns of the transposed copy (padded to the global nf)
-	uint32_t nf_local = 0;
-	uint64_t nnz = 0;
-	uint64_t *col_ptr = nullptr;   // [nf+1]
-	uint2 *csc = nullptr;          // [nnz]
-	uint64_t *row_ptr = nullptr;   // [n+1]
-	uint2 *csr = nullptr;          // [nnz] feature-sorted rows
-	float *target = nullptr;       // [n]
-	float min_target = 0, max_target = 0;
-};
-
-struct HipError {
-	hipError_t e;
-	const char *what;
-};
-
-#define HIPCHK(x)                                                   \
-	do {                                                            \
-		hipError_t _e = (x);                                        \
-		if (_e != hipSuccess) throw HipError{_e, #x};               \
-	} while (0)
-
-#define NCCLCHK(x)                                                  \
-	do {                                                            \
-		ncclResult_t _r = (x);                                      \
-		if (_r != ncclSuccess) throw std::string("RCCL: ") + ncclGetErrorString(_r) + " in " #x; \
-	} while (0)
-
-template <class T> T *dalloc(size_t n)
-{
-	void *p = nullptr;
-	HIPCHK(hipMalloc(&p, (n ? n : 1) * sizeof(T)));
-	return (T *)p;
-}
-
-template <class T> void dfree(T *&p)
-{
-	if (p) (void)hipFree((void *)p);
-	p = nullptr;
-}
-
-enum { EV_BEGIN, EV_W0, EV_W, EV_V, EV_HYPER, EV_TEST, EV_N };
-
-}  // namespace
-
-struct vbfm_ctx {
-	std::string err;
-	int dev = 0;
-	hipStream_t s = nullptr;
-	int k0 = 1, k1 = 1, k = 0;
-	uint32_t D = 0, G = 1;
-	std::vector<uint32_t> group_h, per_group;
-	uint32_t *group_d = nullptr;
-	float min_target = 0, max_target = 0;
-	DevData tr, te;
-	RowRec *rows = nullptr;
-	double *scratch_n = nullptr;   // yhat of train at init
-	double *e_test = nullptr, *pred_test = nullptr;
-	double2 *ms_v = nullptr, *ms_w = nullptr;
-	double *hyp_w_d = nullptr, *hyp_v_d = nullptr;
-	std::vector<double> hyp_w, hyp_v;
-	double alpha = 1.0, sigma_0 = 1.0, mu0 = 0.0, s0d = 0.02;
-	// schedule
-	std::vector<uint32_t> level_ptr, level_h, level_avg;
-	int q_ready[2] = {-1, -1};     // factor whose q-cache each slot holds (-1: none)
-	int qslot = 0;                 // slot reported by vbfm_get_rows
-	uint32_t *level_feats = nullptr;
-	uint8_t *dup = nullptr;
-	bool sched_ready = false;
-	// reductions
-	static constexpr uint32_t RED_BLOCKS = 512;
-	double *red_d = nullptr;
-	std::vector<double> red_h;
-	uint32_t *perm_d = nullptr;
-	vbk::Chunk *chunks_d = nullptr;
-	std::vector<vbk::Chunk> chunks_h;
-	double *chunk_out_d = nullptr;
-	uint32_t *counters = nullptr;
-	// row-sharded multi-GPU
-	int nranks = 1, rank = 0;
-	bool force_split = false;      // VBFM_FORCE_SPLIT=1: the multi-rank kernels on one rank
-	ncclComm_t comm = nullptr;
-	double2 *stats = nullptr;
-	uint32_t stats_cap = 0;
-	uint64_t n_global = 0;
-	uint32_t test_n_global = 0;
-	hipEvent_t ev[EV_N] = {};
-	// per-launch profiling (vbfm_set_profiling)
-	bool profiling = false;
-	std::vector<hipEvent_t> pev;
-	size_t pev_used = 0;
-	struct Span { size_t a; int kind; };   // kind 0 = v level, 1 = w level, 2 = qcache
-	std::vector<Span> spans;
-};
-
-namespace {
+namespace vbi {
 
 int fail(vbfm_ctx *c, const std::string &m)
 {
 	if (c) c->err = m; else vbfm_host_set_error(m.c_str());
 	return -1;
-}
-
-template <class F> int guarded(vbfm_ctx *c, F &&fn)
-{
-	try {
-		if (c) HIPCHK(hipSetDevice(c->dev));
-		fn();
-		return 0;
-	} catch (const HipError &e) {
-		return fail(c, std::string("HIP error ") + hipGetErrorString(e.e) + " in " + e.what);
-	} catch (const std::string &m) {
-		return fail(c, m);
-	} catch (const char *m) {
-		return fail(c, m);
-	} catch (const std::bad_alloc &) {
-		return fail(c, "host out of memory");
-	}
 }
 
 void sync(vbfm_ctx *c) { HIPCHK(hipStreamSynchronize(c->s)); }
@@ -459,6 +339,7 @@ void step_v(vbfm_ctx *c, int f)
 {
 	for (uint32_t l = 0; l < nlevels(c); l++) sweep_level(c, l, false, f);
 	c->qslot = f & 1;
+	c->q_ready[f & 1] = -1;   // corrected in place, no longer the from-scratch sum add_main_q gives
 	if (f + 1 < c->k) c->q_ready[(f + 1) & 1] = f + 1;
 	else c->q_ready[(f + 1) & 1] = -1;
 }
@@ -534,7 +415,7 @@ float ev_ms(vbfm_ctx *c, int a, int b)
 	return ms;
 }
 
-}  // namespace
+}  // namespace vbi
 
 // =========================================================================================
 extern "C" {
@@ -617,6 +498,7 @@ void vbfm_destroy(vbfm_ctx *c)
 	dfree(c->ms_v); dfree(c->ms_w); dfree(c->hyp_w_d); dfree(c->hyp_v_d); dfree(c->group_d);
 	dfree(c->level_feats); dfree(c->dup); dfree(c->red_d); dfree(c->perm_d); dfree(c->chunks_d);
 	dfree(c->chunk_out_d); dfree(c->counters); dfree(c->stats);
+	mc_free(c);
 	if (c->comm) ncclCommDestroy(c->comm);
 	for (hipEvent_t e : c->pev) (void)hipEventDestroy(e);
 	for (int i = 0; i < EV_N; i++)
@@ -844,8 +726,8 @@ int vbfm_init_params_device(vbfm_ctx *c, uint64_t seed)
 {
 	if (!c) return fail(nullptr, "null context");
 	return guarded(c, [&] {
-		HIPCHK(vbk::init_normal_pairs(c->ms_w, c->D, seed, 11, c->s));
-		HIPCHK(vbk::init_normal_pairs(c->ms_v, (size_t)c->k * c->D, seed, 12, c->s));
+		HIPCHK(vbk::init_normal_pairs(c->ms_w, c->D, seed, 11, 0.1, .02, c->s));
+		HIPCHK(vbk::init_normal_pairs(c->ms_v, (size_t)c->k * c->D, seed, 12, 0.1, .02, c->s));
 		std::fill(c->hyp_w.begin(), c->hyp_w.end(), 1.0);
 		std::fill(c->hyp_v.begin(), c->hyp_v.end(), 1.0);
 		upload_hyp(c);
@@ -859,6 +741,7 @@ int vbfm_init_caches(vbfm_ctx *c)
 {
 	if (!c) return fail(nullptr, "null context");
 	return guarded(c, [&] {
+		if (c->mc) throw std::string("an MCMC / ALS context: use the vbfm_mcmc_* entry points");
 		require_train(c);
 		// fm_learn_vb_simultaneous.h:37-44: yhat of train and test, T of train, e = y - yhat
 		const int bl = blocked_predict(c, c->tr);
@@ -974,6 +857,7 @@ int vbfm_iterate(vbfm_ctx *c, vbfm_iter_stats *o)
 {
 	if (!c) return fail(nullptr, "null context");
 	return guarded(c, [&] {
+		if (c->mc) throw std::string("an MCMC / ALS context: use the vbfm_mcmc_* entry points");
 		require_train(c);
 		if (!c->e_test) throw std::string("no test data set (vbfm_set_test)");
 		vbfm_iter_stats st;

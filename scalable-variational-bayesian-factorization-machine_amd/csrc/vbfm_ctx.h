@@ -1,0 +1,151 @@
+// vbfm_ctx.h -- the learner context behind include/vbfm.h and the host-side helpers its
+// two front ends share: the VB learner (vbfm_capi.hip) and the MCMC / ALS learner
+// (vbfm_mcmc_capi.hip). Internal to libvbfm; not part of the ABI.
+#pragma once
+#include "vbfm_device.h"
+#include "../../include/vbfm.h"
+
+#include <rccl/rccl.h>
+
+#include <string>
+#include <vector>
+
+extern "C" const char *vbfm_host_last_error(void);
+extern "C" void vbfm_host_set_error(const char *msg);
+
+struct McState;   // vbfm_mcmc_capi.hip
+
+namespace vbi {
+
+struct DevData {
+	uint32_t n = 0, nf = 0;        // rows; columns of the transposed copy (padded to the global nf)
+	uint32_t nf_local = 0;
+	uint64_t nnz = 0;
+	uint64_t *col_ptr = nullptr;   // [nf+1]
+	uint2 *csc = nullptr;          // [nnz]
+	uint64_t *row_ptr = nullptr;   // [n+1]
+	uint2 *csr = nullptr;          // [nnz] feature-sorted rows
+	float *target = nullptr;       // [n]
+	float min_target = 0, max_target = 0;
+};
+
+struct HipError {
+	hipError_t e;
+	const char *what;
+};
+
+#define HIPCHK(x)                                                   \
+	do {                                                            \
+		hipError_t _e = (x);                                        \
+		if (_e != hipSuccess) throw HipError{_e, #x};               \
+	} while (0)
+
+#define NCCLCHK(x)                                                  \
+	do {                                                            \
+		ncclResult_t _r = (x);                                      \
+		if (_r != ncclSuccess) throw std::string("RCCL: ") + ncclGetErrorString(_r) + " in " #x; \
+	} while (0)
+
+template <class T> inline T *dalloc(size_t n)
+{
+	void *p = nullptr;
+	HIPCHK(hipMalloc(&p, (n ? n : 1) * sizeof(T)));
+	return (T *)p;
+}
+
+template <class T> inline void dfree(T *&p)
+{
+	if (p) (void)hipFree((void *)p);
+	p = nullptr;
+}
+
+enum { EV_BEGIN, EV_W0, EV_W, EV_V, EV_HYPER, EV_TEST, EV_N };
+
+}  // namespace vbi
+
+struct vbfm_ctx {
+	using DevData = vbi::DevData;
+	std::string err;
+	int dev = 0;
+	hipStream_t s = nullptr;
+	int k0 = 1, k1 = 1, k = 0;
+	uint32_t D = 0, G = 1;
+	std::vector<uint32_t> group_h, per_group;
+	uint32_t *group_d = nullptr;
+	float min_target = 0, max_target = 0;
+	DevData tr, te;
+	RowRec *rows = nullptr;
+	double *scratch_n = nullptr;   // yhat of train at init
+	double *e_test = nullptr, *pred_test = nullptr;
+	double2 *ms_v = nullptr, *ms_w = nullptr;
+	double *hyp_w_d = nullptr, *hyp_v_d = nullptr;
+	std::vector<double> hyp_w, hyp_v;
+	double alpha = 1.0, sigma_0 = 1.0, mu0 = 0.0, s0d = 0.02;
+	// schedule
+	std::vector<uint32_t> level_ptr, level_h, level_avg;
+	int q_ready[2] = {-1, -1};     // factor whose q-cache each slot holds (-1: none)
+	int qslot = 0;                 // slot reported by vbfm_get_rows
+	uint32_t *level_feats = nullptr;
+	uint8_t *dup = nullptr;
+	bool sched_ready = false;
+	// reductions
+	static constexpr uint32_t RED_BLOCKS = 512;
+	double *red_d = nullptr;
+	std::vector<double> red_h;
+	uint32_t *perm_d = nullptr;
+	vbk::Chunk *chunks_d = nullptr;
+	std::vector<vbk::Chunk> chunks_h;
+	double *chunk_out_d = nullptr;
+	uint32_t *counters = nullptr;
+	// row-sharded multi-GPU
+	int nranks = 1, rank = 0;
+	bool force_split = false;      // VBFM_FORCE_SPLIT=1: the multi-rank kernels on one rank
+	ncclComm_t comm = nullptr;
+	double2 *stats = nullptr;
+	uint32_t stats_cap = 0;
+	uint64_t n_global = 0;
+	uint32_t test_n_global = 0;
+	hipEvent_t ev[vbi::EV_N] = {};
+	// per-launch profiling (vbfm_set_profiling)
+	bool profiling = false;
+	std::vector<hipEvent_t> pev;
+	size_t pev_used = 0;
+	struct Span { size_t a; int kind; };   // kind 0 = v level, 1 = w level, 2 = qcache
+	std::vector<Span> spans;
+	McState *mc = nullptr;         // set by vbfm_mcmc_init: the context runs the MCMC / ALS learner
+};
+
+
+namespace vbi {
+
+int fail(vbfm_ctx *c, const std::string &m);
+
+template <class F> int guarded(vbfm_ctx *c, F &&fn)
+{
+	try {
+		if (c) HIPCHK(hipSetDevice(c->dev));
+		fn();
+		return 0;
+	} catch (const HipError &e) {
+		return fail(c, std::string("HIP error ") + hipGetErrorString(e.e) + " in " + e.what);
+	} catch (const std::string &m) {
+		return fail(c, m);
+	} catch (const char *m) {
+		return fail(c, m);
+	} catch (const std::bad_alloc &) {
+		return fail(c, "host out of memory");
+	}
+}
+
+void sync(vbfm_ctx *c);
+void allreduce_host(vbfm_ctx *c, double *v, int n);
+double finish_sum(vbfm_ctx *c, uint32_t nblocks);
+void require_train(vbfm_ctx *c);
+uint32_t nlevels(vbfm_ctx *c);
+size_t prof_begin(vbfm_ctx *c, int kind);
+void prof_end(vbfm_ctx *c, size_t a);
+int blocked_predict(const vbfm_ctx *c, const DevData &d);
+float ev_ms(vbfm_ctx *c, int a, int b);
+void mc_free(vbfm_ctx *c);   // vbfm_mcmc_capi.hip
+
+}  // namespace vbi

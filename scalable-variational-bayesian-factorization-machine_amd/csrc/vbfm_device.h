@@ -37,6 +37,7 @@ static_assert(sizeof(RowRec) == 64, "RowRec must be one 64-B line");
 enum {
 	CNT_NAN_MU_W = 0, CNT_NAN_SIGMA_W, CNT_INF_MU_W,
 	CNT_NAN_MU_V, CNT_NAN_SIGMA_V, CNT_INF_MU_V,
+	CNT_RNG_SKIP,   // MCMC: draws not taken (non-finite or zero variance)
 	CNT_N
 };
 
@@ -60,6 +61,35 @@ struct LevelArgs {
 	uint32_t ms_stride_next;
 	int slot;                  // q-cache slot of the factor being swept (v) / of factor 0 (w)
 	uint32_t avg_len;          // mean column length of the level (launch shape)
+};
+
+// per-level launch description for the MCMC / ALS draws (vbfm_mcmc.hip); parameters are
+// kept as double2 {value, 0} in the same feature-major layout as ms_v / ms_w so that the
+// prediction kernels serve both learners
+struct McArgs {
+	const uint64_t *col_ptr;
+	const uint2 *csc;
+	const uint32_t *feats;
+	uint32_t nfeat;
+	RowRec *rows;
+	double2 *par;              // v_f (at f, stride k) or w (stride 1)
+	uint32_t stride;
+	const double2 *par_next;   // v_{f+1} / v_0 for the fused q-cache, or nullptr
+	uint32_t next_stride;
+	const double *lambda;      // prior precision of (group g): lambda[g*hstride]
+	const double *mu;          // prior mean of (group g): mu[g*hstride]
+	uint32_t hstride;
+	const uint32_t *attr_group;
+	const uint8_t *dup;
+	double alpha;
+	const double *z;           // reference-RNG mode: standard normal of feature j, or nullptr
+	uint64_t rng_seed;         // device-RNG mode: counter-based normals keyed (seed, stream, j)
+	uint64_t rng_stream;
+	int sample;                // 0: ALS (conditional mean), 1: MCMC (draw)
+	uint32_t *counters;
+	double2 *stats;            // row-sharded mode: per-level-feature (sum h*e, sum h^2), or nullptr
+	int slot;
+	uint32_t avg_len;
 };
 
 // kernels launched from the C-ABI layer (vbfm_kernels.hip)
@@ -115,9 +145,32 @@ hipError_t sort_pairs_u32(void *tmp, size_t *tmp_bytes, const uint32_t *ki, uint
                           uint32_t *vo, size_t n, int bits, hipStream_t s);
 hipError_t exclusive_scan_u64(void *tmp, size_t *tmp_bytes, const uint64_t *in, uint64_t *out, size_t n,
                               hipStream_t s);
-hipError_t init_normal_pairs(double2 *ms, size_t n, uint64_t seed, uint64_t stream, hipStream_t s);
+// ms[i] = {scale * N(0,1), second}, counter-based (seed, stream, i)
+hipError_t init_normal_pairs(double2 *ms, size_t n, uint64_t seed, uint64_t stream, double scale, double second,
+                             hipStream_t s);
 // layout conversion between the reference's separate mu/sigma arrays ([f][j], f rows of
 // D) and the device's feature-major double2 pairs ([j][f]); rows = 1 for the w arrays
 hipError_t pack_pairs(const double *a, const double *b, double2 *out, uint32_t rows, size_t D, hipStream_t s);
 hipError_t unpack_pairs(const double2 *in, double *a, double *b, uint32_t rows, size_t D, hipStream_t s);
+// MCMC / ALS (vbfm_mcmc.hip); mode 0: fused, 1: statistics only (into a.stats),
+// 2: draw + correction from the (all-reduced) a.stats
+hipError_t mc_v_level(const McArgs &a, int mode, hipStream_t s);
+hipError_t mc_w_level(const McArgs &a, int mode, hipStream_t s);
+hipError_t mc_prior(const McArgs &a, uint32_t j0, uint32_t j1, int is_v, hipStream_t s);
+hipError_t mc_qcache(const uint64_t *row_ptr, const uint2 *csr, const double2 *par_f, uint32_t stride, RowRec *rows,
+                     uint32_t n, int slot, hipStream_t s);
+// per-block sums over rows; mode 0: e*e ; mode 1: e - w0
+hipError_t mc_row_sums(const RowRec *rows, uint32_t n, int mode, double w0, double *out, uint32_t nblocks,
+                       hipStream_t s);
+hipError_t mc_e_shift(RowRec *rows, uint32_t n, double d, hipStream_t s);
+hipError_t mc_train_update(RowRec *rows, const double *yhat, const float *target, uint32_t n, double mn, double mx,
+                           double *out, uint32_t nblocks, hipStream_t s);
+// per block: (sum err_this^2, sum |err_this|, sum err_all^2, sum |err_all|) at out[4*b]
+hipError_t mc_test_update(const double *e_test, const float *target, uint32_t n, double mn, double mx,
+                          double inv_iters, double *pred_this, double *pred_sum, double *out, uint32_t nblocks,
+                          hipStream_t s);
+// mode 0: sum p ; mode 1: sum (p - c)^2 per (w | factor f, group g) chunk
+hipError_t mc_param_sums(const double2 *pw, const double2 *pv, const uint32_t *perm, const Chunk *chunks,
+                         uint32_t nchunks, int mode, const double *cw, const double *cv, int k, double *out,
+                         hipStream_t s);
 }  // namespace vbk

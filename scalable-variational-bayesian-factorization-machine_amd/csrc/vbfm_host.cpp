@@ -3,9 +3,11 @@
 //                           reference's sscanf semantics, or the binary .x/.xt/.y triple
 //                           (src/util/fmatrix.h:46-52,66-82; src/util/matrix.h:296-312)
 //   * vbfm_init_params_host the reference's initial draws (glibc rand() after srand(seed),
-//                           Leva normals: src/util/random.h:150-176) in its exact order.
+//                           Leva normals: src/util/random.h:150-176) in its exact order, on
+//                           a private copy of that generator (vbfm_rng.h).
 // Plain C++; built with -ffp-contract=off like the reference's x86-64 build (no FMA).
 #include "../../include/vbfm.h"
+#include "vbfm_rng.h"
 
 #include <cmath>
 #include <cstdio>
@@ -189,33 +191,6 @@ int load_binary(const std::string &base, const char *ex, const char *ext, const 
 	return 0;
 }
 
-// ---- the reference's RNG path (glibc rand + Leva) ------------------------------------
-double ran_uniform() { return rand() / ((double)RAND_MAX + 1); }   // random.h:174-176
-
-double ran_gaussian()
-{
-	// Leva (1992), "A fast normal random number generator": ratio of uniforms with a
-	// quadratic squeeze (random.h:150-164)
-	double u, v, x, y, Q;
-	for (;;) {
-		do { u = ran_uniform(); } while (u == 0.0);
-		v = 1.7156 * (ran_uniform() - 0.5);
-		x = u - 0.449871;
-		y = std::fabs(v) + 0.386595;
-		Q = x * x + y * (0.19600 * y - 0.25472 * x);
-		if (Q < 0.27597) return v / u;
-		if (Q > 0.27846) continue;
-		if ((v * v) > (-4.0 * u * u * std::log(u))) continue;
-		return v / u;
-	}
-}
-
-double ran_gaussian(double mean, double stdev)   // random.h:166-172
-{
-	if ((stdev == 0.0) || std::isnan(stdev)) return mean;
-	return mean + stdev * ran_gaussian();
-}
-
 }  // namespace
 
 extern "C" {
@@ -250,22 +225,22 @@ int vbfm_init_params_host(uint32_t seed, double init_stdev, int32_t k, uint32_t 
 		return -1;
 	}
 	const size_t kd = (size_t)k * D;
-	srand(seed);                                                       // libfm.cpp:123-124
+	vbrng::Glibc rng(seed);                                            // srand(seed), libfm.cpp:123-124
 	for (size_t i = 0; i < kd; i++) {                                  // fm_model::init (fm_model.h:97)
-		const double v = ran_gaussian(0, init_stdev);
+		const double v = rng.gaussian(0, init_stdev);
 		if (fm_v) fm_v[i] = v;
 	}
 	for (uint32_t i = 0; i < D; i++) {                                 // libfm.cpp:307
-		const double w = ran_gaussian(0, init_stdev);
+		const double w = rng.gaussian(0, init_stdev);
 		if (fm_w) fm_w[i] = w;
 	}
 	// fm_learn_vb::init (fm_learn_vb.h:693-712)
 	p->alpha = 1.0; p->sigma_0 = 1.0; p->mu_0_dash = 0.0; p->sigma_0_dash = 0.02;
 	for (uint32_t g = 0; g < G; g++) p->hyp_sigma_w[g] = 1;
 	for (size_t i = 0; i < (size_t)G * k; i++) p->hyp_sigma_v[i] = 1;
-	for (uint32_t i = 0; i < D; i++) p->mu_w[i] = 0.1 * ran_gaussian(0, 1);   // DVectorDoubleVB::init_normal
+	for (uint32_t i = 0; i < D; i++) p->mu_w[i] = 0.1 * rng.gaussian(0, 1);   // DVectorDoubleVB::init_normal
 	for (uint32_t i = 0; i < D; i++) p->sigma_w[i] = .02;
-	for (size_t i = 0; i < kd; i++) p->mu_v[i] = 0.1 * ran_gaussian(0, 1);   // DMatrixDoubleVB::init_normal
+	for (size_t i = 0; i < kd; i++) p->mu_v[i] = 0.1 * rng.gaussian(0, 1);   // DMatrixDoubleVB::init_normal
 	for (size_t i = 0; i < kd; i++) p->sigma_v[i] = .02;
 	return 0;
 }

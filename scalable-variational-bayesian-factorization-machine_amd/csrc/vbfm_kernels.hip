@@ -848,15 +848,15 @@ __global__ void k_count_features(const uint2 *csr, uint64_t nnz, unsigned long l
 	if (i < nnz) atomicAdd(&counts[csr[i].x], 1ull);
 }
 
-// {0.1 * N(0,1), .02}: Box-Muller on two splitmix64 uniforms in (0, 1]
-__global__ void k_init_normal_pairs(double2 *ms, size_t n, uint64_t seed, uint64_t stream)
+// {scale * N(0,1), second}: Box-Muller on two splitmix64 uniforms in (0, 1]
+__global__ void k_init_normal_pairs(double2 *ms, size_t n, uint64_t seed, uint64_t stream, double scale, double second)
 {
 	const size_t i = (size_t)blockIdx.x * 256u + threadIdx.x;
 	if (i >= n) return;
 	const double u1 = ((double)(hstream(seed, stream, 2 * i) >> 11) + 1.0) * 0x1p-53;
 	const double u2 = (double)(hstream(seed, stream, 2 * i + 1) >> 11) * 0x1p-53;
 	const double z = sqrt(-2.0 * log(u1)) * cos(6.283185307179586 * u2);
-	ms[i] = make_double2(0.1 * z, .02);
+	ms[i] = make_double2(scale * z, second);
 }
 
 // out[j*rows + f] = {a[f*D + j], b[f*D + j]}
@@ -1094,10 +1094,11 @@ hipError_t exclusive_scan_u64(void *tmp, size_t *tmp_bytes, const uint64_t *in, 
 	return rocprim::exclusive_scan(tmp, *tmp_bytes, in, out, (uint64_t)0, n, rocprim::plus<uint64_t>(), s);
 }
 
-hipError_t init_normal_pairs(double2 *ms, size_t n, uint64_t seed, uint64_t stream, hipStream_t s)
+hipError_t init_normal_pairs(double2 *ms, size_t n, uint64_t seed, uint64_t stream, double scale, double second,
+                             hipStream_t s)
 {
 	if (n == 0) return hipSuccess;
-	k_init_normal_pairs<<<grid_for(n), 256, 0, s>>>(ms, n, seed, stream);
+	k_init_normal_pairs<<<grid_for(n), 256, 0, s>>>(ms, n, seed, stream, scale, second);
 	return hipGetLastError();
 }
 

@@ -1,4 +1,4 @@
-// host/libfm_main.cpp -- drop-in for the reference's `bin/libFM -method vb` on MI355X.
+// host/libfm_main.cpp -- drop-in for the reference's `bin/libFM -method vb | mcmc | als` on MI355X.
 //
 // Mirrors main() of src/libfm/libfm.cpp (flag surface, defaults, RNG order, output lines and
 // files) and the iteration loop of fm_learn_vb_simultaneous::_learn
@@ -7,7 +7,7 @@
 //   * -seed is honoured (the reference seeds with time(NULL) and ignores it, libfm.cpp:123);
 //   * -out writes the clipped test predictions of the last iteration (the reference's VB
 //     predict() body is commented out and leaves the vector uninitialised, fm_learn_vb.h:321);
-//   * -method mcmc/als/sgd/... and -task c are rejected with an error instead of running
+//   * -method sgd/sgda/... and -task c are rejected with an error instead of running
 //     other learners; -relation is not supported;
 //   * extra flags: -device (HIP ordinal), -vfile 0 (skip writing v_file.txt).
 #include "../../include/vbfm.h"
@@ -137,6 +137,129 @@ void load(const std::string &fn, Data &d, const char *what)
 
 }  // namespace
 
+// -method mcmc | als (libfm.cpp:131-135, 297-305, 367-411; fm_learn_mcmc_simultaneous.h:50-305)
+struct McmcRun {
+	bool sample;
+	uint32_t seed;
+	double init_stdev;
+	uint32_t num_iter;
+	std::vector<double> reg;
+	const uint32_t *groups;
+	uint32_t G, D;
+	int k0, k1, k;
+	int32_t device;
+	bool vfile;
+	std::string rlog_file, out_file;
+};
+
+static void run_mcmc(const McmcRun &r, Data &train, Data &test)
+{
+	vbfm_ctx *ctx = nullptr;
+	try {
+		vbfm_config cfg{r.k0, r.k1, r.k, r.D, r.G, r.groups, train.h.min_target, train.h.max_target, r.device, 0};
+		check(vbfm_create(&ctx, &cfg), nullptr);
+		const vbfm_csc tr = train.csc(), te = test.csc();
+		check(vbfm_set_train(ctx, &tr), ctx);
+		check(vbfm_set_test(ctx, &te), ctx);
+		vbfm_mcmc_config mc{r.sample, r.sample, VBFM_RNG_REFERENCE, r.seed, r.init_stdev,
+		                    r.reg.empty() ? nullptr : r.reg.data(), (int32_t)r.reg.size()};
+		check(vbfm_mcmc_init(ctx, &mc), ctx);
+		const size_t kd = (size_t)r.k * r.D, gk = (size_t)r.G * r.k;
+		std::vector<double> w(r.D), v(kd), wmu(r.G), wl(r.G), vmu(gk), vl(gk);
+		vbfm_mcmc_params p{w.data(), v.data(), wmu.data(), wl.data(), vmu.data(), vl.data(), 0, 0, 0};
+		if (r.vfile) {   // fm_model.h:98: the initial factors (DMatrix::save, matrix.h:129-152)
+			check(vbfm_mcmc_get_params(ctx, &p), ctx);
+			std::ofstream vf("v_file.txt");
+			for (int f = 0; f < r.k; f++) {
+				for (uint32_t j = 0; j < r.D; j++) vf << (j ? "\t" : "") << v[(size_t)f * r.D + j];
+				vf << std::endl;
+			}
+		}
+		std::ofstream *rlog_out = nullptr;
+		RLog *rlog = nullptr;
+		if (!r.rlog_file.empty()) {   // fm_learn::init + fm_learn_mcmc::init fields (:1118-1149)
+			rlog_out = new std::ofstream(r.rlog_file.c_str());
+			if (!rlog_out->is_open()) throw std::string("Unable to open file " + r.rlog_file);
+			std::cout << "logging to " << r.rlog_file << std::endl;
+			rlog = new RLog(rlog_out);
+			for (const char *f : {"rmse", "mae", "time_pred", "time_learn", "time_learn2", "time_learn4", "alpha",
+			                      "rmse_mcmc_this", "rmse_mcmc_all", "rmse_mcmc_all_but5"})
+				rlog->add(f);
+			for (uint32_t g = 0; g < r.G; g++) {
+				std::ostringstream ss;
+				ss << "wmu[" << g << "]"; rlog->add(ss.str()); ss.str("");
+				ss << "wlambda[" << g << "]"; rlog->add(ss.str()); ss.str("");
+				for (int f = 0; f < r.k; f++) {
+					ss << "vmu[" << g << "," << f << "]"; rlog->add(ss.str()); ss.str("");
+					ss << "vlambda[" << g << "," << f << "]"; rlog->add(ss.str()); ss.str("");
+				}
+			}
+			rlog->init();
+		}
+		std::cout << "in mcmc learn" << std::endl << "preprocess complete" << std::endl;
+		check(vbfm_mcmc_init_caches(ctx), ctx);
+		std::ostringstream tag;
+		tag << r.k0 << r.k1 << r.k;
+		const std::string f_rmse = "test_rmse_" + tag.str() + "_mcmc";
+		{ std::ofstream a(f_rmse.c_str()); }   // truncate (:52-62)
+		for (uint32_t it = 0; it < r.num_iter; it++) {
+			const double t_user = usertime();
+			const clock_t t_clock = clock();
+			const double t_wall = (double)time(NULL);
+			vbfm_mcmc_stats st;
+			check(vbfm_mcmc_iterate(ctx, &st), ctx);
+			// :104-127
+			const struct { const char *name; uint32_t nan, inf; } rep[] = {
+				{"alpha", st.nan_alpha, st.inf_alpha}, {"w0", st.nan_w0, st.inf_w0}, {"w", st.nan_w, st.inf_w},
+				{"v", st.nan_v, st.inf_v}, {"w_mu", st.nan_w_mu, st.inf_w_mu},
+				{"w_lambda", st.nan_w_lambda, st.inf_w_lambda}, {"v_mu", st.nan_v_mu, st.inf_v_mu},
+				{"v_lambda", st.nan_v_lambda, st.inf_v_lambda}};
+			for (const auto &q : rep)
+				if (q.nan > 0 || q.inf > 0)
+					std::cout << "#nans in " << q.name << ":\t" << q.nan << "\t#inf_in_" << q.name << ":\t" << q.inf
+					          << std::endl;
+			if (rlog) {
+				check(vbfm_mcmc_get_params(ctx, &p), ctx);
+				rlog->log("alpha", st.alpha);
+				for (uint32_t g = 0; g < r.G; g++) {
+					std::ostringstream ss;
+					ss << "wmu[" << g << "]"; rlog->log(ss.str(), wmu[g]); ss.str("");
+					ss << "wlambda[" << g << "]"; rlog->log(ss.str(), wl[g]); ss.str("");
+					for (int f = 0; f < r.k; f++) {
+						ss << "vmu[" << g << "," << f << "]"; rlog->log(ss.str(), vmu[(size_t)g * r.k + f]); ss.str("");
+						ss << "vlambda[" << g << "," << f << "]"; rlog->log(ss.str(), vl[(size_t)g * r.k + f]); ss.str("");
+					}
+				}
+				rlog->log("time_learn", usertime() - t_user);
+				rlog->log("time_learn2", (double)(clock() - t_clock) / CLOCKS_PER_SEC);
+				rlog->log("time_learn4", (double)time(NULL) - t_wall);
+				rlog->log("rmse", st.rmse_all);
+				rlog->log("mae", st.mae_all);
+				rlog->log("rmse_mcmc_this", st.rmse_this);
+				rlog->log("rmse_mcmc_all", st.rmse_all);
+				rlog->newline();
+			}
+			std::cout << "#Iter=" << std::setw(3) << it << "\tTrain=" << st.train_rmse << "\tTest=" << st.rmse_all
+			          << std::endl;
+			std::ofstream fr(f_rmse.c_str(), std::ios_base::app);
+			fr << st.rmse_all << "\n";
+		}
+		std::cout << "after learn" << std::endl;   // libfm.cpp:507; no Final line for mcmc (:509)
+		if (!r.out_file.empty()) {                 // libfm.cpp:514-519
+			std::vector<double> pred(test.h.num_rows);
+			check(vbfm_mcmc_get_test_pred(ctx, (int32_t)r.num_iter, pred.data()), ctx);
+			std::ofstream o(r.out_file.c_str());
+			for (double x : pred) o << x << std::endl;
+		}
+		delete rlog;
+		delete rlog_out;
+		vbfm_destroy(ctx);
+	} catch (...) {
+		if (ctx) vbfm_destroy(ctx);
+		throw;
+	}
+}
+
 int main(int argc, char **argv)
 {
 	vbfm_ctx *ctx = nullptr;
@@ -153,7 +276,7 @@ int main(int argc, char **argv)
 		cmd.reg("validation", "filename for validation data (only for SGDA)");
 		const std::string p_out = cmd.reg("out", "filename for output");
 		const std::string p_dim = cmd.reg("dim", "'k0,k1,k2': k0=use bias, k1=use 1-way interactions, k2=dim of 2-way interactions; default=1,1,8");
-		cmd.reg("regular", "'r0,r1,r2' for SGD and ALS: r0=bias regularization, r1=1-way regularization, r2=2-way regularization");
+		const std::string p_reg = cmd.reg("regular", "'r0,r1,r2' for SGD and ALS: r0=bias regularization, r1=1-way regularization, r2=2-way regularization");
 		const std::string p_init = cmd.reg("init_stdev", "stdev for initialization of 2-way factors; default=0.1");
 		cmd.reg("stdev", "standard deviation for the model; default=1");
 		const std::string p_iter = cmd.reg("iter", "number of iterations; default=100");
@@ -173,9 +296,10 @@ int main(int argc, char **argv)
 
 		const uint32_t seed = cmd.has(p_seed) ? (uint32_t)cmd.geti(p_seed, 0) : (uint32_t)time(NULL);
 		const std::string method = cmd.get(p_method, "mcmc");
-		if (method != "vb") throw std::string("method " + method + " is not provided by this build (use -method vb)");
-		if (cmd.get(p_task) != "r") throw std::string("unknown task");   // VB regression only
-		if (!cmd.list(p_rel).empty()) throw std::string("-relation is not supported by the VB learner");
+		if (method != "vb" && method != "mcmc" && method != "als")
+			throw std::string("method " + method + " is not provided by this build (use -method vb, mcmc or als)");
+		if (cmd.get(p_task) != "r") throw std::string("unknown task");   // regression only
+		if (!cmd.list(p_rel).empty()) throw std::string("-relation is not supported by this build");
 
 		Data train, test;
 		load(cmd.get(p_train), train, "train");
@@ -204,6 +328,16 @@ int main(int argc, char **argv)
 		const int k0 = atoi(dim[0].c_str()) != 0, k1 = atoi(dim[1].c_str()) != 0, k = atoi(dim[2].c_str());
 		const double init_stdev = cmd.getd(p_init, 0.1);
 		const uint32_t num_iter = (uint32_t)cmd.geti(p_iter, 100);
+
+		if (method != "vb") {
+			std::vector<double> reg;
+			for (const std::string &r : cmd.list(p_reg)) reg.push_back(atof(r.c_str()));
+			McmcRun run{method == "mcmc", seed, init_stdev, num_iter, reg, cmd.has(p_meta) ? groups.data() : nullptr,
+			            G, D, k0, k1, k, (int32_t)cmd.geti(p_dev, 0), cmd.geti(p_vfile, 1) != 0,
+			            cmd.has(p_rlog) ? cmd.get(p_rlog) : std::string(), cmd.has(p_out) ? cmd.get(p_out) : std::string()};
+			run_mcmc(run, train, test);
+			return 0;
+		}
 
 		// fm.init + fm.w.init_normal + fml->init draws (libfm.cpp:123-366) on the host
 		const size_t kd = (size_t)k * D;

@@ -1,6 +1,7 @@
 """vbfm -- Python host side of libvbfm.so (the MI355X VB factorization machine).
 
-Mirrors the reference's learner interface for `-method vb` so that driver code reads like
+Mirrors the reference's learner interface for `-method vb` (FMLearnVB) and
+`-method mcmc | als` (FMLearnMCMC) so that driver code reads like
 the reference's main() (src/libfm/libfm.cpp:137-511):
 
     train = DataSubset.load("train.libfm")            # Data::load          (Data.h:106-283)
@@ -75,6 +76,34 @@ class IterStats(C.Structure):
         return {k: getattr(self, k) for k, _ in self._fields_}
 
 
+RNG_REFERENCE, RNG_DEVICE = 0, 1
+
+
+class McmcConfig(C.Structure):
+    _fields_ = [("do_sample", C.c_int32), ("do_multilevel", C.c_int32), ("rng", C.c_int32), ("seed", C.c_uint32),
+                ("init_stdev", C.c_double), ("regular", P_f64), ("num_regular", C.c_int32)]
+
+
+class McmcParams(C.Structure):
+    _fields_ = [("w", P_f64), ("v", P_f64), ("w_mu", P_f64), ("w_lambda", P_f64), ("v_mu", P_f64),
+                ("v_lambda", P_f64), ("w0", C.c_double), ("alpha", C.c_double), ("reg0", C.c_double)]
+
+
+class McmcStats(C.Structure):
+    _fields_ = ([("rmse_all", C.c_double), ("mae_all", C.c_double), ("rmse_this", C.c_double),
+                 ("mae_this", C.c_double), ("train_rmse", C.c_double), ("alpha", C.c_double), ("w0", C.c_double)]
+                + [(n, C.c_uint32) for n in ("nan_alpha", "inf_alpha", "nan_w0", "inf_w0", "nan_w", "inf_w",
+                                             "nan_v", "inf_v", "nan_w_mu", "inf_w_mu", "nan_w_lambda",
+                                             "inf_w_lambda", "nan_v_mu", "inf_v_mu", "nan_v_lambda",
+                                             "inf_v_lambda", "rng_skipped")]
+                + [("num_levels", C.c_int32), ("ms_hyper", C.c_double), ("ms_w", C.c_double), ("ms_v", C.c_double),
+                   ("ms_predict", C.c_double), ("ms_total", C.c_double), ("ms_vlevel_kernels", C.c_double),
+                   ("n_vlevel_launches", C.c_int32), ("nnz_train", C.c_uint64)])
+
+    def as_dict(self):
+        return {k: getattr(self, k) for k, _ in self._fields_}
+
+
 class HostData(C.Structure):
     _fields_ = [("num_rows", C.c_uint32), ("num_feature", C.c_uint32), ("nnz", C.c_uint64),
                 ("min_target", C.c_float), ("max_target", C.c_float), ("target", P_f32),
@@ -88,7 +117,8 @@ EXPORTS = ["vbfm_abi_version", "vbfm_last_error", "vbfm_create", "vbfm_destroy",
            "vbfm_step_w0", "vbfm_step_w", "vbfm_step_qcache", "vbfm_step_v", "vbfm_step_hyper",
            "vbfm_free_energy", "vbfm_get_rows", "vbfm_get_test_e", "vbfm_factor_sweep", "vbfm_set_profiling",
            "vbfm_comm_unique_id", "vbfm_comm_init", "vbfm_load_data", "vbfm_free_host_data",
-           "vbfm_init_params_host"]
+           "vbfm_init_params_host", "vbfm_mcmc_init", "vbfm_mcmc_set_params", "vbfm_mcmc_get_params",
+           "vbfm_mcmc_init_caches", "vbfm_mcmc_iterate", "vbfm_mcmc_get_test_pred", "vbfm_mcmc_factor_sweep"]
 
 _lib = None
 
@@ -135,6 +165,13 @@ def lib():
         L.vbfm_free_host_data.restype = None
         L.vbfm_init_params_host.argtypes = [C.c_uint32, C.c_double, C.c_int32, C.c_uint32, C.c_uint32,
                                             C.POINTER(Params), P_f64, P_f64]
+        L.vbfm_mcmc_init.argtypes = [V, C.POINTER(McmcConfig)]
+        L.vbfm_mcmc_set_params.argtypes = [V, C.POINTER(McmcParams)]
+        L.vbfm_mcmc_get_params.argtypes = [V, C.POINTER(McmcParams)]
+        L.vbfm_mcmc_init_caches.argtypes = [V]
+        L.vbfm_mcmc_iterate.argtypes = [V, C.POINTER(McmcStats)]
+        L.vbfm_mcmc_get_test_pred.argtypes = [V, C.c_int32, P_f64]
+        L.vbfm_mcmc_factor_sweep.argtypes = [V, P_f64]
         _lib = L
     return _lib
 
@@ -409,3 +446,69 @@ class FMLearnVB:
             self.close()
         except Exception:
             pass
+
+
+class FMLearnMCMC(FMLearnVB):
+    """fm_learn_mcmc_simultaneous on one MI355X (src/libfm/src/fm_learn_mcmc_simultaneous.h).
+
+    method "mcmc" samples with hyper-prior inference, "als" is the same learner with neither
+    (libfm.cpp:131-135). rng=RNG_REFERENCE replays the reference's rand() stream (draws
+    identical to the reference's on the same inputs), RNG_DEVICE draws the per-attribute
+    normals from a counter-based generator on the device (bench scale)."""
+
+    def __init__(self, k0=1, k1=1, num_factor=8, num_attribute=0, attr_group=None,
+                 min_target=1.0, max_target=5.0, device=0, method="mcmc"):
+        if method not in ("mcmc", "als"):
+            raise VbfmError("method must be mcmc or als")
+        super().__init__(k0, k1, num_factor, num_attribute, attr_group, min_target, max_target, device)
+        self.method = method
+
+    def init(self, seed, init_stdev=0.1, regular=(), rng=RNG_REFERENCE):
+        """srand(seed); fm.init(); fm.w.init_normal(); fml->init(); -regular (libfm.cpp:123-411)."""
+        sample = 1 if self.method == "mcmc" else 0
+        self._reg = np.ascontiguousarray(list(regular), dtype=np.float64)
+        cfg = McmcConfig(sample, sample, rng, seed, init_stdev, _ptr(self._reg, P_f64) if len(self._reg) else None,
+                         len(self._reg))
+        _check(lib().vbfm_mcmc_init(self._ctx, C.byref(cfg)), self._ctx)
+
+    def init_device(self, seed, init_stdev=0.1):
+        self.init(seed, init_stdev, rng=RNG_DEVICE)
+
+    def _mc_struct(self, arrs):
+        return McmcParams(*[_ptr(arrs.get(k), P_f64) for k in ("w", "v", "w_mu", "w_lambda", "v_mu", "v_lambda")],
+                          arrs.get("w0", 0.0), arrs.get("alpha", 1.0), arrs.get("reg0", 0.0))
+
+    def get_params(self):
+        p = {"w": np.zeros(self.D), "v": np.zeros(self.k * self.D), "w_mu": np.zeros(self.G),
+             "w_lambda": np.zeros(self.G), "v_mu": np.zeros(self.G * self.k), "v_lambda": np.zeros(self.G * self.k)}
+        ps = self._mc_struct(p)
+        _check(lib().vbfm_mcmc_get_params(self._ctx, C.byref(ps)), self._ctx)
+        p.update(w0=ps.w0, alpha=ps.alpha, reg0=ps.reg0)
+        return p
+
+    def set_params(self, p):
+        cur = self.get_params()
+        cur.update({k: np.ascontiguousarray(v, dtype=np.float64) if isinstance(v, np.ndarray) else v
+                    for k, v in p.items()})
+        _check(lib().vbfm_mcmc_set_params(self._ctx, C.byref(self._mc_struct(cur))), self._ctx)
+
+    def init_caches(self):
+        _check(lib().vbfm_mcmc_init_caches(self._ctx), self._ctx)
+
+    def iterate(self):
+        st = McmcStats()
+        _check(lib().vbfm_mcmc_iterate(self._ctx, C.byref(st)), self._ctx)
+        self.num_iter_done += 1
+        return st
+
+    def predict(self, num_iter=None):
+        """fm_learn_mcmc::predict (fm_learn_mcmc.h:355-381)."""
+        out = np.zeros(self.n_test)
+        n = self.num_iter_done if num_iter is None else num_iter
+        _check(lib().vbfm_mcmc_get_test_pred(self._ctx, n, _ptr(out, P_f64)), self._ctx)
+        return out
+
+    def factor_sweep(self):
+        ms = C.c_double()
+        _check(lib().vbfm_mcmc_factor_sweep(self._ctx, C.byref(ms)), self._ctx)
+        return ms.value

@@ -126,11 +126,76 @@ def tiny_dataset(path_train, path_test, dup=False):
                 fh.write(" ".join(["%g" % y] + ["%d:%.9g" % (j, float(x)) for j, x in ents]) + "\n")
 
 
+def mcmc_cases(ref):
+    """-method mcmc / als traces and final states (fm_learn_mcmc_simultaneous.h)."""
+    for case in ("tiny", "tiny_dup"):
+        d = os.path.join(HERE, case)
+        tr, te = os.path.join(d, "train.libfm"), os.path.join(d, "test.libfm")
+        out, arr = run_ref(ref, "mcmc", tr, te, "1,1,3", 6, 5)
+        nums, trace = parse_mcmc(out)
+        save_case(case + "/mcmc", nums, trace, arr, {"dim": "1,1,3", "seed": 5, "init_stdev": 0.1, "iter": 6})
+    d = os.path.join(HERE, "tiny")
+    tr, te, meta = (os.path.join(d, n) for n in ("train.libfm", "test.libfm", "groups.meta"))
+    out, arr = run_ref(ref, "mcmc", tr, te, "1,1,2", 5, 11, extra=["--meta", meta, "--init_stdev", "0.2"])
+    nums, trace = parse_mcmc(out)
+    save_case("tiny/mcmc_meta", nums, trace, arr,
+              {"dim": "1,1,2", "seed": 11, "init_stdev": 0.2, "iter": 5, "meta": "groups.meta"})
+    for case in ("tiny", "tiny_dup"):
+        dc = os.path.join(HERE, case)
+        out, arr = run_ref(ref, "als", os.path.join(dc, "train.libfm"), os.path.join(dc, "test.libfm"), "1,1,3", 6, 5,
+                           extra=["--regular", "0.5,1,2"])
+        nums, trace = parse_mcmc(out)
+        save_case(case + "/als_reg", nums, trace, arr,
+                  {"dim": "1,1,3", "seed": 5, "init_stdev": 0.1, "iter": 6, "regular": [0.5, 1.0, 2.0]})
+    reg = [0.25, 0.5, 1.0, 2.0, 0.75, 1.5, 3.0]
+    out, arr = run_ref(ref, "als", tr, te, "0,1,2", 5, 11,
+                       extra=["--meta", meta, "--regular", ",".join(str(r) for r in reg)])
+    nums, trace = parse_mcmc(out)
+    save_case("tiny/als_meta_reg", nums, trace, arr,
+              {"dim": "0,1,2", "seed": 11, "init_stdev": 0.1, "iter": 5, "meta": "groups.meta", "regular": reg})
+    tmp = tempfile.mkdtemp()
+    spec = {"n_rows": 20000, "n_fields": 10, "ids_per_field": 200, "seed": 7, "xmode": 1,
+            "test_rows": 2000, "test_seed": 8}
+    rp, f, v, y = synth.generate(spec["n_rows"], spec["n_fields"], spec["ids_per_field"], spec["seed"], 1)
+    synth.write_libfm(os.path.join(tmp, "tr.libfm"), rp, f, v, y)
+    rp, f, v, y = synth.generate(spec["test_rows"], spec["n_fields"], spec["ids_per_field"], spec["test_seed"], 1)
+    synth.write_libfm(os.path.join(tmp, "te.libfm"), rp, f, v, y)
+    out, arr = run_ref(ref, "mcmc", os.path.join(tmp, "tr.libfm"), os.path.join(tmp, "te.libfm"), "1,1,4", 5, 7)
+    nums, trace = parse_mcmc(out)
+    save_case("synth_mcmc", nums, trace, {k: arr[k] for k in arr if k.startswith("final")},
+              dict(spec, dim="1,1,4", init_stdev=0.1, iter=5))
+    shutil.rmtree(tmp)
+    sa = os.path.join(HERE, "sa_split")
+    tmp = tempfile.mkdtemp()
+    for part in ("train", "test"):
+        with gzip.open(os.path.join(sa, part + ".libfm.gz"), "rt") as fi, \
+                open(os.path.join(tmp, part + ".libfm"), "w") as fo:
+            fo.write(fi.read())
+    out, arr = run_ref(ref, "mcmc", os.path.join(tmp, "train.libfm"), os.path.join(tmp, "test.libfm"),
+                       "1,1,8", 10, 42)
+    nums, trace = parse_mcmc(out)
+    save_case("sa_mcmc", nums, trace, {k: arr[k] for k in arr if k.startswith("final_mcmc") or k.endswith("_mu")
+                                       or k.endswith("_lambda")},
+              {"dim": "1,1,8", "seed": 42, "init_stdev": 0.1, "iter": 10,
+               "array_sums": {k: [float(np.sum(arr[k])), float(np.sum(arr[k] ** 2))] for k in arr}})
+    shutil.rmtree(tmp)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--ref", default=os.path.join(HERE, "..", "..", "oracle", "_ref", "ref_driver"))
+    ap.add_argument("--only", default="", help="comma list of groups: rng,tiny,meta,synth,sa,mcmc")
     args = ap.parse_args()
     ref = os.path.abspath(args.ref)
+    only = set(filter(None, args.only.split(",")))
+
+    def want(group):
+        return not only or group in only
+
+    if want("mcmc"):
+        mcmc_cases(ref)
+    if only == {"mcmc"}:
+        return
 
     # --- RNG known answers: glibc rand() as the reference calls it (random.h:174-176)
     libc = ctypes.CDLL(None)

@@ -44,7 +44,10 @@ class OrALS(C.Structure):
                 ("v_lambda", P_f64), ("w_mu", P_f64), ("v_mu", P_f64),
                 ("n_train", C.c_uint32), ("n_test", C.c_uint32), ("e", P_f64), ("q", P_f64),
                 ("e_test", P_f64), ("q_test", P_f64), ("pred_sum_all", P_f64), ("pred_this", P_f64),
-                ("min_target", C.c_float), ("max_target", C.c_float), ("iter_done", C.c_uint32)]
+                ("min_target", C.c_float), ("max_target", C.c_float), ("iter_done", C.c_uint32),
+                ("do_sample", C.c_int), ("do_multilevel", C.c_int), ("reg0", C.c_double),
+                ("nan_w", C.c_uint32), ("inf_w", C.c_uint32), ("nan_v", C.c_uint32), ("inf_v", C.c_uint32),
+                ("tmp_g", P_f64)]
 
 
 ALLREDUCE_FN = C.CFUNCTYPE(None, P_f64, C.c_int, C.c_void_p)
@@ -86,6 +89,9 @@ def lib():
         L.or_als_iterate.argtypes = [C.POINTER(OrALS), C.POINTER(OrData), C.POINTER(OrData),
                                      P_f64, P_f64, P_f64]
         L.or_als_destroy.argtypes = [C.POINTER(OrALS)]
+        L.or_als_configure.argtypes = [C.POINTER(OrALS), C.c_int, C.c_int, C.c_double]
+        L.or_ran_gamma.argtypes = [C.c_double]
+        L.or_ran_gamma.restype = C.c_double
         _lib = L
     return _lib
 
@@ -189,9 +195,23 @@ class VB:
 
 
 class ALS:
-    def __init__(self, k0, k1, k, D, attr_group=None):
+    """fm_learn_mcmc: method "als" (no sampling, no hyper-prior inference) or "mcmc"."""
+
+    def __init__(self, k0, k1, k, D, attr_group=None, method="als", reg0=0.0):
         self.s = OrALS()
-        lib().or_als_create(C.byref(self.s), int(k0), int(k1), int(k), int(D), None)
+        self._groups = None if attr_group is None else np.ascontiguousarray(attr_group, dtype=np.uint32)
+        gp = None if self._groups is None else self._groups.ctypes.data_as(P_u32)
+        lib().or_als_create(C.byref(self.s), int(k0), int(k1), int(k), int(D), gp)
+        mc = method == "mcmc"
+        lib().or_als_configure(C.byref(self.s), int(mc), int(mc), float(reg0))
+
+    def set_lambda(self, w_lambda, v_lambda):
+        """-regular (libfm.cpp:367-411): w_lambda[G], v_lambda[G*k] at [g*k + f]"""
+        s = self.s
+        for i, x in enumerate(np.asarray(w_lambda, dtype=np.float64).ravel()):
+            s.w_lambda[i] = x
+        for i, x in enumerate(np.asarray(v_lambda, dtype=np.float64).ravel()):
+            s.v_lambda[i] = x
 
     def init_params(self, seed, init_stdev=0.1):
         lib().or_als_init_params(C.byref(self.s), seed, init_stdev)
@@ -208,7 +228,9 @@ class ALS:
 
     def params(self):
         s = self.s
-        return {"w": arr(s.w, s.D), "v": arr(s.v, s.k * s.D), "w0": s.w0}
+        return {"w": arr(s.w, s.D), "v": arr(s.v, s.k * s.D), "w0": s.w0, "alpha": s.alpha,
+                "w_mu": arr(s.w_mu, s.G), "w_lambda": arr(s.w_lambda, s.G),
+                "v_mu": arr(s.v_mu, s.G * s.k), "v_lambda": arr(s.v_lambda, s.G * s.k)}
 
     def __del__(self):
         try:

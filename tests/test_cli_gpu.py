@@ -31,8 +31,8 @@ def same6(a, b):
     return abs(fa - fb) <= 1.01 * 10 ** (np.floor(np.log10(abs(fb))) - 5)
 
 
-def run_cli(tmp_path, train, test, dim, iters, seed, extra=()):
-    out = subprocess.run([CLI, "-task", "r", "-train", train, "-test", test, "-method", "vb", "-dim", dim,
+def run_cli(tmp_path, train, test, dim, iters, seed, extra=(), method="vb"):
+    out = subprocess.run([CLI, "-task", "r", "-train", train, "-test", test, "-method", method, "-dim", dim,
                           "-iter", str(iters), "-seed", str(seed)] + list(extra),
                          cwd=str(tmp_path), capture_output=True, text=True, timeout=600)
     assert "ERROR" not in out.stderr, out.stderr
@@ -96,3 +96,40 @@ def test_cli_binary_input(tmp_path):
     b = run_cli(tmp_path, str(tmp_path / "trb"), str(tmp_path / "teb"), "1,1,3", 3, 9, ["-vfile", "0"])
     ia = re.findall(r"#Iter=.*", a)
     assert len(ia) == 3 and ia == re.findall(r"#Iter=.*", b)
+
+
+@pytest.mark.parametrize("case", ["tiny/mcmc", "tiny/mcmc_meta", "tiny/als", "tiny/als_meta_reg"])
+def test_cli_mcmc_als_match_reference(case, tmp_path):
+    """-method mcmc | als: #Iter lines, test_rmse_<dim>_mcmc, v_file.txt and -out
+    (pred_sum_all / num_iter for mcmc, the last predictions for als; clipped)."""
+    t, a = load_case(case)
+    m = t["meta"]
+    d = os.path.join(GOLDEN, case.split("/")[0])
+    extra = ["-init_stdev", str(m["init_stdev"]), "-out", "pred.txt", "-rlog", "log.tsv"]
+    if "meta" in m:
+        extra += ["-meta", os.path.join(d, m["meta"])]
+    if "regular" in m:
+        extra += ["-regular", ",".join(repr(r) for r in m["regular"])]
+    method = "mcmc" if "mcmc" in case else "als"
+    stdout = run_cli(tmp_path, os.path.join(d, "train.libfm"), os.path.join(d, "test.libfm"), m["dim"],
+                     m["iter"], m["seed"], extra, method=method)
+    iters = re.findall(r"#Iter=\s*(\d+)\tTrain=(\S+)\tTest=(\S+)", stdout)
+    assert len(iters) == m["iter"]
+    for (i, tr, te), ref in zip(iters, t["trace"]):
+        assert same6(tr, g6(ref["train"])) and same6(te, g6(ref["rmse_all"])), (i, tr, te, ref)
+    tag = m["dim"].replace(",", "")
+    rmse = open(tmp_path / ("test_rmse_%s_mcmc" % tag)).read().split()
+    assert [same6(r, g6(ref["rmse_all"])) for r, ref in zip(rmse, t["trace"])] == [True] * m["iter"]
+    assert "Final" not in stdout
+    k = int(m["dim"].split(",")[2])
+    vf = np.loadtxt(tmp_path / "v_file.txt", ndmin=2)
+    np.testing.assert_allclose(vf.ravel(), a["init_fm_v"], rtol=1e-5, atol=1e-7)
+    assert vf.shape[0] == k
+    pred = np.loadtxt(tmp_path / "pred.txt")
+    tg = np.array([float(l.split()[0]) for l in open(os.path.join(d, "test.libfm"))])
+    ytr = np.array([float(l.split()[0]) for l in open(os.path.join(d, "train.libfm"))])
+    assert np.all(pred >= ytr.min()) and np.all(pred <= ytr.max())
+    if method == "mcmc":   # pred_sum_all / num_iter: its RMSE is the last Test= value
+        assert abs(np.sqrt(np.mean((pred - tg) ** 2)) - t["trace"][-1]["rmse_all"]) < 1e-5
+    hdr = open(tmp_path / "log.tsv").readline().rstrip("\n").split("\t")
+    assert "rmse_mcmc_all" in hdr and "alpha" in hdr

@@ -149,24 +149,67 @@ def test_vb_trace_movielens_split_bit_exact(sa_split):
     np.testing.assert_array_equal(got[-1][-1]["mu_w"], a["final_mu_w"])
 
 
-@pytest.mark.parametrize("case", ["tiny/als", "tiny_dup/als", "synth_als"])
-def test_als_trace_bit_exact(case, synth_files):
+def regular_to_lambdas(reg, G, k):
+    """-regular for mcmc/als (libfm.cpp:367-411) -> (reg0, w_lambda[G], v_lambda[G*k])."""
+    reg = list(reg or [])
+    if len(reg) == 0:
+        r0 = rw = rv = 0.0
+    elif len(reg) == 1:
+        r0 = rw = rv = reg[0]
+    elif len(reg) == 3:
+        r0, rw, rv = reg
+    else:
+        assert len(reg) == 1 + 2 * G
+        wl = np.array(reg[1:1 + G])
+        vl = np.repeat(np.array(reg[1 + G:1 + 2 * G]), k)
+        return reg[0], wl, vl
+    return r0, np.full(G, rw), np.full(G * k, rv)
+
+
+MCMC_CASES = ["tiny/als", "tiny_dup/als", "synth_als", "tiny/mcmc", "tiny_dup/mcmc", "tiny/mcmc_meta",
+              "tiny/als_reg", "tiny_dup/als_reg", "tiny/als_meta_reg", "synth_mcmc", "sa_mcmc"]
+
+
+def run_mcmc_oracle(case, synth_files, sa_split=None):
     t, a = load_case(case)
     m = t["meta"]
     if case.startswith("synth"):
         tr, te = oc.Data(synth_files["train"]), oc.Data(synth_files["test"])
+    elif case.startswith("sa_"):
+        tr, te = oc.Data(sa_split["train"]), oc.Data(sa_split["test"])
     else:
         tr, te = _tiny(case.split("/")[0])
     k0, k1, k = [int(x) for x in m["dim"].split(",")]
-    als = oc.ALS(k0, k1, k, oc.num_all_attribute(tr, te))
+    D = oc.num_all_attribute(tr, te)
+    groups = None
+    if "meta" in m:
+        groups = np.loadtxt(os.path.join(GOLDEN, case.split("/")[0], m["meta"]), dtype=np.uint32)
+    method = "mcmc" if "mcmc" in case else "als"
+    G = 1 if groups is None else int(groups.max()) + 1
+    reg0, wl, vl = regular_to_lambdas(m.get("regular"), G, k)
+    als = oc.ALS(k0, k1, k, D, groups, method=method, reg0=reg0)
     als.init_params(m["seed"], m["init_stdev"])
+    als.set_lambda(wl, vl)
     als.attach(tr, te)
-    for it in range(m["iter"]):
-        rmse_all, rmse_this, train = als.iterate()
+    got = [als.iterate() for _ in range(m["iter"])]
+    return t, a, als, got
+
+
+@pytest.mark.parametrize("case", MCMC_CASES)
+def test_mcmc_als_trace_bit_exact(case, synth_files, sa_split):
+    """fm_learn_mcmc_simultaneous::_learn with draw_all, including the hyper-prior draws
+    and the rand() stream (glibc restatement), reproduces the reference bit for bit."""
+    t, a, als, got = run_mcmc_oracle(case, synth_files, sa_split)
+    for it, (rmse_all, rmse_this, train) in enumerate(got):
         ref = t["trace"][it]
         assert rmse_all == ref["rmse_all"], (it, rmse_all, ref["rmse_all"])
         assert train == ref["train"], (it, train, ref["train"])
     p = als.params()
-    np.testing.assert_array_equal(p["v"], a["final_fm_v"])
-    np.testing.assert_array_equal(p["w"], a["final_fm_w"])
+    if "final_fm_v" in a:
+        np.testing.assert_array_equal(p["v"], a["final_fm_v"])
+        np.testing.assert_array_equal(p["w"], a["final_fm_w"])
     assert p["w0"] == a["final_mcmc_scalars"][0]
+    assert p["alpha"] == a["final_mcmc_scalars"][1]
+    for key in ("w_mu", "w_lambda", "v_mu", "v_lambda"):
+        if "final_" + key in a:
+            np.testing.assert_array_equal(p[key], a["final_" + key])
