@@ -97,6 +97,8 @@ def main():
     ap.add_argument("--config", default="c4", choices=sorted(CONFIGS))
     ap.add_argument("--rows", type=int, default=0, help="override rows per GPU")
     ap.add_argument("--k", type=int, default=0, help="override factors")
+    ap.add_argument("--layout", default="auto", choices=["auto", "column", "level"],
+                    help="row-cache layout of the sweeps (include/vbfm.h VBFM_LAYOUT_*)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-rows", type=int, default=1_000_000)
     ap.add_argument("--cpu-factors", type=int, default=2)
@@ -124,7 +126,7 @@ def main():
     torch.cuda.set_device(local_rank)
 
     t0 = time.time()
-    fml = vbfm.FMLearnVB(1, 1, k, D, min_target=1.0, max_target=5.0, device=local_rank)
+    fml = vbfm.FMLearnVB(1, 1, k, D, min_target=1.0, max_target=5.0, device=local_rank, layout=args.layout)
     if world > 1:
         obj = [vbfm.FMLearnVB.comm_unique_id() if rank == 0 else None]
         dist.broadcast_object_list(obj, src=0)
@@ -134,7 +136,8 @@ def main():
     fml.synth(1, n_test, F, S, seed=500000 + rank, xmode=0)
     fml.init_caches()
     fml.set_profiling(True)
-    log("rank %d: setup %.1f s (N=%d F=%d S=%d k=%d)" % (rank, time.time() - t0, N, F, S, k))
+    layout = fml.layout()
+    log("rank %d: setup %.1f s (N=%d F=%d S=%d k=%d, %s layout)" % (rank, time.time() - t0, N, F, S, k, layout))
 
     for i in range(args.warmup):
         st = fml.iterate()
@@ -163,11 +166,12 @@ def main():
     nnz = N * F
     value = world * nnz * k * args.steps / elapsed
     levels = stats[-1].num_levels
-    # roofline of the dominant kernel (k_v_level_fused, one launch per factor and level). It
-    # does the whole factor sweep of its level (stats, posterior, correction and the q-cache
-    # of the next factor), so its algorithmic bytes are SURVEY §8d's per-factor model
-    # B = 128 B/nnz + 24 B/row + 32 B/feature, spread over the level launches of a factor:
-    # 128 = q-build 8 (CSC) + stats 32 (8 CSC + 24 e,q,tq) + correction 88 (8 CSC + 40 + 40).
+    # roofline of the dominant kernel (k_level_lord / k_v_level_fused, one launch per factor
+    # and level). It does the whole factor sweep of its level (stats, posterior, correction
+    # and the q-cache of the next factor), so its algorithmic bytes are SURVEY §8d's
+    # per-factor model B = 128 B/nnz + 24 B/row + 32 B/feature, spread over the level
+    # launches of a factor: 128 = q-build 8 (CSC) + stats 32 (8 CSC + 24 e,q,tq) +
+    # correction 88 (8 CSC + 40 + 40). The same model prices both layouts.
     n_launch = sum(s.n_vlevel_launches for s in stats)
     ms_launch = sum(s.ms_vlevel_kernels for s in stats)
     avg_ms = ms_launch / max(1, n_launch)
@@ -175,7 +179,8 @@ def main():
     achieved = bytes_per_launch / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else 0.0
     sweep_ms = sum(s.ms_v for s in stats) / len(stats)
     traffic = None
-    tf = os.path.join(ROOT, "profiles", "traffic_%s.json" % args.config)
+    kernel = "k_level_lord" if layout == "level" else "k_v_level_fused"
+    tf = os.path.join(ROOT, "profiles", "traffic_%s_%s.json" % (args.config, layout))
     if os.path.exists(tf):
         with open(tf) as fh:
             traffic = json.load(fh).get("bytes_per_launch")
@@ -188,10 +193,10 @@ def main():
         "config": {"workload": cfg["desc"], "rows_per_gpu": N, "fields": F, "ids_per_field": S,
                    "features": F * S, "k": k, "nnz_per_gpu": nnz, "test_rows_per_gpu": n_test,
                    "levels": levels, "step": "one full VB iteration (update_all + test RMSE)",
-                   "parallelism": "row-sharded dp%d" % world},
+                   "parallelism": "row-sharded dp%d" % world, "row_layout": layout},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                     "kernel": "k_v_level_fused", "avg_launch_ms": avg_ms,
+                     "kernel": kernel, "avg_launch_ms": avg_ms,
                      "launches": n_launch, "bytes_per_launch": bytes_per_launch},
         "factor_sweep_ms_per_step": sweep_ms,
         "factor_sweep_nnz_k_per_s": world * nnz * k / (sweep_ms * 1e-3),

@@ -144,6 +144,23 @@ int vbfm_free_energy(vbfm_ctx *ctx, double *F);   /* :646-681 (value only, no fi
 int vbfm_get_rows(vbfm_ctx *ctx, double *e, double *t, double *q, double *tq, double *tz);
 int vbfm_get_test_e(vbfm_ctx *ctx, double *e /*[test rows]*/);
 
+/* Layout of the row caches in HBM during the sweeps (no reference counterpart: the
+ * reference keeps cache[] / cache_t[] in row order, fm_learn_vb.h:17-21,746-786).
+ *   VBFM_LAYOUT_AUTO   (default) level-ordered when every dependency level holds each train
+ *                      row exactly once (field-structured one-hot data), else column-gather;
+ *   VBFM_LAYOUT_COLUMN row order, columns gather their rows;
+ *   VBFM_LAYOUT_LEVEL  records kept in the current level's column order and streamed
+ *                      (vbfm_set_layout fails at the first sweep when the data does not
+ *                      allow it). Results are identical up to the summation order of the
+ *                      data-set sums (w0, alpha, free energy).
+ * Set before vbfm_set_train; VBFM_LAYOUT=auto|column|level in the environment overrides.
+ * vbfm_get_layout reports the layout in use (COLUMN or LEVEL) once the train set is known. */
+#define VBFM_LAYOUT_AUTO 0
+#define VBFM_LAYOUT_COLUMN 1
+#define VBFM_LAYOUT_LEVEL 2
+int vbfm_set_layout(vbfm_ctx *ctx, int32_t layout);
+int vbfm_get_layout(vbfm_ctx *ctx, int32_t *layout);
+
 /* per-launch event timing of the sweep kernels inside vbfm_iterate (off by default) */
 int vbfm_set_profiling(vbfm_ctx *ctx, int32_t on);
 

@@ -117,6 +117,105 @@ void upload(vbfm_ctx *c, DevData &d, const vbfm_csc *in, uint32_t nf_pad)
 	sync(c);
 }
 
+uint32_t nlevels(vbfm_ctx *c);
+
+// ---- level-ordered row store (vbfm_lorder.hip) ------------------------------------------
+void lord_release(vbfm_ctx *c, bool keep_rows)
+{
+	if (keep_rows && c->rows_lorder) {
+		HIPCHK(vbk::rows_scatter(c->rows_alt, c->rows, c->lrow0, c->tr.n, c->s));
+		std::swap(c->rows, c->rows_alt);
+		c->rows_lorder = false;
+	}
+	sync(c);
+	dfree(c->rows_alt); dfree(c->lcp); dfree(c->lx); dfree(c->lnext); dfree(c->lrow0); dfree(c->lpos0);
+	c->lord = false;
+	c->rows_lorder = false;
+}
+
+static int layout_request(const vbfm_ctx *c)
+{
+	const char *env = getenv("VBFM_LAYOUT");
+	if (env && !strcmp(env, "column")) return VBFM_LAYOUT_COLUMN;
+	if (env && !strcmp(env, "level")) return VBFM_LAYOUT_LEVEL;
+	if (env && !strcmp(env, "auto")) return VBFM_LAYOUT_AUTO;
+	return c->layout_req;
+}
+
+// Level-ordered store of the train set when every level holds each row exactly once (no
+// repeated feature in a row): per level l, positions [l*n, (l+1)*n) list the level's
+// columns in ascending feature order, rows ascending within a column.
+void build_lorder(vbfm_ctx *c, const std::vector<uint64_t> &cp, const std::vector<uint32_t> &feats)
+{
+	lord_release(c, true);
+	const int req = layout_request(c);
+	if (c->mc || req == VBFM_LAYOUT_COLUMN) return;
+	DevData &d = c->tr;
+	const uint32_t L = nlevels(c), n = d.n, nf = d.nf;
+	std::string why;
+	std::vector<uint8_t> dup(nf, 0);
+	if (nf) HIPCHK(hipMemcpy(dup.data(), c->dup, nf, hipMemcpyDeviceToHost));
+	std::vector<uint64_t> lcp((size_t)nf + 1, 0);
+	for (uint32_t i = 0; i < nf; i++) lcp[i + 1] = lcp[i] + (cp[feats[i] + 1] - cp[feats[i]]);
+	if (n == 0 || L == 0) why = "no train rows";
+	for (uint32_t l = 0; l < L && why.empty(); l++) {
+		if (lcp[c->level_ptr[l + 1]] - lcp[c->level_ptr[l]] != n)
+			why = "dependency level " + std::to_string(l + 1) + " does not hold every train row exactly once";
+		for (uint32_t i = c->level_ptr[l]; i < c->level_ptr[l + 1] && why.empty(); i++)
+			if (dup[feats[i]]) why = "a row lists feature " + std::to_string(feats[i]) + " twice";
+	}
+	if (!why.empty()) {
+		if (req == VBFM_LAYOUT_LEVEL) throw std::string("level-ordered row layout not possible: ") + why;
+		return;
+	}
+	c->lcp = dalloc<uint64_t>(lcp.size());
+	HIPCHK(hipMemcpyAsync(c->lcp, lcp.data(), lcp.size() * 8, hipMemcpyHostToDevice, c->s));
+	c->lx = dalloc<float>(d.nnz);
+	c->lnext = dalloc<uint32_t>(d.nnz);
+	c->lrow0 = dalloc<uint32_t>(n);
+	c->lpos0 = dalloc<uint32_t>(n);
+	c->rows_alt = dalloc<RowRec>(n);
+	uint32_t *tmp = dalloc<uint32_t>(n);
+	auto lev = [&](uint32_t l, uint32_t *&f, uint32_t &nfl, const uint64_t *&lp) {
+		f = c->level_feats + c->level_ptr[l];
+		nfl = c->level_ptr[l + 1] - c->level_ptr[l];
+		lp = c->lcp + c->level_ptr[l];
+	};
+	uint32_t *f, nfl;
+	const uint64_t *lp;
+	lev(0, f, nfl, lp);
+	HIPCHK(vbk::lord_pos(f, nfl, lp, 0, d.col_ptr, d.csc, c->lpos0, c->s));
+	// backwards over the levels: level l needs the position map of level l+1 (level 0 for
+	// the last level), held in tmp (or lpos0)
+	for (uint32_t l = L; l-- > 0;) {
+		lev(l, f, nfl, lp);
+		const uint32_t *pos_next = (l + 1 == L) ? c->lpos0 : tmp;
+		HIPCHK(vbk::lord_fill(f, nfl, lp, (uint64_t)l * n, d.col_ptr, d.csc, pos_next, c->lx, c->lnext,
+		                      l == 0 ? c->lrow0 : nullptr, c->s));
+		if (l > 0) HIPCHK(vbk::lord_pos(f, nfl, lp, (uint64_t)l * n, d.col_ptr, d.csc, tmp, c->s));
+	}
+	sync(c);
+	dfree(tmp);
+	c->lord = true;
+}
+
+// c->rows in level-0 order (before a sweep) / in row order (row-indexed kernels, readback)
+void rows_level_order(vbfm_ctx *c)
+{
+	if (!c->lord || c->rows_lorder) return;
+	HIPCHK(vbk::rows_gather(c->rows_alt, c->rows, c->lrow0, c->tr.n, c->s));
+	std::swap(c->rows, c->rows_alt);
+	c->rows_lorder = true;
+}
+
+void rows_row_order(vbfm_ctx *c)
+{
+	if (!c->rows_lorder) return;
+	HIPCHK(vbk::rows_scatter(c->rows_alt, c->rows, c->lrow0, c->tr.n, c->s));
+	std::swap(c->rows, c->rows_alt);
+	c->rows_lorder = false;
+}
+
 // Dependency levels of the train features (see vbfm_kernels.hip header). With several
 // row shards every round's levels are max-reduced over the shards, so all ranks share one
 // schedule: the one the un-sharded data set defines.
@@ -176,6 +275,7 @@ void build_schedule(vbfm_ctx *c)
 		c->stats_cap = maxlev;
 	}
 	c->sched_ready = true;
+	build_lorder(c, cp, feats);
 }
 
 // segments of the hyper / free-energy sums: (w or factor f) x group, chunked by 64K attrs
@@ -227,7 +327,7 @@ void require_train(vbfm_ctx *c)
 
 LevelArgs level_args(vbfm_ctx *c, uint32_t l, bool is_w, int f)
 {
-	LevelArgs a;
+	LevelArgs a = {};
 	a.col_ptr = c->tr.col_ptr;
 	a.csc = c->tr.csc;
 	a.feats = c->level_feats + c->level_ptr[l];
@@ -283,6 +383,27 @@ void sweep_level(vbfm_ctx *c, uint32_t l, bool is_w, int f)
 	LevelArgs a = level_args(c, l, is_w, f);
 	if (a.nfeat == 0) return;
 	const size_t p = prof_begin(c, is_w ? 1 : 0);
+	if (c->lord) {
+		// level-ordered store: stream this level's records, move them to the next level's order
+		a.lcp = c->lcp + c->level_ptr[l];
+		a.lx = c->lx;
+		a.lnext = c->lnext;
+		a.lbase = (uint64_t)l * c->tr.n;
+		a.src = c->rows;
+		a.dst = c->rows_alt;
+		a.first_level = l == 0;
+		if (!c->comm && !c->force_split) {
+			HIPCHK(vbk::lord_level(a, is_w, c->s));
+		} else {
+			HIPCHK(vbk::lord_level_stats(a, is_w, c->s));
+			if (c->comm)
+				NCCLCHK(ncclAllReduce(c->stats, c->stats, 2 * (size_t)a.nfeat, ncclDouble, ncclSum, c->comm, c->s));
+			HIPCHK(vbk::lord_level_move(a, is_w, c->s));
+		}
+		std::swap(c->rows, c->rows_alt);
+		prof_end(c, p);
+		return;
+	}
 	if (!c->comm && !c->force_split) {
 		HIPCHK(is_w ? vbk::w_level_fused(a, c->s) : vbk::v_level_fused(a, c->s));
 		prof_end(c, p);
@@ -316,6 +437,7 @@ void step_w0(vbfm_ctx *c)
 // the w sweep; with factors it also leaves the q-cache of factor 0 in slot 0
 void step_w(vbfm_ctx *c)
 {
+	rows_level_order(c);
 	for (uint32_t l = 0; l < nlevels(c); l++) sweep_level(c, l, true, 0);
 	if (c->k > 0) c->q_ready[0] = 0;
 }
@@ -327,7 +449,9 @@ void step_qcache(vbfm_ctx *c, int f)
 	const int slot = f & 1;
 	if (c->q_ready[slot] != f) {
 		const size_t p = prof_begin(c, 2);
-		HIPCHK(vbk::qcache(c->tr.row_ptr, c->tr.csr, c->ms_v + f, (uint32_t)c->k, c->rows, c->tr.n, slot, c->s));
+		rows_level_order(c);
+		HIPCHK(vbk::qcache(c->tr.row_ptr, c->tr.csr, c->ms_v + f, (uint32_t)c->k, c->rows, c->tr.n, slot,
+		                   c->rows_lorder ? c->lpos0 : nullptr, c->s));
 		prof_end(c, p);
 		c->q_ready[slot] = f;
 	}
@@ -337,6 +461,7 @@ void step_qcache(vbfm_ctx *c, int f)
 // the v sweep of factor f (which also accumulates the q-cache of factor f+1)
 void step_v(vbfm_ctx *c, int f)
 {
+	rows_level_order(c);
 	for (uint32_t l = 0; l < nlevels(c); l++) sweep_level(c, l, false, f);
 	c->qslot = f & 1;
 	c->q_ready[f & 1] = -1;   // corrected in place, no longer the from-scratch sum add_main_q gives
@@ -498,6 +623,7 @@ void vbfm_destroy(vbfm_ctx *c)
 	dfree(c->ms_v); dfree(c->ms_w); dfree(c->hyp_w_d); dfree(c->hyp_v_d); dfree(c->group_d);
 	dfree(c->level_feats); dfree(c->dup); dfree(c->red_d); dfree(c->perm_d); dfree(c->chunks_d);
 	dfree(c->chunk_out_d); dfree(c->counters); dfree(c->stats);
+	dfree(c->rows_alt); dfree(c->lcp); dfree(c->lx); dfree(c->lnext); dfree(c->lrow0); dfree(c->lpos0);
 	mc_free(c);
 	if (c->comm) ncclCommDestroy(c->comm);
 	for (hipEvent_t e : c->pev) (void)hipEventDestroy(e);
@@ -509,6 +635,7 @@ void vbfm_destroy(vbfm_ctx *c)
 
 static void alloc_rows(vbfm_ctx *c)
 {
+	lord_release(c, false);   // a new train set: the old records are discarded
 	dfree(c->rows);
 	dfree(c->scratch_n);
 	c->rows = dalloc<RowRec>(c->tr.n);
@@ -744,6 +871,7 @@ int vbfm_init_caches(vbfm_ctx *c)
 		if (c->mc) throw std::string("an MCMC / ALS context: use the vbfm_mcmc_* entry points");
 		require_train(c);
 		// fm_learn_vb_simultaneous.h:37-44: yhat of train and test, T of train, e = y - yhat
+		rows_row_order(c);
 		const int bl = blocked_predict(c, c->tr);
 		HIPCHK(vbk::predict_e(c->tr.row_ptr, c->tr.csr, c->ms_v, c->ms_w, c->k, c->k1, c->k0, c->mu0, c->scratch_n,
 		                      c->tr.n, bl, c->s));
@@ -811,6 +939,8 @@ int vbfm_get_rows(vbfm_ctx *c, double *e, double *t, double *q, double *tq, doub
 {
 	if (!c) return fail(nullptr, "null context");
 	return guarded(c, [&] {
+		rows_row_order(c);
+		sync(c);   // the readback below runs on the null stream, which does not wait for c->s
 		std::vector<RowRec> h(c->tr.n);
 		if (c->tr.n) HIPCHK(hipMemcpy(h.data(), c->rows, (size_t)c->tr.n * sizeof(RowRec), hipMemcpyDeviceToHost));
 		const bool s1 = c->qslot == 1;
@@ -915,6 +1045,24 @@ int vbfm_iterate(vbfm_ctx *c, vbfm_iter_stats *o)
 		}
 		st.ms_qcache = st.ms_qcache_kernels;
 		if (o) *o = st;
+	});
+}
+
+int vbfm_set_layout(vbfm_ctx *c, int32_t layout)
+{
+	if (!c) return fail(nullptr, "null context");
+	if (layout < VBFM_LAYOUT_AUTO || layout > VBFM_LAYOUT_LEVEL) return fail(c, "unknown row layout");
+	if (c->rows) return fail(c, "vbfm_set_layout must precede vbfm_set_train");
+	c->layout_req = layout;
+	return 0;
+}
+
+int vbfm_get_layout(vbfm_ctx *c, int32_t *layout)
+{
+	if (!c || !layout) return fail(c, "null argument");
+	return guarded(c, [&] {
+		require_train(c);
+		*layout = c->lord ? VBFM_LAYOUT_LEVEL : VBFM_LAYOUT_COLUMN;
 	});
 }
 

@@ -112,6 +112,16 @@ struct vbfm_ctx {
 	size_t pev_used = 0;
 	struct Span { size_t a; int kind; };   // kind 0 = v level, 1 = w level, 2 = qcache
 	std::vector<Span> spans;
+	// level-ordered row store (vbfm_lorder.hip)
+	int layout_req = VBFM_LAYOUT_AUTO;
+	bool lord = false;             // built for the current train set and in use
+	bool rows_lorder = false;      // rows currently hold level-0 order (else row order)
+	RowRec *rows_alt = nullptr;    // second record buffer (each level moves rows -> rows_alt)
+	uint64_t *lcp = nullptr;       // [nf+1] global position of each level feature's run
+	float *lx = nullptr;           // [nnz] x per level-ordered entry
+	uint32_t *lnext = nullptr;     // [nnz] position of the entry's row in the next level
+	uint32_t *lrow0 = nullptr;     // [n] row at each level-0 position
+	uint32_t *lpos0 = nullptr;     // [n] level-0 position of each row
 	McState *mc = nullptr;         // set by vbfm_mcmc_init: the context runs the MCMC / ALS learner
 };
 
@@ -147,5 +157,6 @@ void prof_end(vbfm_ctx *c, size_t a);
 int blocked_predict(const vbfm_ctx *c, const DevData &d);
 float ev_ms(vbfm_ctx *c, int a, int b);
 void mc_free(vbfm_ctx *c);   // vbfm_mcmc_capi.hip
+void lord_release(vbfm_ctx *c, bool keep_rows);   // level-ordered store freed (rows back to row order)
 
 }  // namespace vbi

@@ -61,6 +61,14 @@ struct LevelArgs {
 	uint32_t ms_stride_next;
 	int slot;                  // q-cache slot of the factor being swept (v) / of factor 0 (w)
 	uint32_t avg_len;          // mean column length of the level (launch shape)
+	// level-ordered row store (vbfm_lorder.hip); unused by the column-gather kernels
+	const uint64_t *lcp;       // global position of each level feature's run, indexed like feats [nfeat+1]
+	const float *lx;           // x of every level-ordered entry (global position)
+	const uint32_t *lnext;     // position of the entry's row in the next level's order
+	uint64_t lbase;            // global position of the level's first entry (= level * rows)
+	const RowRec *src;         // records in this level's order
+	RowRec *dst;               // records in the next level's order
+	int first_level;           // level 0: every row's smallest feature (q-cache restart)
 };
 
 // per-level launch description for the MCMC / ALS draws (vbfm_mcmc.hip); parameters are
@@ -100,8 +108,21 @@ hipError_t v_level_stats(const LevelArgs &a, hipStream_t s);
 hipError_t v_level_correct(const LevelArgs &a, hipStream_t s);
 hipError_t w_level_stats(const LevelArgs &a, hipStream_t s);
 hipError_t w_level_correct(const LevelArgs &a, hipStream_t s);
+// pos: nullptr, or the record index of each row (level-ordered store: level-0 position)
 hipError_t qcache(const uint64_t *row_ptr, const uint2 *csr, const double2 *ms_f, uint32_t stride, RowRec *rows,
-                  uint32_t n, int slot, hipStream_t s);
+                  uint32_t n, int slot, const uint32_t *pos, hipStream_t s);
+// level-ordered row store (vbfm_lorder.hip): fused level, or split stats -> (all-reduce) -> move
+hipError_t lord_level(const LevelArgs &a, int is_w, hipStream_t s);
+hipError_t lord_level_stats(const LevelArgs &a, int is_w, hipStream_t s);
+hipError_t lord_level_move(const LevelArgs &a, int is_w, hipStream_t s);
+hipError_t lord_pos(const uint32_t *feats, uint32_t nfeat, const uint64_t *lcp, uint64_t lbase, const uint64_t *col_ptr,
+                    const uint2 *csc, uint32_t *pos, hipStream_t s);
+hipError_t lord_fill(const uint32_t *feats, uint32_t nfeat, const uint64_t *lcp, uint64_t lbase, const uint64_t *col_ptr,
+                     const uint2 *csc, const uint32_t *pos_next, float *lx, uint32_t *lnext, uint32_t *row0,
+                     hipStream_t s);
+// dst[p] = src[idx[p]] / dst[idx[p]] = src[p]
+hipError_t rows_gather(RowRec *dst, const RowRec *src, const uint32_t *idx, uint32_t n, hipStream_t s);
+hipError_t rows_scatter(RowRec *dst, const RowRec *src, const uint32_t *idx, uint32_t n, hipStream_t s);
 hipError_t mark_first(const uint64_t *row_ptr, const uint2 *csr, const uint64_t *col_ptr, uint2 *csc,
                       uint32_t n, hipStream_t s);
 // blocked = 0: the reference's summation order (bit-exact); 1: factors in blocks of 8

@@ -1,0 +1,330 @@
+// vbfm_lorder.hip -- the level-ordered row store: sweep kernels that stream the row caches
+// instead of gathering them.
+//
+// The column-gather kernels (vbfm_kernels.hip) keep the row records in row order; a level
+// reads and writes back one 64-B record at a random address per entry, twice per row per
+// level (read, later write), and run at the random read-modify-write ceiling of HBM
+// (~2e10 rows/s). When every dependency level holds each row exactly once
+// (field-structured one-hot data: one level per field, every row one entry per field) the
+// records can instead be kept physically in the order of the current level's CSC entries:
+// position p of level l is the p-th entry of the level's columns taken in ascending
+// feature order (ascending rows within a column), so a column's records are one contiguous
+// run. A level then
+//   * streams its records (coalesced, one pass),
+//   * reduces each column's statistics, computes the posterior and applies the correction
+//     exactly as update_v / update_w do (fm_learn_vb.h:577-644, :527-574), and
+//   * writes every record once to its row's position in the NEXT level's order
+//     (lnext[p]; the last level maps back to level 0, where every sweep starts):
+// one streaming read + one random full-line write per row per level instead of a random
+// read + a random write of the same line. The i-th entry of a column is the same (row, x)
+// in both layouts and is reduced in the same tree order, so both layouts compute
+// bit-identical column statistics, posteriors and corrections.
+//
+// Build (once per train set): level-ordered segment starts lcp (host), then per level the
+// row -> position map (k_lord_pos) and the entry payload x / lnext (k_lord_fill), walking
+// the levels backwards so that one row-sized scratch array holds the next level's map.
+#include "vbfm_math.h"
+
+namespace {
+
+template <bool IS_W, int P>
+DEVI void lo_stat(Rec &v, float x, double mo, double so, double &s1, double &s2)
+{
+	if constexpr (IS_W) w_stat(x, E(v), mo, s1, s2);
+	else v_stat(x, E(v), Q<P>(v), TQ<P>(v), mo, so, s1, s2);
+}
+
+template <bool IS_W>
+DEVI bool lo_post(double s1, double s2, double hyp, double alpha, double mo, double so, double &mu, double &sig,
+                  uint32_t *counters, bool leader)
+{
+	if constexpr (IS_W) return w_post(s1, s2, hyp, alpha, mo, so, mu, sig, counters, leader);
+	else return v_post(s1, s2, hyp, alpha, mo, so, mu, sig, counters, leader);
+}
+
+template <bool IS_W, int P, bool NEXT>
+DEVI void lo_apply(Rec &v, float x, bool first, bool go, double mo, double so, double mu, double sig, double2 nx)
+{
+	if constexpr (IS_W) w_apply<NEXT>(v, x, first, go, mo, so, mu, sig, nx);
+	else v_apply<P, NEXT>(v, x, first, go, mo, so, mu, sig, nx);
+}
+
+// ---- LDS staging -------------------------------------------------------------------------
+// A run of records moves between HBM and LDS four lanes per 64-B record (one 16-B piece
+// each), so that every wave instruction reads or writes whole records: the scattered writes
+// to the next level's order are then full-line writes. (One lane per record with four 16-B
+// stores runs ~35 % slower: tools/probe_lord.hip.) In LDS piece c of record i sits at
+// i*4 + (c ^ ((i >> 2) & 3)): the per-record ds_read_b128 / ds_write_b128 of 16 consecutive
+// lanes then touch 16 distinct 16-B bank groups.
+DEVI uint32_t lslot(uint32_t i, uint32_t c) { return i * 4 + (c ^ ((i >> 2) & 3)); }
+
+template <int BLOCK>
+DEVI void stage_in(double2 *recs, const double2 *src, uint32_t m)
+{
+	for (uint32_t t = threadIdx.x; t < m * 4; t += BLOCK) recs[lslot(t >> 2, t & 3)] = src[t];
+}
+
+DEVI void lds_get(const double2 *recs, uint32_t i, Rec &v)
+{
+#pragma unroll
+	for (uint32_t c = 0; c < 4; ++c) v[c] = recs[lslot(i, c)];
+}
+
+DEVI void lds_put(double2 *recs, uint32_t i, const Rec &v)
+{
+#pragma unroll
+	for (uint32_t c = 0; c < 4; ++c) recs[lslot(i, c)] = v[c];
+}
+
+// statistics of a run of n records in chunks of CAP (the last chunk stays in LDS)
+template <int BLOCK, uint32_t CAP, bool IS_W, int P>
+DEVI void lord_stats(double2 *recs, const RowRec *src, const float *lx, uint32_t n, double mo, double so, double &s1,
+                     double &s2)
+{
+	const double2 *s = reinterpret_cast<const double2 *>(src);
+	for (uint32_t base = 0; base < n; base += CAP) {
+		const uint32_t m = min(CAP, n - base);
+		if (base) __syncthreads();
+		stage_in<BLOCK>(recs, s + (size_t)base * 4, m);
+		__syncthreads();
+		for (uint32_t i = threadIdx.x; i < m; i += BLOCK) {
+			Rec v;
+			lds_get(recs, i, v);
+			lo_stat<IS_W, P>(v, lx[base + i], mo, so, s1, s2);
+		}
+	}
+}
+
+// correction of every record of the run and its move to the next level's order. resident:
+// the run (n <= CAP) is still in LDS from lord_stats. Every record is written even when the
+// guards skip the correction: the write IS the move.
+template <int BLOCK, uint32_t CAP, bool IS_W, int P, bool NEXT>
+DEVI void lord_move(double2 *recs, uint32_t *dsts, const RowRec *src, const float *lx, const uint32_t *nxt, uint32_t n,
+                    bool resident, RowRec *dst, bool first, bool go, double mo, double so, double mu, double sig,
+                    double2 nx)
+{
+	const double2 *s = reinterpret_cast<const double2 *>(src);
+	double2 *d = reinterpret_cast<double2 *>(dst);
+	for (uint32_t base = 0; base < n; base += CAP) {
+		const uint32_t m = min(CAP, n - base);
+		if (!resident) {
+			__syncthreads();
+			stage_in<BLOCK>(recs, s + (size_t)base * 4, m);
+			__syncthreads();
+		}
+		for (uint32_t i = threadIdx.x; i < m; i += BLOCK) {
+			Rec v;
+			lds_get(recs, i, v);
+			lo_apply<IS_W, P, NEXT>(v, lx[base + i], first, go, mo, so, mu, sig, nx);
+			lds_put(recs, i, v);
+			dsts[i] = nxt[base + i];
+		}
+		__syncthreads();
+		for (uint32_t t = threadIdx.x; t < m * 4; t += BLOCK) {
+			const uint32_t i = t >> 2, c = t & 3;
+			d[(size_t)dsts[i] * 4 + c] = recs[lslot(i, c)];
+		}
+	}
+}
+
+// One workgroup per column of the level: stream the column's run of records into LDS,
+// reduce its statistics (update_v :587-596 / update_w :534-539), posterior + guards, then
+// correct and move every record. Runs longer than CAP = BLOCK*R records are streamed twice
+// (contiguous, L2-warm).
+template <int BLOCK, int R, bool IS_W, int P, bool NEXT>
+__global__ __launch_bounds__(BLOCK) void k_level_lord(LevelArgs a)
+{
+	constexpr uint32_t CAP = BLOCK * R;
+	__shared__ double2 recs[CAP * 4];
+	__shared__ uint32_t dsts[CAP];
+	__shared__ double lds[2 * (BLOCK / 64)];
+	const uint32_t j = a.feats[blockIdx.x];
+	const uint64_t sb = a.lcp[blockIdx.x];
+	const uint32_t n = (uint32_t)(a.lcp[blockIdx.x + 1] - sb);
+	const RowRec *src = a.src + (sb - a.lbase);
+	const float *lx = a.lx + sb;
+	const double2 msj = a.ms[(size_t)j * a.ms_stride];
+	const double mo = msj.x, so = msj.y;
+	double2 nx = make_double2(0.0, 0.0);
+	if constexpr (NEXT) nx = a.ms_next[(size_t)j * a.ms_stride_next];
+
+	double s1 = 0.0, s2 = 0.0;
+	lord_stats<BLOCK, CAP, IS_W, P>(recs, src, lx, n, mo, so, s1, s2);
+	block_sum2<BLOCK>(s1, s2, lds);
+
+	double mu, sig;
+	const double hyp = a.hyp[(size_t)a.attr_group[j] * a.hyp_stride];
+	const bool go = lo_post<IS_W>(s1, s2, hyp, a.alpha, mo, so, mu, sig, a.counters, threadIdx.x == 0);
+	if (threadIdx.x == 0) a.ms[(size_t)j * a.ms_stride] = make_double2(mu, sig);
+	lord_move<BLOCK, CAP, IS_W, P, NEXT>(recs, dsts, src, lx, a.lnext + sb, n, n <= CAP, a.dst, a.first_level != 0,
+	                                      go, mo, so, mu, sig, nx);
+}
+
+// split form (row-sharded multi-GPU): statistics of the local rows -> all-reduce -> move
+template <int BLOCK, bool IS_W, int P>
+__global__ __launch_bounds__(BLOCK) void k_level_lord_stats(LevelArgs a)
+{
+	constexpr uint32_t CAP = BLOCK * 2;
+	__shared__ double2 recs[CAP * 4];
+	__shared__ double lds[2 * (BLOCK / 64)];
+	const uint32_t j = a.feats[blockIdx.x];
+	const uint64_t sb = a.lcp[blockIdx.x];
+	const uint32_t n = (uint32_t)(a.lcp[blockIdx.x + 1] - sb);
+	const double2 msj = a.ms[(size_t)j * a.ms_stride];
+	double s1 = 0.0, s2 = 0.0;
+	lord_stats<BLOCK, CAP, IS_W, P>(recs, a.src + (sb - a.lbase), a.lx + sb, n, msj.x, msj.y, s1, s2);
+	block_sum2<BLOCK>(s1, s2, lds);
+	if (threadIdx.x == 0) a.stats[blockIdx.x] = make_double2(s1, s2);
+}
+
+template <int BLOCK, bool IS_W, int P, bool NEXT>
+__global__ __launch_bounds__(BLOCK) void k_level_lord_move(LevelArgs a)
+{
+	constexpr uint32_t CAP = BLOCK * 2;
+	__shared__ double2 recs[CAP * 4];
+	__shared__ uint32_t dsts[CAP];
+	const uint32_t j = a.feats[blockIdx.x];
+	const uint64_t sb = a.lcp[blockIdx.x];
+	const uint32_t n = (uint32_t)(a.lcp[blockIdx.x + 1] - sb);
+	const double2 msj = a.ms[(size_t)j * a.ms_stride];
+	const double2 st = a.stats[blockIdx.x];
+	double2 nx = make_double2(0.0, 0.0);
+	if constexpr (NEXT) nx = a.ms_next[(size_t)j * a.ms_stride_next];
+	double mu, sig;
+	const double hyp = a.hyp[(size_t)a.attr_group[j] * a.hyp_stride];
+	const bool go = lo_post<IS_W>(st.x, st.y, hyp, a.alpha, msj.x, msj.y, mu, sig, a.counters, threadIdx.x == 0);
+	if (threadIdx.x == 0) a.ms[(size_t)j * a.ms_stride] = make_double2(mu, sig);
+	lord_move<BLOCK, CAP, IS_W, P, NEXT>(recs, dsts, a.src + (sb - a.lbase), a.lx + sb, a.lnext + sb, n, false, a.dst,
+	                                      a.first_level != 0, go, msj.x, msj.y, mu, sig, nx);
+}
+
+// ---- build -------------------------------------------------------------------------------
+// pos[row] = level-relative position of the row's entry in this level
+__global__ __launch_bounds__(256) void k_lord_pos(const uint32_t *feats, const uint64_t *lcp, uint64_t lbase,
+                                                  const uint64_t *col_ptr, const uint2 *csc, uint32_t *pos)
+{
+	const uint32_t j = feats[blockIdx.x];
+	const uint64_t cb = col_ptr[j];
+	const uint32_t n = (uint32_t)(col_ptr[j + 1] - cb);
+	const uint32_t p0 = (uint32_t)(lcp[blockIdx.x] - lbase);
+	for (uint32_t i = threadIdx.x; i < n; i += 256) pos[csc[cb + i].x & ROW_MASK] = p0 + i;
+}
+
+// payload of the level's entries: x, the row's position in the next level, and (level 0)
+// the row id of every position
+__global__ __launch_bounds__(256) void k_lord_fill(const uint32_t *feats, const uint64_t *lcp, uint64_t lbase,
+                                                   const uint64_t *col_ptr, const uint2 *csc, const uint32_t *pos_next,
+                                                   float *lx, uint32_t *lnext, uint32_t *row0)
+{
+	const uint32_t j = feats[blockIdx.x];
+	const uint64_t cb = col_ptr[j];
+	const uint32_t n = (uint32_t)(col_ptr[j + 1] - cb);
+	const uint64_t g0 = lcp[blockIdx.x];
+	for (uint32_t i = threadIdx.x; i < n; i += 256) {
+		const uint2 ent = csc[cb + i];
+		const uint32_t r = ent.x & ROW_MASK;
+		lx[g0 + i] = ent_x(ent);
+		lnext[g0 + i] = pos_next[r];
+		if (row0) row0[g0 + i - lbase] = r;
+	}
+}
+
+// record permutations between row order and level-0 order; 4 lanes per 64-B record
+__global__ __launch_bounds__(256) void k_rows_gather(RowRec *__restrict__ dst, const RowRec *__restrict__ src,
+                                                     const uint32_t *__restrict__ idx, uint32_t n)
+{
+	const uint64_t t = (uint64_t)blockIdx.x * 256u + threadIdx.x;
+	const uint32_t p = (uint32_t)(t >> 2), c = (uint32_t)(t & 3);
+	if (p >= n) return;
+	reinterpret_cast<double2 *>(dst + p)[c] = reinterpret_cast<const double2 *>(src + idx[p])[c];
+}
+
+__global__ __launch_bounds__(256) void k_rows_scatter(RowRec *__restrict__ dst, const RowRec *__restrict__ src,
+                                                      const uint32_t *__restrict__ idx, uint32_t n)
+{
+	const uint64_t t = (uint64_t)blockIdx.x * 256u + threadIdx.x;
+	const uint32_t p = (uint32_t)(t >> 2), c = (uint32_t)(t & 3);
+	if (p >= n) return;
+	reinterpret_cast<double2 *>(dst + idx[p])[c] = reinterpret_cast<const double2 *>(src + p)[c];
+}
+
+template <bool IS_W, int P, bool NEXT>
+void launch_lord(const LevelArgs &a, hipStream_t s)
+{
+	if (a.avg_len <= 96) k_level_lord<64, 2, IS_W, P, NEXT><<<a.nfeat, 64, 0, s>>>(a);
+	else if (a.avg_len <= 320) k_level_lord<256, 1, IS_W, P, NEXT><<<a.nfeat, 256, 0, s>>>(a);
+	else if (a.avg_len <= 640) k_level_lord<256, 2, IS_W, P, NEXT><<<a.nfeat, 256, 0, s>>>(a);
+	else k_level_lord<512, 2, IS_W, P, NEXT><<<a.nfeat, 512, 0, s>>>(a);
+}
+
+template <bool IS_W, int P>
+void launch_lord_move(const LevelArgs &a, hipStream_t s)
+{
+	if (a.ms_next) k_level_lord_move<256, IS_W, P, true><<<a.nfeat, 256, 0, s>>>(a);
+	else k_level_lord_move<256, IS_W, P, false><<<a.nfeat, 256, 0, s>>>(a);
+}
+
+}  // namespace
+
+namespace vbk {
+
+hipError_t lord_level(const LevelArgs &a, int is_w, hipStream_t s)
+{
+	if (a.nfeat == 0) return hipSuccess;
+	const bool nx = a.ms_next != nullptr;
+	if (is_w) nx ? launch_lord<true, 0, true>(a, s) : launch_lord<true, 0, false>(a, s);
+	else if (a.slot == 0) nx ? launch_lord<false, 0, true>(a, s) : launch_lord<false, 0, false>(a, s);
+	else nx ? launch_lord<false, 1, true>(a, s) : launch_lord<false, 1, false>(a, s);
+	return hipGetLastError();
+}
+
+hipError_t lord_level_stats(const LevelArgs &a, int is_w, hipStream_t s)
+{
+	if (a.nfeat == 0) return hipSuccess;
+	if (is_w) k_level_lord_stats<256, true, 0><<<a.nfeat, 256, 0, s>>>(a);
+	else if (a.slot == 0) k_level_lord_stats<256, false, 0><<<a.nfeat, 256, 0, s>>>(a);
+	else k_level_lord_stats<256, false, 1><<<a.nfeat, 256, 0, s>>>(a);
+	return hipGetLastError();
+}
+
+hipError_t lord_level_move(const LevelArgs &a, int is_w, hipStream_t s)
+{
+	if (a.nfeat == 0) return hipSuccess;
+	if (is_w) launch_lord_move<true, 0>(a, s);
+	else if (a.slot == 0) launch_lord_move<false, 0>(a, s);
+	else launch_lord_move<false, 1>(a, s);
+	return hipGetLastError();
+}
+
+hipError_t lord_pos(const uint32_t *feats, uint32_t nfeat, const uint64_t *lcp, uint64_t lbase, const uint64_t *col_ptr,
+                    const uint2 *csc, uint32_t *pos, hipStream_t s)
+{
+	if (nfeat == 0) return hipSuccess;
+	k_lord_pos<<<nfeat, 256, 0, s>>>(feats, lcp, lbase, col_ptr, csc, pos);
+	return hipGetLastError();
+}
+
+hipError_t lord_fill(const uint32_t *feats, uint32_t nfeat, const uint64_t *lcp, uint64_t lbase, const uint64_t *col_ptr,
+                     const uint2 *csc, const uint32_t *pos_next, float *lx, uint32_t *lnext, uint32_t *row0,
+                     hipStream_t s)
+{
+	if (nfeat == 0) return hipSuccess;
+	k_lord_fill<<<nfeat, 256, 0, s>>>(feats, lcp, lbase, col_ptr, csc, pos_next, lx, lnext, row0);
+	return hipGetLastError();
+}
+
+hipError_t rows_gather(RowRec *dst, const RowRec *src, const uint32_t *idx, uint32_t n, hipStream_t s)
+{
+	if (n == 0) return hipSuccess;
+	k_rows_gather<<<(unsigned)(((uint64_t)n * 4 + 255) / 256), 256, 0, s>>>(dst, src, idx, n);
+	return hipGetLastError();
+}
+
+hipError_t rows_scatter(RowRec *dst, const RowRec *src, const uint32_t *idx, uint32_t n, hipStream_t s)
+{
+	if (n == 0) return hipSuccess;
+	k_rows_scatter<<<(unsigned)(((uint64_t)n * 4 + 255) / 256), 256, 0, s>>>(dst, src, idx, n);
+	return hipGetLastError();
+}
+
+}  // namespace vbk

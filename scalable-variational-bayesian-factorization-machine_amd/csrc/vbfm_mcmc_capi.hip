@@ -388,6 +388,7 @@ int vbfm_mcmc_init(vbfm_ctx *c, const vbfm_mcmc_config *cfg)
 	return guarded(c, [&] {
 		if (cfg->rng != VBFM_RNG_REFERENCE && cfg->rng != VBFM_RNG_DEVICE) throw std::string("unknown rng mode");
 		mc_free(c);
+		if (c->lord) lord_release(c, true);   // the MCMC kernels index rows in row order
 		c->mc = new McState();
 		McState &m = *c->mc;
 		for (int i = 0; i < MEV_N; i++) HIPCHK(hipEventCreate(&m.ev[i]));

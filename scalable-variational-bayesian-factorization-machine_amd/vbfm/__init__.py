@@ -29,6 +29,9 @@ P_u32, P_u64, P_f32, P_f64, P_u8 = (C.POINTER(C.c_uint32), C.POINTER(C.c_uint64)
                                     C.POINTER(C.c_double), C.POINTER(C.c_uint8))
 
 
+LAYOUTS = {"auto": 0, "column": 1, "level": 2}   # VBFM_LAYOUT_* (include/vbfm.h)
+
+
 class VbfmError(RuntimeError):
     pass
 
@@ -116,6 +119,7 @@ EXPORTS = ["vbfm_abi_version", "vbfm_last_error", "vbfm_create", "vbfm_destroy",
            "vbfm_set_params", "vbfm_get_params", "vbfm_init_params_device", "vbfm_init_caches", "vbfm_iterate", "vbfm_get_test_pred",
            "vbfm_step_w0", "vbfm_step_w", "vbfm_step_qcache", "vbfm_step_v", "vbfm_step_hyper",
            "vbfm_free_energy", "vbfm_get_rows", "vbfm_get_test_e", "vbfm_factor_sweep", "vbfm_set_profiling",
+           "vbfm_set_layout", "vbfm_get_layout",
            "vbfm_comm_unique_id", "vbfm_comm_init", "vbfm_load_data", "vbfm_free_host_data",
            "vbfm_init_params_host", "vbfm_mcmc_init", "vbfm_mcmc_set_params", "vbfm_mcmc_get_params",
            "vbfm_mcmc_init_caches", "vbfm_mcmc_iterate", "vbfm_mcmc_get_test_pred", "vbfm_mcmc_factor_sweep"]
@@ -158,6 +162,8 @@ def lib():
         L.vbfm_get_test_e.argtypes = [V, P_f64]
         L.vbfm_factor_sweep.argtypes = [V, P_f64]
         L.vbfm_set_profiling.argtypes = [V, C.c_int32]
+        L.vbfm_set_layout.argtypes = [V, C.c_int32]
+        L.vbfm_get_layout.argtypes = [V, C.POINTER(C.c_int32)]
         L.vbfm_comm_unique_id.argtypes = [C.POINTER(C.c_uint8)]
         L.vbfm_comm_init.argtypes = [V, C.c_int32, C.c_int32, C.POINTER(C.c_uint8)]
         L.vbfm_load_data.argtypes = [C.c_char_p, C.POINTER(HostData)]
@@ -264,7 +270,7 @@ class FMLearnVB:
     """fm_learn_vb_simultaneous on one MI355X (src/libfm/src/fm_learn_vb_simultaneous.h)."""
 
     def __init__(self, k0=1, k1=1, num_factor=8, num_attribute=0, attr_group=None,
-                 min_target=1.0, max_target=5.0, device=0):
+                 min_target=1.0, max_target=5.0, device=0, layout="auto"):
         self.k0, self.k1, self.k, self.D = int(bool(k0)), int(bool(k1)), int(num_factor), int(num_attribute)
         self.attr_group = None if attr_group is None else np.ascontiguousarray(attr_group, dtype=np.uint32)
         self.G = 1 if self.attr_group is None else int(self.attr_group.max()) + 1 if self.D else 1
@@ -272,8 +278,16 @@ class FMLearnVB:
                      min_target, max_target, device, 0)
         self._ctx = C.c_void_p()
         _check(lib().vbfm_create(C.byref(self._ctx), C.byref(cfg)))
+        _check(lib().vbfm_set_layout(self._ctx, LAYOUTS[layout]), self._ctx)
         self.num_iter_done = 0
         self.fm_v = self.fm_w = None
+
+    def layout(self):
+        """Row layout in use for the sweeps: "column" (row order, gather) or "level"
+        (records kept in the current level's column order, streamed)."""
+        v = C.c_int32()
+        _check(lib().vbfm_get_layout(self._ctx, C.byref(v)), self._ctx)
+        return {1: "column", 2: "level"}[v.value]
 
     # -- parameters ---------------------------------------------------------------------
     def _params_struct(self, arrs):

@@ -127,25 +127,32 @@ def test_trace_tiny_vs_reference(case):
     close(fml.predict(), a["iter%d_pred" % last])
 
 
+@pytest.mark.parametrize("layout", ["column", "level"])
 @pytest.mark.parametrize("split", ["fused", "split"])
-def test_trace_synthetic_vs_reference(synth_files, split, monkeypatch):
-    """split: the row-sharded kernels (stats -> all-reduce -> correct) on one rank."""
+def test_trace_synthetic_vs_reference(synth_files, split, layout, monkeypatch):
+    """split: the row-sharded kernels (stats -> all-reduce -> correct) on one rank;
+    layout: row caches gathered in row order, or kept in level order and streamed."""
     if split == "split":
         monkeypatch.setenv("VBFM_FORCE_SPLIT", "1")
+    monkeypatch.setenv("VBFM_LAYOUT", layout)
     t, a = load_case("synth")
     train, test = vbfm.DataSubset.load(synth_files["train"]), vbfm.DataSubset.load(synth_files["test"])
     fml, stats = run_trace(train, test, t["meta"])
+    assert fml.layout() == layout
     assert stats[0].num_levels == t["meta"]["n_fields"]
     check_trace(stats, t["trace"])
     close(fml.get_params()["mu_v"], a["final_mu_v"])
 
 
+@pytest.mark.parametrize("layout", ["column", "level"])
 @pytest.mark.parametrize("split", ["fused", "split", "rccl"])
-def test_trace_movielens_split_vs_reference(sa_split, split, monkeypatch):
+def test_trace_movielens_split_vs_reference(sa_split, split, layout, monkeypatch):
     """split: the row-sharded kernels on one rank; rccl: the same through a real 1-rank RCCL
-    communicator (every ncclAllReduce of the multi-GPU path runs)."""
+    communicator (every ncclAllReduce of the multi-GPU path runs). Every ML-1M row is one
+    (user, item) pair, so both dependency levels hold every row: the level layout applies."""
     if split != "fused":
         monkeypatch.setenv("VBFM_FORCE_SPLIT", "1")
+    monkeypatch.setenv("VBFM_LAYOUT", layout)
     t, a = load_case("sa_k8")
     train, test = vbfm.DataSubset.load(sa_split["train"]), vbfm.DataSubset.load(sa_split["test"])
     if split == "rccl":
@@ -161,6 +168,7 @@ def test_trace_movielens_split_vs_reference(sa_split, split, monkeypatch):
         stats = [fml.iterate() for _ in range(m["iter"])]
     else:
         fml, stats = run_trace(train, test, t["meta"])
+    assert fml.layout() == layout
     check_trace(stats, t["trace"])
     close(fml.get_params()["mu_w"], a["final_mu_w"])
 
@@ -183,11 +191,14 @@ def test_device_generator_matches_spec():
     np.testing.assert_array_equal(lv[present], (np.arange(F * S) // S + 1)[present])
 
 
-@pytest.mark.parametrize("predict", ["exact", "blocked"])
-def test_generated_data_vs_oracle_two_iterations(predict, monkeypatch):
+@pytest.mark.parametrize("predict,layout", [("exact", "column"), ("blocked", "column"), ("exact", "level"),
+                                            ("blocked", "level")])
+def test_generated_data_vs_oracle_two_iterations(predict, layout, monkeypatch):
     """Device-generated field data (real-valued x) through 2 iterations vs the oracle, with
-    both forms of the prediction kernels (blocked: ~1 ulp from the reference's order)."""
+    both forms of the prediction kernels (blocked: ~1 ulp from the reference's order) and
+    both row layouts."""
     monkeypatch.setenv("VBFM_PREDICT", predict)
+    monkeypatch.setenv("VBFM_LAYOUT", layout)
     n, F, S, seed, k = 60000, 8, 500, 3, 11
     D = F * S + 1
     rp, f, v, y = synth.generate(n, F, S, seed, 1)
@@ -203,6 +214,7 @@ def test_generated_data_vs_oracle_two_iterations(predict, monkeypatch):
     o.init_params(7, 0.1)
     o.attach(tr, te)
     o.init_caches()
+    assert fml.layout() == layout
     rg, ro = fml.rows(), o.rows()
     if predict == "exact":
         np.testing.assert_array_equal(rg["e"], ro["e"])
@@ -230,3 +242,81 @@ def test_deterministic_run_to_run():
     a, b = run(), run()
     assert a[0] == b[0]
     np.testing.assert_array_equal(a[1], b[1])
+
+
+def _synth_learner(n, F, S, k, seed, layout, dim=(1, 1)):
+    rp, f, v, y = synth.generate(n, F, S, seed, 1)
+    rpt, ft, vt, yt = synth.generate(500, F, S, seed + 1, 1)
+    D = F * S + 1
+    g = vbfm.FMLearnVB(dim[0], dim[1], k, D, min_target=float(y.min()), max_target=float(y.max()), layout=layout)
+    g.init(5, 0.1)
+    g.set_data(vbfm.DataSubset.from_csr(rp, f, v, y, F * S), vbfm.DataSubset.from_csr(rpt, ft, vt, yt, F * S))
+    o = oc.VB(dim[0], dim[1], k, D)
+    o.init_params(5, 0.1)
+    o.attach(oc.Data(csr=(n, rp, f, v, y)), oc.Data(csr=(500, rpt, ft, vt, yt)))
+    return g, o
+
+
+@pytest.mark.parametrize("dim", [(1, 1), (1, 0), (0, 0)])
+def test_update_all_steps_level_layout(dim):
+    """update_all step by step with the level-ordered row store (every step reads the rows
+    back in row order): q-caches bit-exact, everything else within REL of the oracle.
+    dim (k0, k1) = (1, 0) / (0, 0): the q-cache of factor 0 comes from the row-parallel
+    kernel writing through the level-0 position map."""
+    g, o = _synth_learner(3000, 5, 40, 3, 21, "level", dim)
+    assert g.layout() == "level"
+    g.init_caches(); o.init_caches()
+    rg, ro = g.rows(), o.rows()
+    np.testing.assert_array_equal(rg["e"], ro["e"])
+    np.testing.assert_array_equal(rg["t"], ro["t"])
+    g.step_w0()
+    if dim[0]:
+        o.step("update_w0")
+    close(g.rows()["e"], o.rows()["e"])
+    g.step_w(); o.step("update_w_all")
+    close(g.get_params()["mu_w"], o.params()["mu_w"]); close(g.rows()["e"], o.rows()["e"])
+    for f in range(3):
+        g.step_qcache(f); o.step("add_main_q", f)
+        rg, ro = g.rows(), o.rows()
+        for key in ("q", "tq", "tz"):
+            np.testing.assert_array_equal(rg[key], ro[key], err_msg="f%d %s" % (f, key))
+        g.step_v(f); o.step("update_v_all", f)
+        rg, ro = g.rows(), o.rows()
+        for key in ("e", "t", "q", "tq", "tz"):
+            close(rg[key], ro[key])
+        close(g.get_params()["mu_v"], o.params()["mu_v"])
+        close(g.get_params()["sigma_v"], o.params()["sigma_v"])
+    g.step_hyper(); o.step("hyper")
+    close(g.get_params()["hyp_sigma_v"], o.params()["hyp_sigma_v"])
+
+
+def test_layouts_agree():
+    """Column-gather and level-ordered layouts compute bit-identical column statistics;
+    only the data-set sums (w0, alpha, free energy) are summed in another row order."""
+    res = {}
+    for layout in ("column", "level"):
+        g, _ = _synth_learner(40000, 6, 300, 4, 8, layout)
+        assert g.layout() == layout
+        g.init_caches()
+        st = [g.iterate() for _ in range(3)]
+        res[layout] = ([s.free_energy for s in st], [s.rmse for s in st], g.get_params()["mu_v"], g.rows()["e"])
+    close(res["level"][0], res["column"][0], 1e-12)
+    close(res["level"][1], res["column"][1], 1e-12)
+    close(res["level"][2], res["column"][2], 1e-12)
+    close(res["level"][3], res["column"][3], 1e-12)
+
+
+def test_level_layout_refused_when_levels_incomplete():
+    """tiny has rows of different lengths: a level misses rows, the level layout cannot
+    apply -- auto falls back to the column layout, an explicit request fails loudly."""
+    d = os.path.join(GOLDEN, "tiny")
+    train = vbfm.DataSubset.load(os.path.join(d, "train.libfm"))
+    test = vbfm.DataSubset.load(os.path.join(d, "test.libfm"))
+    g = gpu_learner(train, test, "1,1,3", 5, 0.1)
+    assert g.layout() == "column"
+    D = vbfm.num_all_attribute(train, test)
+    g2 = vbfm.FMLearnVB(1, 1, 3, D, min_target=train.min_target, max_target=train.max_target, layout="level")
+    g2.init(5, 0.1)
+    g2.set_data(train, test)
+    with pytest.raises(vbfm.VbfmError, match="level-ordered row layout not possible"):
+        g2.init_caches()
