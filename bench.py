@@ -97,6 +97,9 @@ def main():
     ap.add_argument("--config", default="c4", choices=sorted(CONFIGS))
     ap.add_argument("--rows", type=int, default=0, help="override rows per GPU")
     ap.add_argument("--k", type=int, default=0, help="override factors")
+    ap.add_argument("--method", default="vb", choices=["vb", "mcmc", "als"],
+                    help="vb: the metric (fm_learn_vb); mcmc / als: config 5's Gibbs draw_v path "
+                         "(device counter-based RNG streams), reported in the same unit")
     ap.add_argument("--layout", default="auto", choices=["auto", "column", "level"],
                     help="row-cache layout of the sweeps (include/vbfm.h VBFM_LAYOUT_*)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -126,12 +129,17 @@ def main():
     torch.cuda.set_device(local_rank)
 
     t0 = time.time()
-    fml = vbfm.FMLearnVB(1, 1, k, D, min_target=1.0, max_target=5.0, device=local_rank, layout=args.layout)
+    mc = args.method != "vb"
+    if mc:
+        fml = vbfm.FMLearnMCMC(1, 1, k, D, min_target=1.0, max_target=5.0, device=local_rank, method=args.method,
+                               layout=args.layout)
+    else:
+        fml = vbfm.FMLearnVB(1, 1, k, D, min_target=1.0, max_target=5.0, device=local_rank, layout=args.layout)
     if world > 1:
         obj = [vbfm.FMLearnVB.comm_unique_id() if rank == 0 else None]
         dist.broadcast_object_list(obj, src=0)
         fml.comm_init(world, rank, obj[0])
-    fml.init_device(seed=42)
+    fml.init_device(42)
     fml.synth(0, N, F, S, seed=1000 + rank, xmode=0)
     fml.synth(1, n_test, F, S, seed=500000 + rank, xmode=0)
     fml.init_caches()
@@ -139,9 +147,12 @@ def main():
     layout = fml.layout()
     log("rank %d: setup %.1f s (N=%d F=%d S=%d k=%d, %s layout)" % (rank, time.time() - t0, N, F, S, k, layout))
 
+    def rmse_of(st):
+        return st.rmse_all if mc else st.rmse
+
     for i in range(args.warmup):
         st = fml.iterate()
-        log("warmup %d: %.1f ms rmse %.6f F %.6e" % (i, st.ms_total, st.rmse, st.free_energy))
+        log("warmup %d: %.1f ms rmse %.6f" % (i, st.ms_total, rmse_of(st)))
 
     def barrier():
         if world > 1:
@@ -153,9 +164,10 @@ def main():
     stats = []
     for i in range(args.steps):
         stats.append(fml.iterate())
-        log("step %d: %.1f ms (v sweep %.1f, qcache %.1f, w %.1f, hyper %.1f, test %.1f) rmse %.6f" % (
-            i, stats[-1].ms_total, stats[-1].ms_v, stats[-1].ms_qcache_kernels, stats[-1].ms_w,
-            stats[-1].ms_hyper, stats[-1].ms_test, stats[-1].rmse))
+        st = stats[-1]
+        log("step %d: %.1f ms (v sweep %.1f, w %.1f, hyper %.1f, %s %.1f) rmse %.6f" % (
+            i, st.ms_total, st.ms_v, st.ms_w, st.ms_hyper, "predict" if mc else "test",
+            st.ms_predict if mc else st.ms_test, rmse_of(st)))
     barrier()
     elapsed = time.perf_counter() - t_start
     if world > 1:
@@ -172,15 +184,24 @@ def main():
     # per-factor model B = 128 B/nnz + 24 B/row + 32 B/feature, spread over the level
     # launches of a factor: 128 = q-build 8 (CSC) + stats 32 (8 CSC + 24 e,q,tq) +
     # correction 88 (8 CSC + 40 + 40). The same model prices both layouts.
+    # MCMC / ALS draw_v (fm_learn_mcmc.h:780-835) per factor: q-build 8 (CSC) + stats 24
+    # (8 CSC + 16 e,q) + correction 56 (8 CSC + 24 read e,q,q_next + 24 written) = 88 B/nnz,
+    # + 16 B/row (q zero/init) + 16 B/feature (v read/write)
     n_launch = sum(s.n_vlevel_launches for s in stats)
     ms_launch = sum(s.ms_vlevel_kernels for s in stats)
     avg_ms = ms_launch / max(1, n_launch)
-    bytes_per_launch = (128.0 * nnz + 24.0 * N + 32.0 * (F * S)) / max(1, levels)
+    if mc:
+        bytes_per_launch = (88.0 * nnz + 16.0 * N + 16.0 * (F * S)) / max(1, levels)
+    else:
+        bytes_per_launch = (128.0 * nnz + 24.0 * N + 32.0 * (F * S)) / max(1, levels)
     achieved = bytes_per_launch / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else 0.0
     sweep_ms = sum(s.ms_v for s in stats) / len(stats)
     traffic = None
-    kernel = "k_level_lord" if layout == "level" else "k_v_level_fused"
-    tf = os.path.join(ROOT, "profiles", "traffic_%s_%s.json" % (args.config, layout))
+    if mc:
+        kernel = "k_mc_level_lord" if layout == "level" else "k_mc_v_level"
+    else:
+        kernel = "k_level_lord" if layout == "level" else "k_v_level_fused"
+    tf = os.path.join(ROOT, "profiles", "traffic_%s_%s%s.json" % (args.config, layout, "_" + args.method if mc else ""))
     if os.path.exists(tf):
         with open(tf) as fh:
             traffic = json.load(fh).get("bytes_per_launch")
@@ -192,7 +213,9 @@ def main():
                 "device random init of mu (0.1*N(0,1))",
         "config": {"workload": cfg["desc"], "rows_per_gpu": N, "fields": F, "ids_per_field": S,
                    "features": F * S, "k": k, "nnz_per_gpu": nnz, "test_rows_per_gpu": n_test,
-                   "levels": levels, "step": "one full VB iteration (update_all + test RMSE)",
+                   "levels": levels, "method": args.method,
+                   "step": ("one full %s iteration (draw_all + train/test re-prediction, device RNG streams)"
+                            % args.method.upper()) if mc else "one full VB iteration (update_all + test RMSE)",
                    "parallelism": "row-sharded dp%d" % world, "row_layout": layout},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
@@ -200,12 +223,13 @@ def main():
                      "launches": n_launch, "bytes_per_launch": bytes_per_launch},
         "factor_sweep_ms_per_step": sweep_ms,
         "factor_sweep_nnz_k_per_s": world * nnz * k / (sweep_ms * 1e-3),
-        "test_rmse": stats[-1].rmse, "free_energy": stats[-1].free_energy,
-        "phase_ms": {kk: getattr(stats[-1], kk) for kk in ("ms_w0", "ms_w", "ms_qcache_kernels", "ms_v",
-                                                             "ms_hyper", "ms_test", "ms_total")},
+        "test_rmse": rmse_of(stats[-1]), "free_energy": None if mc else stats[-1].free_energy,
+        "phase_ms": {kk: getattr(stats[-1], kk) for kk in (
+            ("ms_hyper", "ms_w", "ms_v", "ms_predict", "ms_total") if mc else
+            ("ms_w0", "ms_w", "ms_qcache_kernels", "ms_v", "ms_hyper", "ms_test", "ms_total"))},
         "cpu_baseline": None,
     }
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and not mc:
         try:
             rows = min(args.cpu_rows, N)
             result["cpu_baseline"] = cpu_baseline(cfg, rows, min(args.cpu_factors, k))

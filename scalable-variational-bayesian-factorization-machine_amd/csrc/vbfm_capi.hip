@@ -149,7 +149,7 @@ void build_lorder(vbfm_ctx *c, const std::vector<uint64_t> &cp, const std::vecto
 {
 	lord_release(c, true);
 	const int req = layout_request(c);
-	if (c->mc || req == VBFM_LAYOUT_COLUMN) return;
+	if (req == VBFM_LAYOUT_COLUMN) return;
 	DevData &d = c->tr;
 	const uint32_t L = nlevels(c), n = d.n, nf = d.nf;
 	std::string why;
@@ -508,14 +508,15 @@ double free_energy(vbfm_ctx *c, double energy)
 	return fe;
 }
 
-// the reference's exact summation order for small data sets, the factor-blocked form for
-// large ones (VBFM_PREDICT=exact|blocked overrides)
+// the reference's exact summation order for small data sets, the wave-per-row form for
+// large ones (VBFM_PREDICT=exact|blocked|wave overrides)
 int blocked_predict(const vbfm_ctx *c, const DevData &d)
 {
 	const char *env = getenv("VBFM_PREDICT");
 	if (env && !strcmp(env, "exact")) return 0;
 	if (env && !strcmp(env, "blocked")) return 1;
-	return (double)d.nnz * c->k > 5e7 ? 1 : 0;
+	if (env && !strcmp(env, "wave")) return 2;
+	return (double)d.nnz * c->k > 5e7 ? 2 : 0;
 }
 
 void test_predict(vbfm_ctx *c)

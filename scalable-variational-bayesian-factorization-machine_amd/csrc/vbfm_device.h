@@ -98,6 +98,14 @@ struct McArgs {
 	double2 *stats;            // row-sharded mode: per-level-feature (sum h*e, sum h^2), or nullptr
 	int slot;
 	uint32_t avg_len;
+	// level-ordered row store (as LevelArgs)
+	const uint64_t *lcp;
+	const float *lx;
+	const uint32_t *lnext;
+	uint64_t lbase;
+	const RowRec *src;
+	RowRec *dst;
+	int first_level;
 };
 
 // kernels launched from the C-ABI layer (vbfm_kernels.hip)
@@ -126,7 +134,9 @@ hipError_t rows_scatter(RowRec *dst, const RowRec *src, const uint32_t *idx, uin
 hipError_t mark_first(const uint64_t *row_ptr, const uint2 *csr, const uint64_t *col_ptr, uint2 *csc,
                       uint32_t n, hipStream_t s);
 // blocked = 0: the reference's summation order (bit-exact); 1: factors in blocks of 8
-// (exact per-factor sums, the -1/2 sum v^2 x^2 term summed block-major: ~1 ulp apart)
+// (exact per-factor sums, the -1/2 sum v^2 x^2 term summed block-major: ~1 ulp apart);
+// 2: one wave per row, lanes over factors (exact per-factor sums, cross-factor sums in a
+// butterfly: ~1 ulp apart; k <= 256, else the blocked form)
 hipError_t predict_e(const uint64_t *row_ptr, const uint2 *csr, const double2 *ms_v, const double2 *ms_w,
                      int k, int k1, int k0, double mu0, double *out_e, uint32_t n, int blocked,
                      hipStream_t s);
@@ -179,13 +189,15 @@ hipError_t mc_v_level(const McArgs &a, int mode, hipStream_t s);
 hipError_t mc_w_level(const McArgs &a, int mode, hipStream_t s);
 hipError_t mc_prior(const McArgs &a, uint32_t j0, uint32_t j1, int is_v, hipStream_t s);
 hipError_t mc_qcache(const uint64_t *row_ptr, const uint2 *csr, const double2 *par_f, uint32_t stride, RowRec *rows,
-                     uint32_t n, int slot, hipStream_t s);
+                     uint32_t n, int slot, const uint32_t *pos, hipStream_t s);
+// MCMC / ALS level on the level-ordered store; mode as mc_v_level (2 = draw + move)
+hipError_t mc_lord_level(const McArgs &a, int mode, int is_w, hipStream_t s);
 // per-block sums over rows; mode 0: e*e ; mode 1: e - w0
 hipError_t mc_row_sums(const RowRec *rows, uint32_t n, int mode, double w0, double *out, uint32_t nblocks,
                        hipStream_t s);
 hipError_t mc_e_shift(RowRec *rows, uint32_t n, double d, hipStream_t s);
 hipError_t mc_train_update(RowRec *rows, const double *yhat, const float *target, uint32_t n, double mn, double mx,
-                           double *out, uint32_t nblocks, hipStream_t s);
+                           double *out, uint32_t nblocks, const uint32_t *pos, hipStream_t s);
 // per block: (sum err_this^2, sum |err_this|, sum err_all^2, sum |err_all|) at out[4*b]
 hipError_t mc_test_update(const double *e_test, const float *target, uint32_t n, double mn, double mx,
                           double inv_iters, double *pred_this, double *pred_sum, double *out, uint32_t nblocks,

@@ -477,6 +477,112 @@ __global__ __launch_bounds__(256) void k_predict_t_blocked(const uint64_t *__res
 	rows[r].t = t;
 }
 
+// Wave form (large data sets): one 64-lane wave per row, factor f on lane f % 64 (pass
+// f / 64, KP passes). Each entry's k {mu, sigma} pairs are one contiguous run, read by the
+// wave as whole 1 KiB pieces instead of one strided pair per thread; the row's entries are
+// loaded once (one lane each) and broadcast. Every lane keeps the reference's order over the
+// row's entries for its factors; the per-factor terms are summed across lanes in a fixed
+// butterfly (~1 ulp from the reference's sequential factor order, like the blocked form),
+// the linear term is added after them in the reference's entry order.
+template <int KP>
+__global__ __launch_bounds__(256) void k_predict_e_wave(const uint64_t *__restrict__ row_ptr,
+                                                         const uint2 *__restrict__ csr,
+                                                         const double2 *__restrict__ ms_v,
+                                                         const double2 *__restrict__ ms_w, int k, int k1, int k0,
+                                                         double mu0, double *__restrict__ out, uint32_t n)
+{
+	const uint32_t lane = threadIdx.x & 63;
+	const uint32_t nwaves = gridDim.x * 4;
+	for (uint32_t r = (blockIdx.x * 256 + threadIdx.x) >> 6; r < n; r += nwaves) {
+		const uint64_t b = row_ptr[r], en = row_ptr[r + 1];
+		double q[KP];
+#pragma unroll
+		for (int c = 0; c < KP; ++c) q[c] = 0.0;
+		double qq = 0.0;
+		for (uint64_t p0 = b; p0 < en; p0 += 64) {
+			const uint32_t cnt = (uint32_t)min<uint64_t>(64, en - p0);
+			const uint2 mine = lane < cnt ? csr[p0 + lane] : make_uint2(0u, 0u);
+			for (uint32_t i = 0; i < cnt; ++i) {
+				const uint32_t j = __shfl(mine.x, (int)i, 64);
+				const float x = __uint_as_float(__shfl(mine.y, (int)i, 64));
+				const double2 *m = ms_v + (size_t)j * k;
+#pragma unroll
+				for (int c = 0; c < KP; ++c) {
+					const int f = (int)lane + 64 * c;
+					if (f < k) {
+						const double v = m[f].x;
+						q[c] += v * x;                             // :93-133
+						qq -= 0.5 * v * v * x * x;                 // :136-163
+					}
+				}
+			}
+		}
+		double e = 0.0;
+#pragma unroll
+		for (int c = 0; c < KP; ++c)
+			if ((int)lane + 64 * c < k) e += 0.5 * q[c] * q[c];
+		e = wave_sum(e);
+		qq = wave_sum(qq);
+		if (k1)                                                // (3) :166-188
+			for (uint64_t p = b; p < en; ++p) { const uint2 ent = csr[p]; qq += ms_w[ent.x].x * ent_x(ent); }
+		e = e + qq;
+		if (k0) e += mu0;
+		if (lane == 0) out[r] = e;
+	}
+}
+
+template <int KP>
+__global__ __launch_bounds__(256) void k_predict_t_wave(const uint64_t *__restrict__ row_ptr,
+                                                         const uint2 *__restrict__ csr,
+                                                         const double2 *__restrict__ ms_v,
+                                                         const double2 *__restrict__ ms_w, int k, int k1, int k0,
+                                                         double s0d, RowRec *__restrict__ rows, uint32_t n)
+{
+	const uint32_t lane = threadIdx.x & 63;
+	const uint32_t nwaves = gridDim.x * 4;
+	for (uint32_t r = (blockIdx.x * 256 + threadIdx.x) >> 6; r < n; r += nwaves) {
+		const uint64_t b = row_ptr[r], en = row_ptr[r + 1];
+		double q[KP], z[KP];
+#pragma unroll
+		for (int c = 0; c < KP; ++c) { q[c] = 0.0; z[c] = 0.0; }
+		double qq = 0.0;
+		for (uint64_t p0 = b; p0 < en; p0 += 64) {
+			const uint32_t cnt = (uint32_t)min<uint64_t>(64, en - p0);
+			const uint2 mine = lane < cnt ? csr[p0 + lane] : make_uint2(0u, 0u);
+			for (uint32_t i = 0; i < cnt; ++i) {
+				const uint32_t j = __shfl(mine.x, (int)i, 64);
+				const float x = __uint_as_float(__shfl(mine.y, (int)i, 64));
+				const double2 *m = ms_v + (size_t)j * k;
+#pragma unroll
+				for (int c = 0; c < KP; ++c) {
+					const int f = (int)lane + 64 * c;
+					if (f < k) {
+						const double2 vm = m[f];
+						q[c] += vm.x * x * vm.x * x;               // :222-254
+						z[c] += vm.y * x * x;
+						qq -= (vm.x * vm.x * x * x * x * x * vm.y + 0.5 * x * x * x * x * vm.y * vm.y);   // :257-281
+					}
+				}
+			}
+		}
+		double t = 0.0;
+#pragma unroll
+		for (int c = 0; c < KP; ++c)
+			if ((int)lane + 64 * c < k) t += (0.5 * z[c] * z[c] + z[c] * q[c]);
+		t = wave_sum(t);
+		qq = wave_sum(qq);
+		if (k1)                                                // (3) :284-301
+			for (uint64_t p = b; p < en; ++p) {
+				const uint2 ent = csr[p];
+				const float x = ent_x(ent);
+				qq += ms_w[ent.x].y * x * x;
+			}
+		t = t + qq;                                            // :304-311
+		if (k0) t += s0d;
+		if (lane == 0) rows[r].t = t;
+	}
+}
+
 // e = y - yhat (fm_learn_vb_simultaneous.h:42-44)
 __global__ void k_residual_init(RowRec *rows, const double *yhat, const float *target, uint32_t n)
 {
@@ -793,7 +899,11 @@ hipError_t predict_e(const uint64_t *row_ptr, const uint2 *csr, const double2 *m
                      int k0, double mu0, double *out, uint32_t n, int blocked, hipStream_t s)
 {
 	if (n == 0) return hipSuccess;
-	if (blocked) k_predict_e_blocked<8><<<grid_for(n), 256, 0, s>>>(row_ptr, csr, ms_v, ms_w, k, k1, k0, mu0, out, n);
+	const unsigned wg = (unsigned)std::min<uint64_t>(((uint64_t)n + 3) / 4, 8192);   // 4 waves (rows) per workgroup
+	if (blocked == 2 && k <= 64) k_predict_e_wave<1><<<wg, 256, 0, s>>>(row_ptr, csr, ms_v, ms_w, k, k1, k0, mu0, out, n);
+	else if (blocked == 2 && k <= 128) k_predict_e_wave<2><<<wg, 256, 0, s>>>(row_ptr, csr, ms_v, ms_w, k, k1, k0, mu0, out, n);
+	else if (blocked == 2 && k <= 256) k_predict_e_wave<4><<<wg, 256, 0, s>>>(row_ptr, csr, ms_v, ms_w, k, k1, k0, mu0, out, n);
+	else if (blocked) k_predict_e_blocked<8><<<grid_for(n), 256, 0, s>>>(row_ptr, csr, ms_v, ms_w, k, k1, k0, mu0, out, n);
 	else k_predict_e<<<grid_for(n), 256, 0, s>>>(row_ptr, csr, ms_v, ms_w, k, k1, k0, mu0, out, n);
 	return hipGetLastError();
 }
@@ -802,7 +912,11 @@ hipError_t predict_t(const uint64_t *row_ptr, const uint2 *csr, const double2 *m
                      int k0, double s0d, RowRec *rows, uint32_t n, int blocked, hipStream_t s)
 {
 	if (n == 0) return hipSuccess;
-	if (blocked) k_predict_t_blocked<8><<<grid_for(n), 256, 0, s>>>(row_ptr, csr, ms_v, ms_w, k, k1, k0, s0d, rows, n);
+	const unsigned wg = (unsigned)std::min<uint64_t>(((uint64_t)n + 3) / 4, 8192);
+	if (blocked == 2 && k <= 64) k_predict_t_wave<1><<<wg, 256, 0, s>>>(row_ptr, csr, ms_v, ms_w, k, k1, k0, s0d, rows, n);
+	else if (blocked == 2 && k <= 128) k_predict_t_wave<2><<<wg, 256, 0, s>>>(row_ptr, csr, ms_v, ms_w, k, k1, k0, s0d, rows, n);
+	else if (blocked == 2 && k <= 256) k_predict_t_wave<4><<<wg, 256, 0, s>>>(row_ptr, csr, ms_v, ms_w, k, k1, k0, s0d, rows, n);
+	else if (blocked) k_predict_t_blocked<8><<<grid_for(n), 256, 0, s>>>(row_ptr, csr, ms_v, ms_w, k, k1, k0, s0d, rows, n);
 	else k_predict_t<<<grid_for(n), 256, 0, s>>>(row_ptr, csr, ms_v, ms_w, k, k1, k0, s0d, rows, n);
 	return hipGetLastError();
 }

@@ -24,30 +24,74 @@
 // row -> position map (k_lord_pos) and the entry payload x / lnext (k_lord_fill), walking
 // the levels backwards so that one row-sized scratch array holds the next level's map.
 #include "vbfm_math.h"
+#include "vbfm_mc_math.h"
 
 namespace {
 
-template <bool IS_W, int P>
-DEVI void lo_stat(Rec &v, float x, double mo, double so, double &s1, double &s2)
-{
-	if constexpr (IS_W) w_stat(x, E(v), mo, s1, s2);
-	else v_stat(x, E(v), Q<P>(v), TQ<P>(v), mo, so, s1, s2);
-}
+// What one level does to one record, as a policy of the staging loops below.
+// VB (update_v :587-596/:623-643, update_w :534-539/:567-573): statistics, then the
+// correction with the new posterior; NEXT adds the q-cache term of the next factor.
+template <bool IS_W, int P, bool NEXT>
+struct VbOp {
+	double mo, so, mu, sig;
+	double2 nx;
+	bool go;
+	DEVI void stat(Rec &v, float x, double &s1, double &s2) const
+	{
+		if constexpr (IS_W) w_stat(x, E(v), mo, s1, s2);
+		else v_stat(x, E(v), Q<P>(v), TQ<P>(v), mo, so, s1, s2);
+	}
+	DEVI void apply(Rec &v, float x, bool first) const
+	{
+		if constexpr (IS_W) w_apply<NEXT>(v, x, first, go, mo, so, mu, sig, nx);
+		else v_apply<P, NEXT>(v, x, first, go, mo, so, mu, sig, nx);
+	}
+};
 
 template <bool IS_W>
-DEVI bool lo_post(double s1, double s2, double hyp, double alpha, double mo, double so, double &mu, double &sig,
+DEVI bool vb_post(double s1, double s2, double hyp, double alpha, double mo, double so, double &mu, double &sig,
                   uint32_t *counters, bool leader)
 {
 	if constexpr (IS_W) return w_post(s1, s2, hyp, alpha, mo, so, mu, sig, counters, leader);
 	else return v_post(s1, s2, hyp, alpha, mo, so, mu, sig, counters, leader);
 }
 
+// MCMC / ALS (draw_v :785-792/:826-834, draw_w :674-679/:712-717); row caches e (= yhat - y)
+// and the q-cache of factor f in slot P, of factor f+1 (or 0 after draw_w) in the other
 template <bool IS_W, int P, bool NEXT>
-DEVI void lo_apply(Rec &v, float x, bool first, bool go, double mo, double so, double mu, double sig, double2 nx)
-{
-	if constexpr (IS_W) w_apply<NEXT>(v, x, first, go, mo, so, mu, sig, nx);
-	else v_apply<P, NEXT>(v, x, first, go, mo, so, mu, sig, nx);
-}
+struct McOp {
+	double vo, v, vn;
+	bool go;
+	DEVI void stat(Rec &r, float x, double &s1, double &s2) const
+	{
+		if constexpr (IS_W) {
+			s1 += x * (E(r) - vo * x);
+			s2 += x * x;                                       // fp32 product
+		} else {
+			const double h = x * (Q<P>(r) - x * vo);
+			s1 += h * E(r);
+			s2 += h * h;
+		}
+	}
+	DEVI void apply(Rec &r, float x, bool first) const
+	{
+		if (go) {
+			if constexpr (IS_W) {
+				const double h = x;
+				E(r) -= h * (vo - v);
+			} else {
+				const double h = x * (Q<P>(r) - x * vo);
+				Q<P>(r) -= x * (vo - v);
+				E(r) -= h * (vo - v);
+			}
+		}
+		if constexpr (NEXT) {
+			const double a = vn * x;
+			double &q = IS_W ? Q<0>(r) : Q<1 - P>(r);
+			q = first ? 0.0 + a : q + a;
+		}
+	}
+};
 
 // ---- LDS staging -------------------------------------------------------------------------
 // A run of records moves between HBM and LDS four lanes per 64-B record (one 16-B piece
@@ -77,8 +121,8 @@ DEVI void lds_put(double2 *recs, uint32_t i, const Rec &v)
 }
 
 // statistics of a run of n records in chunks of CAP (the last chunk stays in LDS)
-template <int BLOCK, uint32_t CAP, bool IS_W, int P>
-DEVI void lord_stats(double2 *recs, const RowRec *src, const float *lx, uint32_t n, double mo, double so, double &s1,
+template <int BLOCK, uint32_t CAP, class Op>
+DEVI void lord_stats(double2 *recs, const RowRec *src, const float *lx, uint32_t n, const Op &op, double &s1,
                      double &s2)
 {
 	const double2 *s = reinterpret_cast<const double2 *>(src);
@@ -90,7 +134,7 @@ DEVI void lord_stats(double2 *recs, const RowRec *src, const float *lx, uint32_t
 		for (uint32_t i = threadIdx.x; i < m; i += BLOCK) {
 			Rec v;
 			lds_get(recs, i, v);
-			lo_stat<IS_W, P>(v, lx[base + i], mo, so, s1, s2);
+			op.stat(v, lx[base + i], s1, s2);
 		}
 	}
 }
@@ -98,10 +142,9 @@ DEVI void lord_stats(double2 *recs, const RowRec *src, const float *lx, uint32_t
 // correction of every record of the run and its move to the next level's order. resident:
 // the run (n <= CAP) is still in LDS from lord_stats. Every record is written even when the
 // guards skip the correction: the write IS the move.
-template <int BLOCK, uint32_t CAP, bool IS_W, int P, bool NEXT>
+template <int BLOCK, uint32_t CAP, class Op>
 DEVI void lord_move(double2 *recs, uint32_t *dsts, const RowRec *src, const float *lx, const uint32_t *nxt, uint32_t n,
-                    bool resident, RowRec *dst, bool first, bool go, double mo, double so, double mu, double sig,
-                    double2 nx)
+                    bool resident, RowRec *dst, bool first, const Op &op)
 {
 	const double2 *s = reinterpret_cast<const double2 *>(src);
 	double2 *d = reinterpret_cast<double2 *>(dst);
@@ -115,7 +158,7 @@ DEVI void lord_move(double2 *recs, uint32_t *dsts, const RowRec *src, const floa
 		for (uint32_t i = threadIdx.x; i < m; i += BLOCK) {
 			Rec v;
 			lds_get(recs, i, v);
-			lo_apply<IS_W, P, NEXT>(v, lx[base + i], first, go, mo, so, mu, sig, nx);
+			op.apply(v, lx[base + i], first);
 			lds_put(recs, i, v);
 			dsts[i] = nxt[base + i];
 		}
@@ -144,20 +187,18 @@ __global__ __launch_bounds__(BLOCK) void k_level_lord(LevelArgs a)
 	const RowRec *src = a.src + (sb - a.lbase);
 	const float *lx = a.lx + sb;
 	const double2 msj = a.ms[(size_t)j * a.ms_stride];
-	const double mo = msj.x, so = msj.y;
-	double2 nx = make_double2(0.0, 0.0);
-	if constexpr (NEXT) nx = a.ms_next[(size_t)j * a.ms_stride_next];
+	VbOp<IS_W, P, NEXT> op;
+	op.mo = msj.x; op.so = msj.y;
+	op.nx = NEXT ? a.ms_next[(size_t)j * a.ms_stride_next] : make_double2(0.0, 0.0);
 
 	double s1 = 0.0, s2 = 0.0;
-	lord_stats<BLOCK, CAP, IS_W, P>(recs, src, lx, n, mo, so, s1, s2);
+	lord_stats<BLOCK, CAP>(recs, src, lx, n, op, s1, s2);
 	block_sum2<BLOCK>(s1, s2, lds);
 
-	double mu, sig;
 	const double hyp = a.hyp[(size_t)a.attr_group[j] * a.hyp_stride];
-	const bool go = lo_post<IS_W>(s1, s2, hyp, a.alpha, mo, so, mu, sig, a.counters, threadIdx.x == 0);
-	if (threadIdx.x == 0) a.ms[(size_t)j * a.ms_stride] = make_double2(mu, sig);
-	lord_move<BLOCK, CAP, IS_W, P, NEXT>(recs, dsts, src, lx, a.lnext + sb, n, n <= CAP, a.dst, a.first_level != 0,
-	                                      go, mo, so, mu, sig, nx);
+	op.go = vb_post<IS_W>(s1, s2, hyp, a.alpha, op.mo, op.so, op.mu, op.sig, a.counters, threadIdx.x == 0);
+	if (threadIdx.x == 0) a.ms[(size_t)j * a.ms_stride] = make_double2(op.mu, op.sig);
+	lord_move<BLOCK, CAP>(recs, dsts, src, lx, a.lnext + sb, n, n <= CAP, a.dst, a.first_level != 0, op);
 }
 
 // split form (row-sharded multi-GPU): statistics of the local rows -> all-reduce -> move
@@ -171,8 +212,10 @@ __global__ __launch_bounds__(BLOCK) void k_level_lord_stats(LevelArgs a)
 	const uint64_t sb = a.lcp[blockIdx.x];
 	const uint32_t n = (uint32_t)(a.lcp[blockIdx.x + 1] - sb);
 	const double2 msj = a.ms[(size_t)j * a.ms_stride];
+	VbOp<IS_W, P, false> op;
+	op.mo = msj.x; op.so = msj.y;
 	double s1 = 0.0, s2 = 0.0;
-	lord_stats<BLOCK, CAP, IS_W, P>(recs, a.src + (sb - a.lbase), a.lx + sb, n, msj.x, msj.y, s1, s2);
+	lord_stats<BLOCK, CAP>(recs, a.src + (sb - a.lbase), a.lx + sb, n, op, s1, s2);
 	block_sum2<BLOCK>(s1, s2, lds);
 	if (threadIdx.x == 0) a.stats[blockIdx.x] = make_double2(s1, s2);
 }
@@ -188,14 +231,56 @@ __global__ __launch_bounds__(BLOCK) void k_level_lord_move(LevelArgs a)
 	const uint32_t n = (uint32_t)(a.lcp[blockIdx.x + 1] - sb);
 	const double2 msj = a.ms[(size_t)j * a.ms_stride];
 	const double2 st = a.stats[blockIdx.x];
-	double2 nx = make_double2(0.0, 0.0);
-	if constexpr (NEXT) nx = a.ms_next[(size_t)j * a.ms_stride_next];
-	double mu, sig;
+	VbOp<IS_W, P, NEXT> op;
+	op.mo = msj.x; op.so = msj.y;
+	op.nx = NEXT ? a.ms_next[(size_t)j * a.ms_stride_next] : make_double2(0.0, 0.0);
 	const double hyp = a.hyp[(size_t)a.attr_group[j] * a.hyp_stride];
-	const bool go = lo_post<IS_W>(st.x, st.y, hyp, a.alpha, msj.x, msj.y, mu, sig, a.counters, threadIdx.x == 0);
-	if (threadIdx.x == 0) a.ms[(size_t)j * a.ms_stride] = make_double2(mu, sig);
-	lord_move<BLOCK, CAP, IS_W, P, NEXT>(recs, dsts, a.src + (sb - a.lbase), a.lx + sb, a.lnext + sb, n, false, a.dst,
-	                                      a.first_level != 0, go, msj.x, msj.y, mu, sig, nx);
+	op.go = vb_post<IS_W>(st.x, st.y, hyp, a.alpha, op.mo, op.so, op.mu, op.sig, a.counters, threadIdx.x == 0);
+	if (threadIdx.x == 0) a.ms[(size_t)j * a.ms_stride] = make_double2(op.mu, op.sig);
+	lord_move<BLOCK, CAP>(recs, dsts, a.src + (sb - a.lbase), a.lx + sb, a.lnext + sb, n, false, a.dst,
+	                      a.first_level != 0, op);
+}
+
+// ---- MCMC / ALS on the level-ordered store -----------------------------------------------
+// MODE 0: fused; 1: statistics of this shard's rows into a.stats; 2: draw from the
+// all-reduced a.stats, correct and move. Launch shape (BLOCK) as the column-gather MCMC
+// kernel so that both reduce a column in the same order.
+template <int BLOCK, int R, bool IS_W, int P, bool NEXT, int MODE>
+__global__ __launch_bounds__(BLOCK) void k_mc_level_lord(McArgs a)
+{
+	constexpr uint32_t CAP = BLOCK * R;
+	__shared__ double2 recs[CAP * 4];
+	__shared__ uint32_t dsts[MODE == 1 ? 1 : CAP];
+	__shared__ double lds[2 * (BLOCK / 64)];
+	const uint32_t j = a.feats[blockIdx.x];
+	const uint64_t sb = a.lcp[blockIdx.x];
+	const uint32_t n = (uint32_t)(a.lcp[blockIdx.x + 1] - sb);
+	const RowRec *src = a.src + (sb - a.lbase);
+	const float *lx = a.lx + sb;
+	McOp<IS_W, P, NEXT> op;
+	op.vo = a.par[(size_t)j * a.stride].x;
+	op.vn = NEXT ? a.par_next[(size_t)j * a.next_stride].x : 0.0;
+	double sm = 0.0, ss = 0.0;
+	if constexpr (MODE != 2) {
+		lord_stats<BLOCK, CAP>(recs, src, lx, n, op, sm, ss);
+		block_sum2<BLOCK>(sm, ss, lds);
+		if constexpr (MODE == 1) {
+			if (threadIdx.x == 0) a.stats[blockIdx.x] = make_double2(sm, ss);
+			return;
+		}
+	} else {
+		const double2 st = a.stats[blockIdx.x];
+		sm = st.x;
+		ss = st.y;
+	}
+	if constexpr (MODE != 1) {
+		const uint32_t g = a.attr_group[j];
+		op.go = mc_draw(sm, ss, op.vo, a.lambda[(size_t)g * a.hstride], a.mu[(size_t)g * a.hstride], a.alpha,
+		                mc_z(a, j), a.z != nullptr, a.sample, !IS_W, op.v, a.counters, threadIdx.x == 0);
+		if (threadIdx.x == 0) a.par[(size_t)j * a.stride].x = op.v;
+		lord_move<BLOCK, CAP>(recs, dsts, src, lx, a.lnext + sb, n, MODE == 0 && n <= CAP, a.dst, a.first_level != 0,
+		                      op);
+	}
 }
 
 // ---- build -------------------------------------------------------------------------------
@@ -264,9 +349,45 @@ void launch_lord_move(const LevelArgs &a, hipStream_t s)
 	else k_level_lord_move<256, IS_W, P, false><<<a.nfeat, 256, 0, s>>>(a);
 }
 
+template <int BLOCK, int R, int MODE>
+void launch_mc_lord(const McArgs &a, int is_w, hipStream_t s)
+{
+	const bool nx = a.par_next != nullptr;
+	if (is_w) {
+		if (nx) k_mc_level_lord<BLOCK, R, true, 0, true, MODE><<<a.nfeat, BLOCK, 0, s>>>(a);
+		else k_mc_level_lord<BLOCK, R, true, 0, false, MODE><<<a.nfeat, BLOCK, 0, s>>>(a);
+	} else if (a.slot == 0) {
+		if (nx) k_mc_level_lord<BLOCK, R, false, 0, true, MODE><<<a.nfeat, BLOCK, 0, s>>>(a);
+		else k_mc_level_lord<BLOCK, R, false, 0, false, MODE><<<a.nfeat, BLOCK, 0, s>>>(a);
+	} else {
+		if (nx) k_mc_level_lord<BLOCK, R, false, 1, true, MODE><<<a.nfeat, BLOCK, 0, s>>>(a);
+		else k_mc_level_lord<BLOCK, R, false, 1, false, MODE><<<a.nfeat, BLOCK, 0, s>>>(a);
+	}
+}
+
+template <int MODE>
+void launch_mc_lord_shape(const McArgs &a, int is_w, hipStream_t s)
+{
+	// the column-gather MCMC kernel's BLOCK (vbfm_mcmc.hip launch_level), records per thread
+	// as the VB level kernel
+	if (a.avg_len <= 96) launch_mc_lord<64, 2, MODE>(a, is_w, s);
+	else if (a.avg_len <= 320) launch_mc_lord<256, 1, MODE>(a, is_w, s);
+	else if (a.avg_len <= 640) launch_mc_lord<256, 2, MODE>(a, is_w, s);
+	else launch_mc_lord<512, 2, MODE>(a, is_w, s);
+}
+
 }  // namespace
 
 namespace vbk {
+
+hipError_t mc_lord_level(const McArgs &a, int mode, int is_w, hipStream_t s)
+{
+	if (a.nfeat == 0) return hipSuccess;
+	if (mode == 0) launch_mc_lord_shape<0>(a, is_w, s);
+	else if (mode == 1) launch_mc_lord_shape<1>(a, is_w, s);
+	else launch_mc_lord_shape<2>(a, is_w, s);
+	return hipGetLastError();
+}
 
 hipError_t lord_level(const LevelArgs &a, int is_w, hipStream_t s)
 {

@@ -11,6 +11,7 @@
 #include "vbfm_device.h"
 
 #define DEVI __device__ __forceinline__
+#include "vbfm_mc_math.h"
 
 namespace {
 
@@ -53,63 +54,6 @@ DEVI double block_sum1(double a, double *lds)
 }
 
 DEVI float ent_x(uint2 ent) { return __uint_as_float(ent.y); }
-DEVI bool bad(double v) { return __builtin_isnan(v) || __builtin_isinf(v); }
-
-DEVI uint64_t splitmix64(uint64_t z)
-{
-	z += 0x9E3779B97F4A7C15ull;
-	z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
-	z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
-	return z ^ (z >> 31);
-}
-
-// counter-based standard normal (Box-Muller on two 53-bit uniforms)
-DEVI double device_normal(uint64_t seed, uint64_t stream, uint64_t j)
-{
-	const uint64_t base = seed * 0x9E3779B97F4A7C15ull + stream * 0xD1B54A32D192ED03ull + 2 * j;
-	const double u1 = ((double)(splitmix64(base) >> 11) + 1.0) * 0x1p-53;
-	const double u2 = (double)(splitmix64(base + 1) >> 11) * 0x1p-53;
-	return sqrt(-2.0 * log(u1)) * cos(6.283185307179586 * u2);
-}
-
-DEVI double mc_z(const McArgs &a, uint32_t j)
-{
-	if (!a.sample) return 0.0;
-	if (a.z) return a.z[j];
-	return device_normal(a.rng_seed, a.rng_stream, j);
-}
-
-// draw of one parameter from its conditional (fm_learn_mcmc.h:680-709 for w, :793-824 for
-// v, identical in form): returns false when the reference restores the old value and
-// skips the correction
-DEVI bool mc_draw(double mean_sum, double ss, double cur, double lambda, double mu, double alpha, double z,
-                  bool zref, bool sample, bool is_v, double &out, uint32_t *counters, bool leader)
-{
-	double m = mean_sum;
-	if (is_v) m -= cur * ss;                                   // :793 (draw_v only)
-	const double s2 = (double)1.0 / (lambda + alpha * ss);     // :680 / :794
-	m = -s2 * (alpha * m - mu * lambda);                       // :681 / :795
-	bool skipped = sample;
-	if (bad(s2)) out = 0.0;                                    // :686-687
-	else if (sample) {
-		const double sd = sqrt(s2);
-		skipped = sd == 0.0 || __builtin_isnan(sd);
-		out = skipped ? m : m + sd * z;                        // ran_gaussian(m, sd)
-	} else out = m;
-	// reference RNG: the host took a normal for this attribute unless z is NaN; count the
-	// attributes where the data disagree (the stream then parts from the reference's)
-	const bool off = zref ? (skipped != (bool)__builtin_isnan(z)) : skipped;
-	if (off && leader) atomicAdd(&counters[CNT_RNG_SKIP], 1u);
-	if (bad(out)) {
-		if (leader)
-			atomicAdd(&counters[__builtin_isnan(out) ? (is_v ? CNT_NAN_MU_V : CNT_NAN_MU_W)
-			                                         : (is_v ? CNT_INF_MU_V : CNT_INF_MU_W)], 1u);
-		out = cur;
-		return false;
-	}
-	return true;
-}
-
 // q-cache term of the next factor: cache[i].q += v_if * x_li (fm_learn_mcmc.h:404)
 template <int S> DEVI void mc_qacc(RowRec &r, float x, bool first, double vn)
 {
@@ -261,7 +205,7 @@ __global__ void k_mc_prior(McArgs a, uint32_t j0, uint32_t j1, int is_v)
 
 // q-cache of one factor from scratch (add_main_q, fm_learn_mcmc.h:384-409), row-parallel
 __global__ void k_mc_qcache(const uint64_t *row_ptr, const uint2 *csr, const double2 *par_f, uint32_t stride,
-                            RowRec *rows, uint32_t n, int slot)
+                            RowRec *rows, uint32_t n, int slot, const uint32_t *pos)
 {
 	const uint32_t r = blockIdx.x * 256u + threadIdx.x;
 	if (r >= n) return;
@@ -270,7 +214,8 @@ __global__ void k_mc_qcache(const uint64_t *row_ptr, const uint2 *csr, const dou
 		const uint2 ent = csr[p];
 		q += par_f[(size_t)ent.x * stride].x * ent_x(ent);
 	}
-	if (slot == 0) rows[r].q = q; else rows[r].q1 = q;
+	RowRec &rec = rows[pos ? pos[r] : r];   // record index of row r (level-ordered store: level-0 position)
+	if (slot == 0) rec.q = q; else rec.q1 = q;
 }
 
 // per block: mode 0 sum e^2 (draw_alpha :908-910), mode 1 sum (e - w0) (draw_w0 :635-637)
@@ -305,7 +250,8 @@ DEVI double clip(double p, double mn, double mx)
 // sum (clip(yhat) - y)^2, and e = yhat - y
 template <int BLOCK>
 __global__ __launch_bounds__(BLOCK) void k_mc_train_update(RowRec *rows, const double *yhat, const float *target,
-                                                           uint32_t n, double mn, double mx, double *out)
+                                                           uint32_t n, double mn, double mx, double *out,
+                                                           const uint32_t *pos)
 {
 	__shared__ double lds[BLOCK / 64];
 	double s = 0.0;
@@ -313,7 +259,7 @@ __global__ __launch_bounds__(BLOCK) void k_mc_train_update(RowRec *rows, const d
 		const double yh = yhat[c];
 		const double err = clip(yh, mn, mx) - target[c];
 		s += err * err;
-		rows[c].e = yh - target[c];
+		rows[pos ? pos[c] : c].e = yh - target[c];
 	}
 	s = block_sum1<BLOCK>(s, lds);
 	if (threadIdx.x == 0) out[blockIdx.x] = s;
@@ -398,12 +344,14 @@ static void launch_w(const McArgs &a, hipStream_t s)
 	else k_mc_w_level<BLOCK, false, MODE><<<a.nfeat, BLOCK, 0, s>>>(a);
 }
 
-// one wave per column up to 96 entries on average, else four
+// threads per column from the level's mean column length (the VB kernels' shapes; the
+// level-ordered MCMC kernel uses the same BLOCK, so both reduce a column in one order)
 template <int MODE>
 static void launch_level(const McArgs &a, bool is_w, hipStream_t s)
 {
 	if (a.avg_len <= 96) { if (is_w) launch_w<64, MODE>(a, s); else launch_v<64, MODE>(a, s); }
-	else { if (is_w) launch_w<256, MODE>(a, s); else launch_v<256, MODE>(a, s); }
+	else if (a.avg_len <= 640) { if (is_w) launch_w<256, MODE>(a, s); else launch_v<256, MODE>(a, s); }
+	else { if (is_w) launch_w<512, MODE>(a, s); else launch_v<512, MODE>(a, s); }
 }
 
 static hipError_t mc_level(const McArgs &a, int mode, bool is_w, hipStream_t s)
@@ -426,10 +374,10 @@ hipError_t mc_prior(const McArgs &a, uint32_t j0, uint32_t j1, int is_v, hipStre
 }
 
 hipError_t mc_qcache(const uint64_t *row_ptr, const uint2 *csr, const double2 *par_f, uint32_t stride, RowRec *rows,
-                     uint32_t n, int slot, hipStream_t s)
+                     uint32_t n, int slot, const uint32_t *pos, hipStream_t s)
 {
 	if (n == 0) return hipSuccess;
-	k_mc_qcache<<<grid_for(n), 256, 0, s>>>(row_ptr, csr, par_f, stride, rows, n, slot);
+	k_mc_qcache<<<grid_for(n), 256, 0, s>>>(row_ptr, csr, par_f, stride, rows, n, slot, pos);
 	return hipGetLastError();
 }
 
@@ -447,9 +395,9 @@ hipError_t mc_e_shift(RowRec *rows, uint32_t n, double d, hipStream_t s)
 }
 
 hipError_t mc_train_update(RowRec *rows, const double *yhat, const float *target, uint32_t n, double mn, double mx,
-                           double *out, uint32_t nblocks, hipStream_t s)
+                           double *out, uint32_t nblocks, const uint32_t *pos, hipStream_t s)
 {
-	k_mc_train_update<256><<<nblocks, 256, 0, s>>>(rows, yhat, target, n, mn, mx, out);
+	k_mc_train_update<256><<<nblocks, 256, 0, s>>>(rows, yhat, target, n, mn, mx, out, pos);
 	return hipGetLastError();
 }
 

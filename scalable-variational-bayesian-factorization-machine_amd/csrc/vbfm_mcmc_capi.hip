@@ -293,10 +293,31 @@ McArgs mc_args(vbfm_ctx *c, uint32_t l, bool is_w, int f)
 
 void mc_sweep(vbfm_ctx *c, bool is_w, int f)
 {
+	rows_level_order(c);
 	for (uint32_t l = 0; l < nlevels(c); l++) {
 		McArgs a = mc_args(c, l, is_w, f);
 		if (a.nfeat == 0) continue;
 		const size_t p = prof_begin(c, is_w ? 1 : 0);
+		if (c->lord) {   // level-ordered store: stream the runs, move the records to level l+1
+			a.lcp = c->lcp + c->level_ptr[l];
+			a.lx = c->lx;
+			a.lnext = c->lnext;
+			a.lbase = (uint64_t)l * c->tr.n;
+			a.src = c->rows;
+			a.dst = c->rows_alt;
+			a.first_level = l == 0;
+			if (!c->comm && !c->force_split) {
+				HIPCHK(vbk::mc_lord_level(a, 0, is_w, c->s));
+			} else {
+				HIPCHK(vbk::mc_lord_level(a, 1, is_w, c->s));
+				if (c->comm)
+					NCCLCHK(ncclAllReduce(c->stats, c->stats, 2 * (size_t)a.nfeat, ncclDouble, ncclSum, c->comm, c->s));
+				HIPCHK(vbk::mc_lord_level(a, 2, is_w, c->s));
+			}
+			std::swap(c->rows, c->rows_alt);
+			prof_end(c, p);
+			continue;
+		}
 		if (!c->comm && !c->force_split) {
 			HIPCHK(is_w ? vbk::mc_w_level(a, 0, c->s) : vbk::mc_v_level(a, 0, c->s));
 		} else {   // row-sharded: statistics of this shard, summed over shards, identical draws
@@ -326,7 +347,9 @@ void mc_step_v(vbfm_ctx *c, int f)
 	const int slot = f & 1;
 	if (c->q_ready[slot] != f) {
 		const size_t p = prof_begin(c, 2);
-		HIPCHK(vbk::mc_qcache(c->tr.row_ptr, c->tr.csr, c->ms_v + f, (uint32_t)c->k, c->rows, c->tr.n, slot, c->s));
+		rows_level_order(c);
+		HIPCHK(vbk::mc_qcache(c->tr.row_ptr, c->tr.csr, c->ms_v + f, (uint32_t)c->k, c->rows, c->tr.n, slot,
+		                      c->rows_lorder ? c->lpos0 : nullptr, c->s));
 		prof_end(c, p);
 	}
 	fill_normals(c, c->mc->v_lambda.data() + f, (size_t)c->k);
@@ -388,7 +411,6 @@ int vbfm_mcmc_init(vbfm_ctx *c, const vbfm_mcmc_config *cfg)
 	return guarded(c, [&] {
 		if (cfg->rng != VBFM_RNG_REFERENCE && cfg->rng != VBFM_RNG_DEVICE) throw std::string("unknown rng mode");
 		mc_free(c);
-		if (c->lord) lord_release(c, true);   // the MCMC kernels index rows in row order
 		c->mc = new McState();
 		McState &m = *c->mc;
 		for (int i = 0; i < MEV_N; i++) HIPCHK(hipEventCreate(&m.ev[i]));
@@ -505,7 +527,7 @@ int vbfm_mcmc_init_caches(vbfm_ctx *c)
 		// fm_learn_mcmc_simultaneous.h:71-80: predict train and test, e = yhat - y
 		mc_predict(c);
 		HIPCHK(vbk::mc_train_update(c->rows, c->scratch_n, c->tr.target, c->tr.n, c->min_target, c->max_target,
-		                            m.red_d, MC_RED_BLOCKS, c->s));
+		                            m.red_d, MC_RED_BLOCKS, c->rows_lorder ? c->lpos0 : nullptr, c->s));
 		sync(c);
 		m.iter = 0;
 		m.caches = true;
@@ -549,7 +571,8 @@ int vbfm_mcmc_iterate(vbfm_ctx *c, vbfm_mcmc_stats *o)
 		double tm[5] = {0, 0, 0, 0, 0};
 		for (uint32_t b = 0; b < MC_RED_BLOCKS; b++)
 			for (int q = 0; q < 4; q++) tm[q] += m.red_h[4 * b + q];
-		HIPCHK(vbk::mc_train_update(c->rows, c->scratch_n, c->tr.target, c->tr.n, mn, mx, c->red_d, c->RED_BLOCKS, c->s));
+		HIPCHK(vbk::mc_train_update(c->rows, c->scratch_n, c->tr.target, c->tr.n, mn, mx, c->red_d, c->RED_BLOCKS,
+		                            c->rows_lorder ? c->lpos0 : nullptr, c->s));
 		tm[4] = finish_sum(c, c->RED_BLOCKS);
 		allreduce_host(c, tm, 5);
 		HIPCHK(hipEventRecord(m.ev[MEV_PRED], c->s));

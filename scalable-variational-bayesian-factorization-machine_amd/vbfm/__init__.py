@@ -471,10 +471,10 @@ class FMLearnMCMC(FMLearnVB):
     normals from a counter-based generator on the device (bench scale)."""
 
     def __init__(self, k0=1, k1=1, num_factor=8, num_attribute=0, attr_group=None,
-                 min_target=1.0, max_target=5.0, device=0, method="mcmc"):
+                 min_target=1.0, max_target=5.0, device=0, method="mcmc", layout="auto"):
         if method not in ("mcmc", "als"):
             raise VbfmError("method must be mcmc or als")
-        super().__init__(k0, k1, num_factor, num_attribute, attr_group, min_target, max_target, device)
+        super().__init__(k0, k1, num_factor, num_attribute, attr_group, min_target, max_target, device, layout)
         self.method = method
 
     def init(self, seed, init_stdev=0.1, regular=(), rng=RNG_REFERENCE):

@@ -191,12 +191,12 @@ def test_device_generator_matches_spec():
     np.testing.assert_array_equal(lv[present], (np.arange(F * S) // S + 1)[present])
 
 
-@pytest.mark.parametrize("predict,layout", [("exact", "column"), ("blocked", "column"), ("exact", "level"),
-                                            ("blocked", "level")])
+@pytest.mark.parametrize("predict,layout", [("exact", "column"), ("blocked", "column"), ("wave", "column"),
+                                            ("exact", "level"), ("blocked", "level"), ("wave", "level")])
 def test_generated_data_vs_oracle_two_iterations(predict, layout, monkeypatch):
     """Device-generated field data (real-valued x) through 2 iterations vs the oracle, with
-    both forms of the prediction kernels (blocked: ~1 ulp from the reference's order) and
-    both row layouts."""
+    every form of the prediction kernels (blocked, wave: ~1 ulp from the reference's order)
+    and both row layouts."""
     monkeypatch.setenv("VBFM_PREDICT", predict)
     monkeypatch.setenv("VBFM_LAYOUT", layout)
     n, F, S, seed, k = 60000, 8, 500, 3, 11
@@ -320,3 +320,16 @@ def test_level_layout_refused_when_levels_incomplete():
     g2.set_data(train, test)
     with pytest.raises(vbfm.VbfmError, match="level-ordered row layout not possible"):
         g2.init_caches()
+
+
+@pytest.mark.parametrize("k", [70, 130])
+def test_wave_prediction_many_factors(k, monkeypatch):
+    """The wave-per-row prediction with two and three factor passes per lane (k > 64),
+    against the oracle's initial caches (e and T of every row)."""
+    monkeypatch.setenv("VBFM_PREDICT", "wave")
+    g, o = _synth_learner(4000, 6, 100, k, 31, "auto")
+    g.init_caches(); o.init_caches()
+    rg, ro = g.rows(), o.rows()
+    close(rg["e"], ro["e"], 1e-12)
+    close(rg["t"], ro["t"], 1e-12)
+    np.testing.assert_allclose(g.test_e(), oc.arr(o.s.e_test, o.s.n_test), rtol=1e-12, atol=1e-12)

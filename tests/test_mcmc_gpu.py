@@ -58,14 +58,25 @@ def run_case(case, synth_files, sa_split, rng=vbfm.RNG_REFERENCE):
     return t, a, fml, stats
 
 
+# data sets whose every dependency level holds each row once: the level-ordered store applies
+COMPLETE = ("synth_als", "synth_mcmc", "sa_mcmc")
+
+
+@pytest.mark.parametrize("layout", ["auto", "column"])
 @pytest.mark.parametrize("split", ["fused", "split"])
 @pytest.mark.parametrize("case", CASES)
-def test_mcmc_als_chain_vs_reference(case, split, synth_files, sa_split, monkeypatch):
+def test_mcmc_als_chain_vs_reference(case, split, layout, synth_files, sa_split, monkeypatch):
     """The whole chain: per-iteration Train= / Test= values, then the final parameters and
-    hyper-priors. split: the row-sharded kernels (statistics, then draw + correction)."""
+    hyper-priors. split: the row-sharded kernels (statistics, then draw + correction);
+    layout auto = the level-ordered row store on the complete-level data sets."""
+    if layout == "column" and case not in COMPLETE:
+        pytest.skip("auto is already the column layout here")
     if split == "split":
         monkeypatch.setenv("VBFM_FORCE_SPLIT", "1")
+    monkeypatch.setenv("VBFM_LAYOUT", layout)
     t, a, fml, stats = run_case(case, synth_files, sa_split)
+    expect = "level" if (layout == "auto" and case in COMPLETE) else "column"
+    assert fml.layout() == expect
     for it, st in enumerate(stats):
         ref = t["trace"][it]
         assert st.rng_skipped == 0
@@ -131,3 +142,17 @@ def test_device_rng_chain_is_statistically_equivalent(synth_files):
     ref = t["trace"][-1]["rmse_all"]
     assert np.isfinite(stats[-1].rmse_all)
     assert abs(stats[-1].rmse_all - ref) <= 0.05 * ref, (stats[-1].rmse_all, ref)
+
+
+def test_device_rng_layouts_agree(synth_files, monkeypatch):
+    """Device-RNG chain on both row layouts: the column statistics and draws are identical,
+    only the data-set sums (alpha, w0) add the rows in another order."""
+    runs = {}
+    for layout in ("column", "level"):
+        monkeypatch.setenv("VBFM_LAYOUT", layout)
+        _, _, fml, stats = run_case("synth_mcmc", synth_files, None, rng=vbfm.RNG_DEVICE)
+        assert fml.layout() == layout
+        runs[layout] = ([s.rmse_all for s in stats], fml.get_params()["v"])
+        fml.close()
+    assert rel_err(runs["level"][0], runs["column"][0]) <= 1e-10
+    assert rel_err(runs["level"][1], runs["column"][1]) <= 1e-10
