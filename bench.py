@@ -104,7 +104,7 @@ def main():
                     help="row-cache layout of the sweeps (include/vbfm.h VBFM_LAYOUT_*)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-rows", type=int, default=1_000_000)
-    ap.add_argument("--cpu-factors", type=int, default=2)
+    ap.add_argument("--cpu-factors", type=int, default=8)
     args = ap.parse_args()
 
     import numpy as np
@@ -184,14 +184,14 @@ def main():
     # per-factor model B = 128 B/nnz + 24 B/row + 32 B/feature, spread over the level
     # launches of a factor: 128 = q-build 8 (CSC) + stats 32 (8 CSC + 24 e,q,tq) +
     # correction 88 (8 CSC + 40 + 40). The same model prices both layouts.
-    # MCMC / ALS draw_v (fm_learn_mcmc.h:780-835) per factor: q-build 8 (CSC) + stats 24
-    # (8 CSC + 16 e,q) + correction 56 (8 CSC + 24 read e,q,q_next + 24 written) = 88 B/nnz,
-    # + 16 B/row (q zero/init) + 16 B/feature (v read/write)
+    # MCMC / ALS draw_v (fm_learn_mcmc.h:780-835), SURVEY §8d: per factor
+    # B = 72 B/nnz (q-build 8 + stats 8 CSC + 16 e,q + correction 8 CSC + 32 e,q read/write)
+    #   + 8 B/row + 16 B/feature
     n_launch = sum(s.n_vlevel_launches for s in stats)
     ms_launch = sum(s.ms_vlevel_kernels for s in stats)
     avg_ms = ms_launch / max(1, n_launch)
     if mc:
-        bytes_per_launch = (88.0 * nnz + 16.0 * N + 16.0 * (F * S)) / max(1, levels)
+        bytes_per_launch = (72.0 * nnz + 8.0 * N + 16.0 * (F * S)) / max(1, levels)
     else:
         bytes_per_launch = (128.0 * nnz + 24.0 * N + 32.0 * (F * S)) / max(1, levels)
     achieved = bytes_per_launch / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else 0.0
