@@ -100,6 +100,10 @@ def main():
     ap.add_argument("--method", default="vb", choices=["vb", "mcmc", "als"],
                     help="vb: the metric (fm_learn_vb); mcmc / als: config 5's Gibbs draw_v path "
                          "(device counter-based RNG streams), reported in the same unit")
+    ap.add_argument("--shard", default="rows", choices=["rows", "features"],
+                    help="rows: exact row shards, each rank its own rows (weak scaling, default); "
+                         "features: the north star's column partition, every rank all rows (strong "
+                         "scaling, Jacobi across shards)")
     ap.add_argument("--layout", default="auto", choices=["auto", "column", "level"],
                     help="row-cache layout of the sweeps (include/vbfm.h VBFM_LAYOUT_*)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -135,13 +139,19 @@ def main():
                                layout=args.layout)
     else:
         fml = vbfm.FMLearnVB(1, 1, k, D, min_target=1.0, max_target=5.0, device=local_rank, layout=args.layout)
+    fshard = args.shard == "features"
+    if fshard:
+        if mc:
+            raise SystemExit("--shard features is a VB mode")
+        fml.set_shard_mode("features")
     if world > 1:
         obj = [vbfm.FMLearnVB.comm_unique_id() if rank == 0 else None]
         dist.broadcast_object_list(obj, src=0)
         fml.comm_init(world, rank, obj[0])
     fml.init_device(42)
-    fml.synth(0, N, F, S, seed=1000 + rank, xmode=0)
-    fml.synth(1, n_test, F, S, seed=500000 + rank, xmode=0)
+    dseed = 0 if fshard else rank          # feature shards: every rank holds the same rows
+    fml.synth(0, N, F, S, seed=1000 + dseed, xmode=0)
+    fml.synth(1, n_test, F, S, seed=500000 + dseed, xmode=0)
     fml.init_caches()
     fml.set_profiling(True)
     layout = fml.layout()
@@ -176,7 +186,8 @@ def main():
         elapsed = float(t.item())
 
     nnz = N * F
-    value = world * nnz * k * args.steps / elapsed
+    units = 1 if fshard else world       # rows processed per step, in units of one rank's rows
+    value = units * nnz * k * args.steps / elapsed
     levels = stats[-1].num_levels
     # roofline of the dominant kernel (k_level_lord / k_v_level_fused, one launch per factor
     # and level). It does the whole factor sweep of its level (stats, posterior, correction
@@ -194,6 +205,8 @@ def main():
         bytes_per_launch = (72.0 * nnz + 8.0 * N + 16.0 * (F * S)) / max(1, levels)
     else:
         bytes_per_launch = (128.0 * nnz + 24.0 * N + 32.0 * (F * S)) / max(1, levels)
+    if fshard:
+        bytes_per_launch /= world          # each rank sweeps 1/world of every level's columns
     achieved = bytes_per_launch / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else 0.0
     sweep_ms = sum(s.ms_v for s in stats) / len(stats)
     traffic = None
@@ -208,7 +221,7 @@ def main():
     result = {
         "metric": METRIC, "value": value, "unit": "nnz*k/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": elapsed * 1000.0 / args.steps, "higher_is_better": True,
-        "scaling": "weak", "vs_baseline": None, "dtype": "f64",
+        "scaling": "strong" if fshard else "weak", "vs_baseline": None, "dtype": "f64",
         "data": "synthetic field-structured one-hot libfm data generated in HBM (tests/synth.py spec), "
                 "device random init of mu (0.1*N(0,1))",
         "config": {"workload": cfg["desc"], "rows_per_gpu": N, "fields": F, "ids_per_field": S,
@@ -216,13 +229,14 @@ def main():
                    "levels": levels, "method": args.method,
                    "step": ("one full %s iteration (draw_all + train/test re-prediction, device RNG streams)"
                             % args.method.upper()) if mc else "one full VB iteration (update_all + test RMSE)",
-                   "parallelism": "row-sharded dp%d" % world, "row_layout": layout},
+                   "parallelism": ("feature-sharded fs%d" if fshard else "row-sharded dp%d") % world,
+                   "row_layout": layout},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                      "kernel": kernel, "avg_launch_ms": avg_ms,
                      "launches": n_launch, "bytes_per_launch": bytes_per_launch},
         "factor_sweep_ms_per_step": sweep_ms,
-        "factor_sweep_nnz_k_per_s": world * nnz * k / (sweep_ms * 1e-3),
+        "factor_sweep_nnz_k_per_s": units * nnz * k / (sweep_ms * 1e-3),
         "test_rmse": rmse_of(stats[-1]), "free_energy": None if mc else stats[-1].free_energy,
         "phase_ms": {kk: getattr(stats[-1], kk) for kk in (
             ("ms_hyper", "ms_w", "ms_v", "ms_predict", "ms_total") if mc else

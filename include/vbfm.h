@@ -173,6 +173,21 @@ int vbfm_factor_sweep(vbfm_ctx *ctx, double *ms_device);
 int vbfm_comm_unique_id(uint8_t out[128]);
 int vbfm_comm_init(vbfm_ctx *ctx, int32_t nranks, int32_t rank, const uint8_t uid[128]);
 
+/* Partition of the VB sweep over ranks (set before vbfm_set_train).
+ *   VBFM_SHARD_ROWS (default): the exact row-sharded mode above.
+ *   VBFM_SHARD_FEATURES: the north star's feature-column partition. Every rank holds ALL train
+ *     rows; the columns of every dependency level are split into num_shards contiguous chunks
+ *     and each rank sweeps its chunk; after the w sweep and after every factor pass the ranks'
+ *     changes of the e / t row caches, their partial q-caches of the next factor and their
+ *     updated parameters are summed with one ncclAllReduce each. Shards do not see each
+ *     other's updates within a pass (Jacobi across shards), so results differ from the
+ *     reference's sequential sweep when num_shards > 1 (exact for num_shards = 1). Without a
+ *     communicator num_shards > 1 runs the shards one after another in this process (same
+ *     arithmetic; for tests). num_shards = 0: one shard per rank. VB learner only. */
+#define VBFM_SHARD_ROWS 0
+#define VBFM_SHARD_FEATURES 1
+int vbfm_set_shard_mode(vbfm_ctx *ctx, int32_t mode, int32_t num_shards);
+
 /* ---- MCMC / ALS learner (-method mcmc | als) -------------------------------------------
  * Replaces fm_learn_mcmc / fm_learn_mcmc_simultaneous (src/libfm/src/fm_learn_mcmc.h,
  * src/libfm/src/fm_learn_mcmc_simultaneous.h), regression, without relation blocks.

@@ -600,6 +600,91 @@ void or_vb_update_all(or_vb *st, const or_data *train)
 	if (!st->hyper_skipped) or_vb_free_energy(st, train);
 }
 
+/* ---- feature-sharded update_all (see vbfm_oracle.h) ----------------------------------- */
+/* partial q-cache of factor f over the features of one shard, ascending id (the order the
+ * fused kernels add a row's own entries in), from 0.0 */
+static void fs_partial_q(const or_vb *st, const or_data *train, int f, int s, const int32_t *shard,
+                         double *q, double *tq, double *tz)
+{
+	uint32_t i, c;
+	uint64_t p;
+	const double *v = st->mu_v + (size_t)f * st->D, *vs = st->sig_v + (size_t)f * st->D;
+	for (c = 0; c < train->num_rows; c++) { q[c] = 0.0; tq[c] = 0.0; tz[c] = 0.0; }
+	for (i = 0; i < train->num_feature; i++) {
+		if (shard[i] != s) continue;
+		for (p = train->col_ptr[i]; p < train->col_ptr[i + 1]; p++) {
+			uint32_t r = train->col_row[p];
+			float x = train->col_val[p];
+			q[r] += v[i] * x;
+			tq[r] += vs[i] * x * x;
+			tz[r] += v[i] * v[i] * x * x;
+		}
+	}
+}
+
+/* one pass (f < 0: the w sweep) over all shards, then the sums of their changes */
+static void fs_pass(or_vb *st, const or_data *train, int f, int P, const int32_t *shard)
+{
+	const uint32_t n = train->num_rows;
+	const int next = f < 0 ? (st->k > 0 ? 0 : -1) : (f + 1 < st->k ? f + 1 : -1);
+	double *e0 = (double *)xcalloc(n, 8), *t0 = (double *)xcalloc(n, 8);
+	double *q0 = (double *)xcalloc(n, 8), *tq0 = (double *)xcalloc(n, 8), *tz0 = (double *)xcalloc(n, 8);
+	double *de = (double *)xcalloc(n, 8), *dt = (double *)xcalloc(n, 8);
+	double *nq = (double *)xcalloc(n, 8), *ntq = (double *)xcalloc(n, 8), *ntz = (double *)xcalloc(n, 8);
+	double *pq = (double *)xcalloc(n, 8), *ptq = (double *)xcalloc(n, 8), *ptz = (double *)xcalloc(n, 8);
+	uint32_t c, i;
+	int s;
+	memcpy(e0, st->e, n * 8); memcpy(t0, st->t, n * 8);
+	memcpy(q0, st->q, n * 8); memcpy(tq0, st->tq, n * 8); memcpy(tz0, st->tz, n * 8);
+	for (s = 0; s < P; s++) {
+		memcpy(st->e, e0, n * 8); memcpy(st->t, t0, n * 8);
+		memcpy(st->q, q0, n * 8); memcpy(st->tq, tq0, n * 8); memcpy(st->tz, tz0, n * 8);
+		for (i = 0; i < train->num_feature; i++) {
+			uint64_t b = train->col_ptr[i], m = train->col_ptr[i + 1] - b;
+			if (shard[i] != s) continue;
+			if (f < 0)
+				vb_update_w(st, &st->mu_w[i], &st->sig_w[i], st->sigma_w[st->attr_group[i]], train->col_row + b,
+				            train->col_val + b, m);
+			else
+				vb_update_v(st, &st->mu_v[(size_t)f * st->D + i], &st->sig_v[(size_t)f * st->D + i],
+				            st->sigma_v[(size_t)st->attr_group[i] * st->k + f], train->col_row + b, train->col_val + b, m);
+		}
+		if (next >= 0) fs_partial_q(st, train, next, s, shard, pq, ptq, ptz);
+		for (c = 0; c < n; c++) {
+			double a = st->e[c] - e0[c], b = st->t[c] - t0[c];
+			de[c] = s ? de[c] + a : a;
+			dt[c] = s ? dt[c] + b : b;
+			if (next >= 0) {
+				nq[c] = s ? nq[c] + pq[c] : pq[c];
+				ntq[c] = s ? ntq[c] + ptq[c] : ptq[c];
+				ntz[c] = s ? ntz[c] + ptz[c] : ptz[c];
+			}
+		}
+	}
+	for (c = 0; c < n; c++) {
+		st->e[c] = e0[c] + de[c];
+		st->t[c] = t0[c] + dt[c];
+		if (next >= 0) { st->q[c] = nq[c]; st->tq[c] = ntq[c]; st->tz[c] = ntz[c]; }
+	}
+	free(e0); free(t0); free(q0); free(tq0); free(tz0); free(de); free(dt);
+	free(nq); free(ntq); free(ntz); free(pq); free(ptq); free(ptz);
+}
+
+void or_vb_update_all_fsharded(or_vb *st, const or_data *train, int P, const int32_t *shard)
+{
+	int f, have_q = 0;
+	if (st->k0) or_vb_update_w0(st, train);
+	if (st->k1) { fs_pass(st, train, -1, P, shard); have_q = st->k > 0; }
+	if (st->D > 0)
+		for (f = 0; f < st->k; f++) {
+			if (!have_q) or_vb_add_main_q(st, train, f);   /* factor 0 without a w sweep */
+			fs_pass(st, train, f, P, shard);
+			have_q = 1;
+		}
+	st->hyper_skipped = or_vb_hyper(st, train);
+	if (!st->hyper_skipped) or_vb_free_energy(st, train);
+}
+
 void or_vb_iterate(or_vb *st, const or_data *train, const or_data *test,
                    double *rmse, double *mae, double *train_quirk)
 {

@@ -92,6 +92,14 @@ typedef void (*or_allreduce_fn)(double *buf, int n, void *user);
 void or_vb_update_all_sharded(or_vb *st, const or_data *train, uint32_t n_train_global,
                               uint32_t nf_train_global, or_allreduce_fn allreduce, void *user);
 
+/* Feature-sharded update_all: libvbfm's VBFM_SHARD_FEATURES mode (the north star's column
+ * partition; NOT an algorithm of the reference, so its parity is unpinned against it and
+ * equals or_vb_update_all only for nshards = 1, up to the e0 + (e - e0) rounding). Each
+ * shard updates its own features (shard[j] for j < train->num_feature, ascending id) from
+ * the same row caches; then the shards' changes of e / t and their partial q-caches of the
+ * next factor are summed in shard order. */
+void or_vb_update_all_fsharded(or_vb *st, const or_data *train, int nshards, const int32_t *shard);
+
 /* MCMC / ALS learner state (fm_learn_mcmc.h); ALS = mcmc without sampling / multilevel
  * (libfm.cpp:131-135). Draws come from the or_srand stream, as the reference's rand(). */
 typedef struct {

@@ -31,7 +31,7 @@ void sync(vbfm_ctx *c) { HIPCHK(hipStreamSynchronize(c->s)); }
 // all-reduce a few host doubles across the row shards (identity with one rank)
 void allreduce_host(vbfm_ctx *c, double *v, int n)
 {
-	if (!c->comm) return;
+	if (!c->row_comm()) return;   // feature shards hold every row: their sums are already global
 	HIPCHK(hipMemcpyAsync(c->red_d, v, n * sizeof(double), hipMemcpyHostToDevice, c->s));
 	NCCLCHK(ncclAllReduce(c->red_d, c->red_d, n, ncclDouble, ncclSum, c->comm, c->s));
 	HIPCHK(hipMemcpyAsync(v, c->red_d, n * sizeof(double), hipMemcpyDeviceToHost, c->s));
@@ -118,6 +118,7 @@ void upload(vbfm_ctx *c, DevData &d, const vbfm_csc *in, uint32_t nf_pad)
 }
 
 uint32_t nlevels(vbfm_ctx *c);
+LevelArgs level_args(vbfm_ctx *c, uint32_t l, bool is_w, int f);
 
 // ---- level-ordered row store (vbfm_lorder.hip) ------------------------------------------
 void lord_release(vbfm_ctx *c, bool keep_rows)
@@ -150,6 +151,10 @@ void build_lorder(vbfm_ctx *c, const std::vector<uint64_t> &cp, const std::vecto
 	lord_release(c, true);
 	const int req = layout_request(c);
 	if (req == VBFM_LAYOUT_COLUMN) return;
+	if (c->shard_mode == VBFM_SHARD_FEATURES) {
+		if (req == VBFM_LAYOUT_LEVEL) throw std::string("the level-ordered row layout does not combine with feature shards");
+		return;
+	}
 	DevData &d = c->tr;
 	const uint32_t L = nlevels(c), n = d.n, nf = d.nf;
 	std::string why;
@@ -216,6 +221,93 @@ void rows_row_order(vbfm_ctx *c)
 	c->rows_lorder = false;
 }
 
+// ---- feature shards (vbfm_set_shard_mode) ------------------------------------------------
+void fs_free(vbfm_ctx *c)
+{
+	dfree(c->fs_own); dfree(c->fs_base); dfree(c->fs_buf); dfree(c->fs_pbuf); dfree(c->fs_rows0);
+	c->fs_own_n = 0;
+	c->fs_lo.clear();
+}
+
+// chunk s of level l: level_feats[fs_lo[l*(P+1) + s], fs_lo[l*(P+1) + s + 1])
+void build_fshards(vbfm_ctx *c)
+{
+	fs_free(c);
+	if (c->shard_mode != VBFM_SHARD_FEATURES) return;
+	if (c->comm && c->fs_req > 1 && c->fs_req != c->nranks)
+		throw std::string("feature shards: num_shards must equal the number of ranks (or 0)");
+	const int P = c->comm ? c->nranks : std::max(1, c->fs_req);
+	c->fs_n = P;
+	const uint32_t L = nlevels(c), n = c->tr.n;
+	c->fs_lo.assign((size_t)L * (P + 1), 0);
+	for (uint32_t l = 0; l < L; l++) {
+		const uint32_t b = c->level_ptr[l], nl = c->level_ptr[l + 1] - b;
+		for (int s = 0; s <= P; s++) c->fs_lo[(size_t)l * (P + 1) + s] = b + (uint32_t)((uint64_t)nl * s / P);
+	}
+	if (c->comm) {
+		std::vector<uint32_t> feats(c->tr.nf), own;
+		if (c->tr.nf) HIPCHK(hipMemcpy(feats.data(), c->level_feats, (size_t)c->tr.nf * 4, hipMemcpyDeviceToHost));
+		for (uint32_t l = 0; l < L; l++)
+			for (uint32_t i = c->fs_lo[(size_t)l * (P + 1) + c->rank]; i < c->fs_lo[(size_t)l * (P + 1) + c->rank + 1]; i++)
+				own.push_back(feats[i]);
+		c->fs_own = dalloc<uint32_t>(own.size());
+		c->fs_own_n = (uint32_t)own.size();
+		if (!own.empty()) HIPCHK(hipMemcpy(c->fs_own, own.data(), own.size() * 4, hipMemcpyHostToDevice));
+		c->fs_pbuf = dalloc<double2>(c->tr.nf);
+	}
+	c->fs_base = dalloc<double>(2 * (size_t)n);
+	c->fs_buf = dalloc<double>(5 * (size_t)n);
+	if (!c->comm && P > 1) c->fs_rows0 = dalloc<RowRec>(n);
+}
+
+// one level of one shard: the shard's chunk of the level's columns (fused kernels; the fused
+// q-cache does not restart at a row's first entry: each shard sums its own entries into the
+// zeroed slot)
+void sweep_level_shard(vbfm_ctx *c, uint32_t l, bool is_w, int f, int s)
+{
+	LevelArgs a = level_args(c, l, is_w, f);
+	const size_t P1 = (size_t)c->fs_n + 1;
+	const uint32_t lo = c->fs_lo[l * P1 + s], hi = c->fs_lo[l * P1 + s + 1];
+	a.feats = c->level_feats + lo;
+	a.nfeat = hi - lo;
+	a.first_mask = 0;
+	if (a.nfeat == 0) return;
+	const size_t p = prof_begin(c, is_w ? 1 : 0);
+	HIPCHK(is_w ? vbk::w_level_fused(a, c->s) : vbk::v_level_fused(a, c->s));
+	prof_end(c, p);
+}
+
+// the w sweep (is_w) or the v sweep of factor f, feature-sharded: every shard starts from
+// the same row caches and sweeps its chunks (fm_learn_vb.h:390-406 / :420-438 restricted to
+// its columns), then the shards' changes are summed
+void fs_pass(vbfm_ctx *c, bool is_w, int f)
+{
+	const uint32_t n = c->tr.n;
+	const int next = is_w ? (c->k > 0 ? 0 : -1) : (f + 1 < c->k ? ((f + 1) & 1) : -1);
+	const bool local = !c->comm;   // shards run here one after another
+	const int s0 = local ? 0 : c->rank, s1 = local ? c->fs_n : c->rank + 1;
+	HIPCHK(vbk::fs_begin(c->rows, n, c->fs_base, next, c->s));
+	if (local && c->fs_n > 1)
+		HIPCHK(hipMemcpyAsync(c->fs_rows0, c->rows, (size_t)n * sizeof(RowRec), hipMemcpyDeviceToDevice, c->s));
+	for (int s = s0; s < s1; s++) {
+		if (s > s0)
+			HIPCHK(hipMemcpyAsync(c->rows, c->fs_rows0, (size_t)n * sizeof(RowRec), hipMemcpyDeviceToDevice, c->s));
+		for (uint32_t l = 0; l < nlevels(c); l++) sweep_level_shard(c, l, is_w, f, s);
+		HIPCHK(vbk::fs_pack(c->rows, n, c->fs_base, c->fs_buf, next, s > s0, c->s));
+	}
+	if (c->comm) {
+		NCCLCHK(ncclAllReduce(c->fs_buf, c->fs_buf, (next < 0 ? 2 : 5) * (size_t)n, ncclDouble, ncclSum, c->comm, c->s));
+		// parameters: each rank contributes its own features, zero elsewhere
+		double2 *ms = is_w ? c->ms_w : c->ms_v + f;
+		const uint32_t stride = is_w ? 1 : (uint32_t)c->k;
+		HIPCHK(hipMemsetAsync(c->fs_pbuf, 0, (size_t)c->tr.nf * 16, c->s));
+		HIPCHK(vbk::fs_params(ms, stride, c->fs_own, c->fs_own_n, c->fs_pbuf, 1, c->s));
+		NCCLCHK(ncclAllReduce(c->fs_pbuf, c->fs_pbuf, 2 * (size_t)c->tr.nf, ncclDouble, ncclSum, c->comm, c->s));
+		HIPCHK(vbk::fs_params(ms, stride, c->level_feats, c->tr.nf, c->fs_pbuf, 0, c->s));
+	}
+	HIPCHK(vbk::fs_unpack(c->rows, n, c->fs_base, c->fs_buf, next, c->s));
+}
+
 // Dependency levels of the train features (see vbfm_kernels.hip header). With several
 // row shards every round's levels are max-reduced over the shards, so all ranks share one
 // schedule: the one the un-sharded data set defines.
@@ -269,12 +361,13 @@ void build_schedule(vbfm_ctx *c)
 	}
 	uint32_t maxlev = 0;
 	for (uint32_t l = 0; l < L; l++) maxlev = std::max(maxlev, c->level_ptr[l + 1] - c->level_ptr[l]);
-	if ((c->comm || c->force_split) && maxlev > c->stats_cap) {
+	if ((c->row_comm() || c->force_split) && maxlev > c->stats_cap) {
 		dfree(c->stats);
 		c->stats = dalloc<double2>(maxlev);
 		c->stats_cap = maxlev;
 	}
 	c->sched_ready = true;
+	build_fshards(c);
 	build_lorder(c, cp, feats);
 }
 
@@ -344,6 +437,7 @@ LevelArgs level_args(vbfm_ctx *c, uint32_t l, bool is_w, int f)
 	a.counters = c->counters;
 	a.stats = c->stats;
 	a.avg_len = c->level_avg[l];
+	a.first_mask = ROW_FIRST;
 	if (is_w) {
 		a.slot = 0;                                          // fused q-cache of factor 0
 		a.ms_next = c->k > 0 ? c->ms_v : nullptr;          // factor 0: ms_v[j*k + 0]
@@ -392,11 +486,11 @@ void sweep_level(vbfm_ctx *c, uint32_t l, bool is_w, int f)
 		a.src = c->rows;
 		a.dst = c->rows_alt;
 		a.first_level = l == 0;
-		if (!c->comm && !c->force_split) {
+		if (!c->row_comm() && !c->force_split) {
 			HIPCHK(vbk::lord_level(a, is_w, c->s));
 		} else {
 			HIPCHK(vbk::lord_level_stats(a, is_w, c->s));
-			if (c->comm)
+			if (c->row_comm())
 				NCCLCHK(ncclAllReduce(c->stats, c->stats, 2 * (size_t)a.nfeat, ncclDouble, ncclSum, c->comm, c->s));
 			HIPCHK(vbk::lord_level_move(a, is_w, c->s));
 		}
@@ -404,7 +498,7 @@ void sweep_level(vbfm_ctx *c, uint32_t l, bool is_w, int f)
 		prof_end(c, p);
 		return;
 	}
-	if (!c->comm && !c->force_split) {
+	if (!c->row_comm() && !c->force_split) {
 		HIPCHK(is_w ? vbk::w_level_fused(a, c->s) : vbk::v_level_fused(a, c->s));
 		prof_end(c, p);
 		return;
@@ -412,7 +506,7 @@ void sweep_level(vbfm_ctx *c, uint32_t l, bool is_w, int f)
 	// row-sharded form: per-feature sufficient statistics of this shard's rows, summed over
 	// the shards, then every shard applies the identical posterior to its own rows
 	HIPCHK(is_w ? vbk::w_level_stats(a, c->s) : vbk::v_level_stats(a, c->s));
-	if (c->comm)
+	if (c->row_comm())
 		NCCLCHK(ncclAllReduce(c->stats, c->stats, 2 * (size_t)a.nfeat, ncclDouble, ncclSum, c->comm, c->s));
 	HIPCHK(is_w ? vbk::w_level_correct(a, c->s) : vbk::v_level_correct(a, c->s));
 	prof_end(c, p);
@@ -438,7 +532,9 @@ void step_w0(vbfm_ctx *c)
 void step_w(vbfm_ctx *c)
 {
 	rows_level_order(c);
-	for (uint32_t l = 0; l < nlevels(c); l++) sweep_level(c, l, true, 0);
+	if (c->shard_mode == VBFM_SHARD_FEATURES) fs_pass(c, true, 0);
+	else
+		for (uint32_t l = 0; l < nlevels(c); l++) sweep_level(c, l, true, 0);
 	if (c->k > 0) c->q_ready[0] = 0;
 }
 
@@ -462,7 +558,9 @@ void step_qcache(vbfm_ctx *c, int f)
 void step_v(vbfm_ctx *c, int f)
 {
 	rows_level_order(c);
-	for (uint32_t l = 0; l < nlevels(c); l++) sweep_level(c, l, false, f);
+	if (c->shard_mode == VBFM_SHARD_FEATURES) fs_pass(c, false, f);
+	else
+		for (uint32_t l = 0; l < nlevels(c); l++) sweep_level(c, l, false, f);
 	c->qslot = f & 1;
 	c->q_ready[f & 1] = -1;   // corrected in place, no longer the from-scratch sum add_main_q gives
 	if (f + 1 < c->k) c->q_ready[(f + 1) & 1] = f + 1;
@@ -625,6 +723,7 @@ void vbfm_destroy(vbfm_ctx *c)
 	dfree(c->level_feats); dfree(c->dup); dfree(c->red_d); dfree(c->perm_d); dfree(c->chunks_d);
 	dfree(c->chunk_out_d); dfree(c->counters); dfree(c->stats);
 	dfree(c->rows_alt); dfree(c->lcp); dfree(c->lx); dfree(c->lnext); dfree(c->lrow0); dfree(c->lpos0);
+	fs_free(c);
 	mc_free(c);
 	if (c->comm) ncclCommDestroy(c->comm);
 	for (hipEvent_t e : c->pev) (void)hipEventDestroy(e);
@@ -1047,6 +1146,18 @@ int vbfm_iterate(vbfm_ctx *c, vbfm_iter_stats *o)
 		st.ms_qcache = st.ms_qcache_kernels;
 		if (o) *o = st;
 	});
+}
+
+int vbfm_set_shard_mode(vbfm_ctx *c, int32_t mode, int32_t num_shards)
+{
+	if (!c) return fail(nullptr, "null context");
+	if (mode != VBFM_SHARD_ROWS && mode != VBFM_SHARD_FEATURES) return fail(c, "unknown shard mode");
+	if (num_shards < 0) return fail(c, "negative number of shards");
+	if (c->rows) return fail(c, "vbfm_set_shard_mode must precede vbfm_set_train");
+	if (c->mc && mode == VBFM_SHARD_FEATURES) return fail(c, "feature shards are implemented for the VB learner only");
+	c->shard_mode = mode;
+	c->fs_req = mode == VBFM_SHARD_FEATURES ? num_shards : 1;
+	return 0;
 }
 
 int vbfm_set_layout(vbfm_ctx *c, int32_t layout)

@@ -122,6 +122,18 @@ struct vbfm_ctx {
 	uint32_t *lnext = nullptr;     // [nnz] position of the entry's row in the next level
 	uint32_t *lrow0 = nullptr;     // [n] row at each level-0 position
 	uint32_t *lpos0 = nullptr;     // [n] level-0 position of each row
+	// feature-sharded mode (vbfm_set_shard_mode): shards own column chunks of every level
+	int shard_mode = VBFM_SHARD_ROWS;
+	int fs_req = 1;                // shards requested (no communicator: run one after another here)
+	int fs_n = 1;                  // shards in use
+	std::vector<uint32_t> fs_lo;   // [L * (fs_n + 1)] chunk bounds of each level in level_feats
+	uint32_t *fs_own = nullptr;    // this rank's features (all levels) for the parameter exchange
+	uint32_t fs_own_n = 0;
+	double *fs_base = nullptr;     // [2n] e, t at the start of a pass
+	double *fs_buf = nullptr;      // [5n] summed changes / partial q-caches
+	double2 *fs_pbuf = nullptr;    // [nf] parameter exchange
+	RowRec *fs_rows0 = nullptr;    // in-process shards: the rows at the start of a pass
+	bool row_comm() const { return comm && shard_mode == VBFM_SHARD_ROWS; }
 	McState *mc = nullptr;         // set by vbfm_mcmc_init: the context runs the MCMC / ALS learner
 };
 

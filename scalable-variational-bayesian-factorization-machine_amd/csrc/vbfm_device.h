@@ -61,6 +61,8 @@ struct LevelArgs {
 	uint32_t ms_stride_next;
 	int slot;                  // q-cache slot of the factor being swept (v) / of factor 0 (w)
 	uint32_t avg_len;          // mean column length of the level (launch shape)
+	uint32_t first_mask;       // ROW_FIRST: the fused q-cache restarts at a row's first entry;
+	                           // 0 (feature shards): partial sums from a zeroed slot
 	// level-ordered row store (vbfm_lorder.hip); unused by the column-gather kernels
 	const uint64_t *lcp;       // global position of each level feature's run, indexed like feats [nfeat+1]
 	const float *lx;           // x of every level-ordered entry (global position)
@@ -164,6 +166,14 @@ hipError_t level_init(uint32_t *level, uint32_t nf, hipStream_t s);
 hipError_t level_relax(const uint64_t *row_ptr, const uint2 *csr, uint32_t n, uint32_t nf, uint32_t *level,
                        uint32_t *changed, hipStream_t s);
 hipError_t mark_dups(const uint64_t *row_ptr, const uint2 *csr, uint32_t n, uint8_t *dup, hipStream_t s);
+// feature-sharded passes (vbfm_capi.hip fs_pass): save e/t and zero the next q-cache slot;
+// pack (or add) the shard's changes; unpack the summed changes; parameter exchange
+hipError_t fs_begin(RowRec *rows, uint32_t n, double *base, int next_slot, hipStream_t s);
+hipError_t fs_pack(const RowRec *rows, uint32_t n, const double *base, double *buf, int next_slot, int acc,
+                   hipStream_t s);
+hipError_t fs_unpack(RowRec *rows, uint32_t n, const double *base, const double *buf, int next_slot, hipStream_t s);
+hipError_t fs_params(double2 *ms, uint32_t stride, const uint32_t *feats, uint32_t nfeat, double2 *pbuf, int to_buf,
+                     hipStream_t s);
 // synthetic generator (tests/synth.py is the specification)
 hipError_t synth_csr(uint32_t n, uint32_t F, uint32_t S, uint64_t seed, int xmode, uint64_t *row_ptr,
                      uint2 *csr, float *target, hipStream_t s);

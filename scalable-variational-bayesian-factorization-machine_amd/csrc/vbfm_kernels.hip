@@ -24,7 +24,7 @@ namespace {
 
 template <int P, bool NEXT>
 DEVI void v_apply_serial(const uint2 *col, uint32_t n, RowRec *rows, bool go, double mo, double so, double mu,
-                         double sig, double2 nx)
+                         double sig, double2 nx, uint32_t fm)
 {
 	// a column listing some row twice: the reference corrects entry after entry, a repeated
 	// row seeing its own earlier update
@@ -32,7 +32,7 @@ DEVI void v_apply_serial(const uint2 *col, uint32_t n, RowRec *rows, bool go, do
 		const uint2 ent = col[i];
 		Rec v;
 		load_rec(rows, ent.x & ROW_MASK, v);
-		v_apply<P, NEXT>(v, ent_x(ent), (ent.x & ROW_FIRST) != 0, go, mo, so, mu, sig, nx);
+		v_apply<P, NEXT>(v, ent_x(ent), (ent.x & fm) != 0, go, mo, so, mu, sig, nx);
 		store_rec(rows, ent.x & ROW_MASK, v);
 	}
 }
@@ -84,20 +84,20 @@ __global__ __launch_bounds__(BLOCK) void k_v_level_fused(LevelArgs a)
 	if (!go && !NEXT) return;
 	if (a.dup[j]) {
 		__syncthreads();
-		if (threadIdx.x == 0) v_apply_serial<P, NEXT>(col, n, a.rows, go, mo, so, mu, sig, nx);
+		if (threadIdx.x == 0) v_apply_serial<P, NEXT>(col, n, a.rows, go, mo, so, mu, sig, nx, a.first_mask);
 		return;
 	}
 #pragma unroll
 	for (int u = 0; u < R; ++u)
 		if (threadIdx.x + u * BLOCK < n) {
-			v_apply<P, NEXT>(rec[u], xv[u], (row[u] & ROW_FIRST) != 0, go, mo, so, mu, sig, nx);
+			v_apply<P, NEXT>(rec[u], xv[u], (row[u] & a.first_mask) != 0, go, mo, so, mu, sig, nx);
 			store_rec(a.rows, row[u] & ROW_MASK, rec[u]);
 		}
 	for (uint32_t i = threadIdx.x + R * BLOCK; i < n; i += BLOCK) {
 		const uint2 ent = col[i];
 		Rec v;
 		load_rec(a.rows, ent.x & ROW_MASK, v);
-		v_apply<P, NEXT>(v, ent_x(ent), (ent.x & ROW_FIRST) != 0, go, mo, so, mu, sig, nx);
+		v_apply<P, NEXT>(v, ent_x(ent), (ent.x & a.first_mask) != 0, go, mo, so, mu, sig, nx);
 		store_rec(a.rows, ent.x & ROW_MASK, v);
 	}
 }
@@ -140,14 +140,14 @@ __global__ __launch_bounds__(BLOCK) void k_v_level_correct(LevelArgs a)
 	if (threadIdx.x == 0) a.ms[(size_t)j * a.ms_stride] = make_double2(mu, sig);
 	if (!go && !NEXT) return;
 	if (a.dup[j]) {
-		if (threadIdx.x == 0) v_apply_serial<P, NEXT>(col, n, a.rows, go, msj.x, msj.y, mu, sig, nx);
+		if (threadIdx.x == 0) v_apply_serial<P, NEXT>(col, n, a.rows, go, msj.x, msj.y, mu, sig, nx, a.first_mask);
 		return;
 	}
 	for (uint32_t i = threadIdx.x; i < n; i += BLOCK) {
 		const uint2 ent = col[i];
 		Rec v;
 		load_rec(a.rows, ent.x & ROW_MASK, v);
-		v_apply<P, NEXT>(v, ent_x(ent), (ent.x & ROW_FIRST) != 0, go, msj.x, msj.y, mu, sig, nx);
+		v_apply<P, NEXT>(v, ent_x(ent), (ent.x & a.first_mask) != 0, go, msj.x, msj.y, mu, sig, nx);
 		store_rec(a.rows, ent.x & ROW_MASK, v);
 	}
 }
@@ -157,13 +157,13 @@ __global__ __launch_bounds__(BLOCK) void k_v_level_correct(LevelArgs a)
 // q-cache of factor 0 into slot 0 (add_main_q(train, 0), fm_learn_vb.h:354-381).
 template <bool NEXT>
 DEVI void w_apply_serial(const uint2 *col, uint32_t n, RowRec *rows, bool go, double mo, double so, double mu,
-                         double sig, double2 nx)
+                         double sig, double2 nx, uint32_t fm)
 {
 	for (uint32_t i = 0; i < n; ++i) {
 		const uint2 ent = col[i];
 		Rec v;
 		load_rec(rows, ent.x & ROW_MASK, v);
-		w_apply<NEXT>(v, ent_x(ent), (ent.x & ROW_FIRST) != 0, go, mo, so, mu, sig, nx);
+		w_apply<NEXT>(v, ent_x(ent), (ent.x & fm) != 0, go, mo, so, mu, sig, nx);
 		store_rec(rows, ent.x & ROW_MASK, v);
 	}
 }
@@ -208,20 +208,20 @@ __global__ __launch_bounds__(BLOCK) void k_w_level_fused(LevelArgs a)
 	if (!go && !NEXT) return;
 	if (a.dup[j]) {
 		__syncthreads();
-		if (threadIdx.x == 0) w_apply_serial<NEXT>(col, n, a.rows, go, mo, so, mu, sig, nx);
+		if (threadIdx.x == 0) w_apply_serial<NEXT>(col, n, a.rows, go, mo, so, mu, sig, nx, a.first_mask);
 		return;
 	}
 #pragma unroll
 	for (int u = 0; u < R; ++u)
 		if (threadIdx.x + u * BLOCK < n) {
-			w_apply<NEXT>(rec[u], xv[u], (row[u] & ROW_FIRST) != 0, go, mo, so, mu, sig, nx);
+			w_apply<NEXT>(rec[u], xv[u], (row[u] & a.first_mask) != 0, go, mo, so, mu, sig, nx);
 			store_rec(a.rows, row[u] & ROW_MASK, rec[u]);
 		}
 	for (uint32_t i = threadIdx.x + R * BLOCK; i < n; i += BLOCK) {
 		const uint2 ent = col[i];
 		Rec v;
 		load_rec(a.rows, ent.x & ROW_MASK, v);
-		w_apply<NEXT>(v, ent_x(ent), (ent.x & ROW_FIRST) != 0, go, mo, so, mu, sig, nx);
+		w_apply<NEXT>(v, ent_x(ent), (ent.x & a.first_mask) != 0, go, mo, so, mu, sig, nx);
 		store_rec(a.rows, ent.x & ROW_MASK, v);
 	}
 }
@@ -261,14 +261,14 @@ __global__ __launch_bounds__(BLOCK) void k_w_level_correct(LevelArgs a)
 	if (threadIdx.x == 0) a.ms[(size_t)j * a.ms_stride] = make_double2(mu, sig);
 	if (!go && !NEXT) return;
 	if (a.dup[j]) {
-		if (threadIdx.x == 0) w_apply_serial<NEXT>(col, n, a.rows, go, msj.x, msj.y, mu, sig, nx);
+		if (threadIdx.x == 0) w_apply_serial<NEXT>(col, n, a.rows, go, msj.x, msj.y, mu, sig, nx, a.first_mask);
 		return;
 	}
 	for (uint32_t i = threadIdx.x; i < n; i += BLOCK) {
 		const uint2 ent = col[i];
 		Rec v;
 		load_rec(a.rows, ent.x & ROW_MASK, v);
-		w_apply<NEXT>(v, ent_x(ent), (ent.x & ROW_FIRST) != 0, go, msj.x, msj.y, mu, sig, nx);
+		w_apply<NEXT>(v, ent_x(ent), (ent.x & a.first_mask) != 0, go, msj.x, msj.y, mu, sig, nx);
 		store_rec(a.rows, ent.x & ROW_MASK, v);
 	}
 }
@@ -804,6 +804,61 @@ __global__ void k_unpack(const double2 *in, double *a, double *b, uint32_t rows,
 	b[f * D + j] = in[i].y;
 }
 
+// ------------------------------------------------------------------------------------
+// feature-sharded passes (the north star's feature-column partition; Jacobi across shards):
+// every shard holds all rows and starts a pass from the same row caches; afterwards the
+// shards' changes of e and t and their partial q-caches of the next factor are summed.
+// base[r] = e, base[n + r] = t at the start of a pass; the next factor's q-cache slot zeroed
+__global__ void k_fs_begin(RowRec *rows, uint32_t n, double *base, int next_slot)
+{
+	const uint32_t r = blockIdx.x * 256u + threadIdx.x;
+	if (r >= n) return;
+	RowRec &x = rows[r];
+	base[r] = x.e;
+	base[(size_t)n + r] = x.t;
+	if (next_slot == 0) { x.q = 0.0; x.tq = 0.0; x.tz = 0.0; }
+	else if (next_slot == 1) { x.q1 = 0.0; x.tq1 = 0.0; x.tz1 = 0.0; }
+}
+
+// buf = [e - e0 | t - t0 | q | tq | tz of the next slot], written (acc = 0) or added to
+__global__ void k_fs_pack(const RowRec *rows, uint32_t n, const double *base, double *buf, int next_slot, int acc)
+{
+	const uint32_t r = blockIdx.x * 256u + threadIdx.x;
+	if (r >= n) return;
+	const RowRec &x = rows[r];
+	double v[5] = {x.e - base[r], x.t - base[(size_t)n + r], 0.0, 0.0, 0.0};
+	if (next_slot == 0) { v[2] = x.q; v[3] = x.tq; v[4] = x.tz; }
+	else if (next_slot == 1) { v[2] = x.q1; v[3] = x.tq1; v[4] = x.tz1; }
+	const int m = next_slot < 0 ? 2 : 5;
+	for (int i = 0; i < m; ++i) {
+		double *d = buf + (size_t)i * n + r;
+		*d = acc ? *d + v[i] : v[i];
+	}
+}
+
+__global__ void k_fs_unpack(RowRec *rows, uint32_t n, const double *base, const double *buf, int next_slot)
+{
+	const uint32_t r = blockIdx.x * 256u + threadIdx.x;
+	if (r >= n) return;
+	RowRec &x = rows[r];
+	x.e = base[r] + buf[r];
+	x.t = base[(size_t)n + r] + buf[(size_t)n + r];
+	const double q = buf[2 * (size_t)n + r], tq = buf[3 * (size_t)n + r], tz = buf[4 * (size_t)n + r];
+	if (next_slot == 0) { x.q = q; x.tq = tq; x.tz = tz; }
+	else if (next_slot == 1) { x.q1 = q; x.tq1 = tq; x.tz1 = tz; }
+}
+
+// to_buf: pbuf[j] = ms[j*stride] for the listed features; else ms[j*stride] = pbuf[j]
+__global__ void k_fs_params(double2 *ms, uint32_t stride, const uint32_t *feats, uint32_t nfeat, double2 *pbuf,
+                            int to_buf)
+{
+	const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+	if (i >= nfeat) return;
+	const uint32_t j = feats[i];
+	if (to_buf) pbuf[j] = ms[(size_t)j * stride];
+	else ms[(size_t)j * stride] = pbuf[j];
+}
+
 inline unsigned grid_for(uint64_t n, unsigned block = 256) { return (unsigned)((n + block - 1) / block); }
 
 }  // namespace
@@ -983,6 +1038,36 @@ hipError_t mark_dups(const uint64_t *row_ptr, const uint2 *csr, uint32_t n, uint
 {
 	if (n == 0) return hipSuccess;
 	k_mark_dups<<<grid_for(n), 256, 0, s>>>(row_ptr, csr, n, dup);
+	return hipGetLastError();
+}
+
+hipError_t fs_begin(RowRec *rows, uint32_t n, double *base, int next_slot, hipStream_t s)
+{
+	if (n == 0) return hipSuccess;
+	k_fs_begin<<<grid_for(n), 256, 0, s>>>(rows, n, base, next_slot);
+	return hipGetLastError();
+}
+
+hipError_t fs_pack(const RowRec *rows, uint32_t n, const double *base, double *buf, int next_slot, int acc,
+                   hipStream_t s)
+{
+	if (n == 0) return hipSuccess;
+	k_fs_pack<<<grid_for(n), 256, 0, s>>>(rows, n, base, buf, next_slot, acc);
+	return hipGetLastError();
+}
+
+hipError_t fs_unpack(RowRec *rows, uint32_t n, const double *base, const double *buf, int next_slot, hipStream_t s)
+{
+	if (n == 0) return hipSuccess;
+	k_fs_unpack<<<grid_for(n), 256, 0, s>>>(rows, n, base, buf, next_slot);
+	return hipGetLastError();
+}
+
+hipError_t fs_params(double2 *ms, uint32_t stride, const uint32_t *feats, uint32_t nfeat, double2 *pbuf, int to_buf,
+                     hipStream_t s)
+{
+	if (nfeat == 0) return hipSuccess;
+	k_fs_params<<<grid_for(nfeat), 256, 0, s>>>(ms, stride, feats, nfeat, pbuf, to_buf);
 	return hipGetLastError();
 }
 

@@ -306,11 +306,11 @@ void mc_sweep(vbfm_ctx *c, bool is_w, int f)
 			a.src = c->rows;
 			a.dst = c->rows_alt;
 			a.first_level = l == 0;
-			if (!c->comm && !c->force_split) {
+			if (!c->row_comm() && !c->force_split) {
 				HIPCHK(vbk::mc_lord_level(a, 0, is_w, c->s));
 			} else {
 				HIPCHK(vbk::mc_lord_level(a, 1, is_w, c->s));
-				if (c->comm)
+				if (c->row_comm())
 					NCCLCHK(ncclAllReduce(c->stats, c->stats, 2 * (size_t)a.nfeat, ncclDouble, ncclSum, c->comm, c->s));
 				HIPCHK(vbk::mc_lord_level(a, 2, is_w, c->s));
 			}
@@ -318,11 +318,11 @@ void mc_sweep(vbfm_ctx *c, bool is_w, int f)
 			prof_end(c, p);
 			continue;
 		}
-		if (!c->comm && !c->force_split) {
+		if (!c->row_comm() && !c->force_split) {
 			HIPCHK(is_w ? vbk::mc_w_level(a, 0, c->s) : vbk::mc_v_level(a, 0, c->s));
 		} else {   // row-sharded: statistics of this shard, summed over shards, identical draws
 			HIPCHK(is_w ? vbk::mc_w_level(a, 1, c->s) : vbk::mc_v_level(a, 1, c->s));
-			if (c->comm)
+			if (c->row_comm())
 				NCCLCHK(ncclAllReduce(c->stats, c->stats, 2 * (size_t)a.nfeat, ncclDouble, ncclSum, c->comm, c->s));
 			HIPCHK(is_w ? vbk::mc_w_level(a, 2, c->s) : vbk::mc_v_level(a, 2, c->s));
 		}
@@ -410,6 +410,8 @@ int vbfm_mcmc_init(vbfm_ctx *c, const vbfm_mcmc_config *cfg)
 	if (!c || !cfg) return fail(c, "vbfm_mcmc_init: null argument");
 	return guarded(c, [&] {
 		if (cfg->rng != VBFM_RNG_REFERENCE && cfg->rng != VBFM_RNG_DEVICE) throw std::string("unknown rng mode");
+		if (c->shard_mode == VBFM_SHARD_FEATURES)
+			throw std::string("feature shards are implemented for the VB learner only");
 		mc_free(c);
 		c->mc = new McState();
 		McState &m = *c->mc;

@@ -119,7 +119,7 @@ EXPORTS = ["vbfm_abi_version", "vbfm_last_error", "vbfm_create", "vbfm_destroy",
            "vbfm_set_params", "vbfm_get_params", "vbfm_init_params_device", "vbfm_init_caches", "vbfm_iterate", "vbfm_get_test_pred",
            "vbfm_step_w0", "vbfm_step_w", "vbfm_step_qcache", "vbfm_step_v", "vbfm_step_hyper",
            "vbfm_free_energy", "vbfm_get_rows", "vbfm_get_test_e", "vbfm_factor_sweep", "vbfm_set_profiling",
-           "vbfm_set_layout", "vbfm_get_layout",
+           "vbfm_set_layout", "vbfm_get_layout", "vbfm_set_shard_mode",
            "vbfm_comm_unique_id", "vbfm_comm_init", "vbfm_load_data", "vbfm_free_host_data",
            "vbfm_init_params_host", "vbfm_mcmc_init", "vbfm_mcmc_set_params", "vbfm_mcmc_get_params",
            "vbfm_mcmc_init_caches", "vbfm_mcmc_iterate", "vbfm_mcmc_get_test_pred", "vbfm_mcmc_factor_sweep"]
@@ -163,6 +163,7 @@ def lib():
         L.vbfm_factor_sweep.argtypes = [V, P_f64]
         L.vbfm_set_profiling.argtypes = [V, C.c_int32]
         L.vbfm_set_layout.argtypes = [V, C.c_int32]
+        L.vbfm_set_shard_mode.argtypes = [V, C.c_int32, C.c_int32]
         L.vbfm_get_layout.argtypes = [V, C.POINTER(C.c_int32)]
         L.vbfm_comm_unique_id.argtypes = [C.POINTER(C.c_uint8)]
         L.vbfm_comm_init.argtypes = [V, C.c_int32, C.c_int32, C.POINTER(C.c_uint8)]
@@ -281,6 +282,12 @@ class FMLearnVB:
         _check(lib().vbfm_set_layout(self._ctx, LAYOUTS[layout]), self._ctx)
         self.num_iter_done = 0
         self.fm_v = self.fm_w = None
+
+    def set_shard_mode(self, mode, num_shards=0):
+        """"rows" (exact row shards, default) or "features" (the north star's column
+        partition, Jacobi across shards; num_shards > 1 without a communicator runs the
+        shards one after another in this process). Before set_data / synth."""
+        _check(lib().vbfm_set_shard_mode(self._ctx, {"rows": 0, "features": 1}[mode], int(num_shards)), self._ctx)
 
     def layout(self):
         """Row layout in use for the sweeps: "column" (row order, gather) or "level"

@@ -83,6 +83,8 @@ def lib():
         L.or_vb_update_all_sharded.argtypes = [C.POINTER(OrVB), C.POINTER(OrData), C.c_uint32,
                                                C.c_uint32, ALLREDUCE_FN, C.c_void_p]
         L.or_vb_destroy.argtypes = [C.POINTER(OrVB)]
+        L.or_vb_update_all_fsharded.argtypes = [C.POINTER(OrVB), C.POINTER(OrData), C.c_int,
+                                                C.POINTER(C.c_int32)]
         L.or_als_create.argtypes = [C.POINTER(OrALS), C.c_int, C.c_int, C.c_int, C.c_uint32, P_u32]
         L.or_als_init_params.argtypes = [C.POINTER(OrALS), C.c_uint32, C.c_double]
         L.or_als_attach.argtypes = [C.POINTER(OrALS), C.POINTER(OrData), C.POINTER(OrData)]
@@ -169,6 +171,12 @@ class VB:
 
     def step(self, name, *args):
         return getattr(lib(), "or_vb_" + name)(C.byref(self.s), C.byref(self.train.d), *args)
+
+    def update_all_fsharded(self, shard):
+        """libvbfm's feature-sharded update_all (shard[j] = owning shard of train feature j)."""
+        sh = np.ascontiguousarray(shard, dtype=np.int32)
+        lib().or_vb_update_all_fsharded(C.byref(self.s), C.byref(self.train.d), int(sh.max()) + 1 if sh.size else 1,
+                                        sh.ctypes.data_as(C.POINTER(C.c_int32)))
 
     def iterate(self):
         r, m, t = C.c_double(), C.c_double(), C.c_double()

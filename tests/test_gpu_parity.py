@@ -333,3 +333,34 @@ def test_wave_prediction_many_factors(k, monkeypatch):
     close(rg["e"], ro["e"], 1e-12)
     close(rg["t"], ro["t"], 1e-12)
     np.testing.assert_allclose(g.test_e(), oc.arr(o.s.e_test, o.s.n_test), rtol=1e-12, atol=1e-12)
+
+
+@pytest.mark.parametrize("P", [1, 2, 3])
+def test_feature_shards_vs_oracle(P):
+    """VBFM_SHARD_FEATURES (the north star's column partition) with P shards run one after
+    another in this process -- the kernels, the shard chunks of every level, the zeroed
+    q-cache partials and the merge of the multi-rank mode, without the all-reduce -- against
+    the oracle's restatement of the same Jacobi-across-shards sweep, 2 iterations."""
+    from shards import feature_shards
+    n, F, S, k = 8000, 5, 60, 3
+    rp, f, v, y = synth.generate(n, F, S, 41, 1)
+    rpt, ft, vt, yt = synth.generate(500, F, S, 42, 1)
+    D = F * S + 1
+    g = vbfm.FMLearnVB(1, 1, k, D, min_target=float(y.min()), max_target=float(y.max()))
+    g.set_shard_mode("features", P)
+    g.init(5, 0.1)
+    g.set_data(vbfm.DataSubset.from_csr(rp, f, v, y, F * S), vbfm.DataSubset.from_csr(rpt, ft, vt, yt, F * S))
+    assert g.layout() == "column"
+    o = oc.VB(1, 1, k, D)
+    o.init_params(5, 0.1)
+    o.attach(oc.Data(csr=(n, rp, f, v, y)), oc.Data(csr=(500, rpt, ft, vt, yt)))
+    shard = feature_shards(rp, f, F * S, P)
+    g.init_caches(); o.init_caches()
+    for _ in range(2):
+        st = g.iterate()
+        o.update_all_fsharded(shard)
+        close([st.free_energy], [o.s.last_free_energy])
+        close([st.alpha], [o.s.alpha])
+    close(g.rows()["e"], o.rows()["e"])
+    close(g.get_params()["mu_v"], o.params()["mu_v"])
+    close(g.get_params()["mu_w"], o.params()["mu_w"])

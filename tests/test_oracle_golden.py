@@ -213,3 +213,43 @@ def test_mcmc_als_trace_bit_exact(case, synth_files, sa_split):
     for key in ("w_mu", "w_lambda", "v_mu", "v_lambda"):
         if "final_" + key in a:
             np.testing.assert_array_equal(p[key], a["final_" + key])
+
+
+def test_feature_sharded_oracle_one_shard_is_update_all():
+    """The feature-sharded restatement with one shard is update_all (up to the e0 + (e - e0)
+    rounding of the merge); with two shards it is a different (Jacobi) sweep."""
+    import synth
+    from shards import feature_shards
+    n, F, S, k = 3000, 5, 40, 3
+    rp, f, v, y = synth.generate(n, F, S, 12, 1)
+    rpt, ft, vt, yt = synth.generate(300, F, S, 13, 1)
+    res = {}
+    for P in (0, 1, 2):
+        o = oc.VB(1, 1, k, F * S + 1)
+        o.init_params(4, 0.1)
+        o.attach(oc.Data(csr=(n, rp, f, v, y)), oc.Data(csr=(300, rpt, ft, vt, yt)))
+        o.init_caches()
+        for _ in range(2):
+            if P == 0:
+                o.step("update_all")
+            else:
+                o.update_all_fsharded(feature_shards(rp, f, F * S, P))
+        res[P] = (o.rows()["e"].copy(), o.params()["mu_v"].copy(), o.s.last_free_energy)
+    e0, v0, fe0 = res[0]
+    e1, v1, fe1 = res[1]
+    assert np.max(np.abs(e1 - e0)) <= 1e-12 * np.max(np.abs(e0))
+    assert np.max(np.abs(v1 - v0)) <= 1e-12 * np.max(np.abs(v0))
+    assert abs(fe1 - fe0) <= 1e-12 * abs(fe0)
+    e2, v2, fe2 = res[2]
+    assert np.all(np.isfinite(e2)) and np.isfinite(fe2)
+    assert np.max(np.abs(v2 - v0)) > 1e-9   # Jacobi across shards: not the sequential sweep
+
+
+def test_feature_shards_match_level_schedule():
+    """tests/shards.py levels == the field index on field-structured data (one level per field)."""
+    import synth
+    from shards import levels
+    rp, f, v, y = synth.generate(2000, 6, 30, 3, 0)
+    lv = levels(rp, f, 180)
+    present = np.bincount(f, minlength=180) > 0
+    np.testing.assert_array_equal(lv[present], (np.arange(180) // 30 + 1)[present])
