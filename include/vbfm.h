@@ -263,8 +263,14 @@ typedef struct {
 	uint64_t *col_ptr; vbfm_entry *col_ent;   /* transposed copy     (Data.h:457-509) */
 } vbfm_host_data;
 /* Data::load (Data.h:106-283): libfm text, or the binary triple <name>.x/.xt/.y
- * (fmatrix.h:46-52, matrix.h:296-312) when those files exist. */
+ * (fmatrix.h:46-52, matrix.h:296-312) when those files exist. Text is parsed in parallel
+ * (VBFM_LOADER_THREADS, default min(cores, 16)) with the reference's sscanf semantics; the
+ * transpose (Data::create_data_t) is a parallel stable counting sort. */
 int vbfm_load_data(const char *filename, vbfm_host_data *out);
+/* The reference's binary triple of a loaded data set: <base>.x (CSR rows in file order),
+ * <base>.xt (the transposed copy) and <base>.y, as tools/convert + tools/transpose write them
+ * (fmatrix.h:67-86, matrix.h:280-293). vbfm_load_data(<base>) then reads it back. */
+int vbfm_save_data(const char *basename, const vbfm_host_data *d);
 void vbfm_free_host_data(vbfm_host_data *d);
 /* srand(seed) then the reference's draw order: fm.v (k*D) ~ N(0, init_stdev)
  * (fm_model.h:97), fm.w (D) (libfm.cpp:307), mu_w_dash (D), mu_v_dash (k*D) as 0.1*N(0,1)

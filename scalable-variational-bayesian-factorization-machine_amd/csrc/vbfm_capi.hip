@@ -54,24 +54,6 @@ void free_data(DevData &d)
 	d = DevData();
 }
 
-// host CSC -> host CSR sorted by feature: the order the reference's column loops visit a row
-void csc_to_csr(const vbfm_csc *in, std::vector<uint64_t> &row_ptr, std::vector<uint2> &csr)
-{
-	row_ptr.assign((size_t)in->num_rows + 1, 0);
-	for (uint64_t p = 0; p < in->nnz; p++) row_ptr[(size_t)in->col_ent[p].id + 1]++;
-	for (uint32_t r = 0; r < in->num_rows; r++) row_ptr[r + 1] += row_ptr[r];
-	std::vector<uint64_t> pos(row_ptr.begin(), row_ptr.end() - 1);
-	csr.resize(in->nnz);
-	for (uint32_t j = 0; j < in->num_feature; j++)
-		for (uint64_t p = in->col_ptr[j]; p < in->col_ptr[j + 1]; p++) {
-			const vbfm_entry &e = in->col_ent[p];
-			uint2 v;
-			v.x = j;
-			memcpy(&v.y, &e.value, 4);
-			csr[pos[e.id]++] = v;
-		}
-}
-
 void check_csc(const vbfm_csc *in)
 {
 	if (!in) throw std::string("null data set");
@@ -96,20 +78,14 @@ void upload(vbfm_ctx *c, DevData &d, const vbfm_csc *in, uint32_t nf_pad)
 	std::vector<uint64_t> cp((size_t)d.nf + 1, in->nnz);
 	if (in->num_feature) memcpy(cp.data(), in->col_ptr, ((size_t)in->num_feature + 1) * sizeof(uint64_t));
 	else cp[0] = 0;
-	std::vector<uint64_t> row_ptr;
-	std::vector<uint2> csr;
-	csc_to_csr(in, row_ptr, csr);
 	d.col_ptr = dalloc<uint64_t>(cp.size());
 	d.csc = dalloc<uint2>(d.nnz);
-	d.row_ptr = dalloc<uint64_t>(row_ptr.size());
+	d.row_ptr = dalloc<uint64_t>((size_t)d.n + 1);
 	d.csr = dalloc<uint2>(d.nnz);
 	d.target = dalloc<float>(d.n);
 	HIPCHK(hipMemcpyAsync(d.col_ptr, cp.data(), cp.size() * 8, hipMemcpyHostToDevice, c->s));
-	if (d.nnz) {
-		HIPCHK(hipMemcpyAsync(d.csc, in->col_ent, d.nnz * 8, hipMemcpyHostToDevice, c->s));
-		HIPCHK(hipMemcpyAsync(d.csr, csr.data(), d.nnz * 8, hipMemcpyHostToDevice, c->s));
-	}
-	HIPCHK(hipMemcpyAsync(d.row_ptr, row_ptr.data(), row_ptr.size() * 8, hipMemcpyHostToDevice, c->s));
+	if (d.nnz) HIPCHK(hipMemcpyAsync(d.csc, in->col_ent, d.nnz * 8, hipMemcpyHostToDevice, c->s));
+	HIPCHK(vbk::build_csr(d.col_ptr, d.csc, d.nf_local, d.n, d.nnz, d.row_ptr, d.csr, c->s));
 	if (d.n) HIPCHK(hipMemcpyAsync(d.target, in->target, d.n * 4, hipMemcpyHostToDevice, c->s));
 	float mn = 3.40282347e+38f, mx = -3.40282347e+38f;
 	for (uint32_t i = 0; i < d.n; i++) { mn = std::min(in->target[i], mn); mx = std::max(in->target[i], mx); }

@@ -13,7 +13,9 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <algorithm>
 #include <string>
+#include <thread>
 #include <vector>
 
 namespace {
@@ -28,92 +30,233 @@ bool file_exists(const std::string &f)
 	return true;
 }
 
-// one text line: "<target> <id>:<value> ..." (Data.h:196-215 / 247-272)
-int parse_line(const char *line, float *target, std::vector<vbfm_entry> &ents, int *maxf)
+// ---- libfm text (Data.h:185-278) -----------------------------------------------------------
+// The reference parses each line with sscanf("%f%n") and then sscanf("%d:%f%n") pairs. This
+// parser keeps those semantics byte for byte without calling sscanf per line: strtol base 10
+// for %d (what glibc's scanf converts with), a literal ':', the whitespace sscanf skips
+// before a conversion (space, \t, \v, \f, \r; a line never holds \n), and the reference's
+// checks: leading spaces / tabs, empty and '#' lines skipped, after the pairs only spaces /
+// tabs and an optional '#' comment. Lines end at '\n' or at the buffer's NUL.
+inline bool scan_ws(char c) { return c == ' ' || c == '\t' || c == '\v' || c == '\f' || c == '\r'; }
+
+// %f: glibc's scanf and strtof agree on plain decimal numbers ([+-]digits[.digits][e[+-]digits])
+// but not on malformed or exotic ones ("1e", "0x", "infin", "nan(1)"): a token that strtof
+// does not consume whole, or that holds other characters than [0-9.eE+-], is converted by
+// sscanf itself from a NUL-terminated copy. Every character %f can consume is in
+// [0-9A-Za-z.+-()], so the copy holds all sscanf could read. Returns the end, or nullptr.
+const char *scan_float(const char *q, const char *eol, float *v)
 {
-	const char *p = line;
-	while (*p == ' ' || *p == '\t') p++;
-	if (*p == 0 || *p == '#') return 0;
-	float v;
-	int nchar, fid;
-	if (sscanf(p, "%f%n", &v, &nchar) < 1) return -1;
-	p += nchar;
-	*target = v;
-	while (sscanf(p, "%d:%f%n", &fid, &v, &nchar) >= 2) {
-		p += nchar;
-		if (fid < 0) return -2;
-		if (fid > *maxf) *maxf = fid;
-		ents.push_back(vbfm_entry{(uint32_t)fid, v});
+	const char *t = q;
+	bool plain = true;
+	while (t < eol) {
+		const char c = *t;
+		const bool dec = (c >= '0' && c <= '9') || c == '.' || c == 'e' || c == 'E' || c == '+' || c == '-';
+		if (!dec && !((c >= 'a' && c <= 'z') || (c >= 'A' && c <= 'Z') || c == '(' || c == ')')) break;
+		plain &= dec;
+		t++;
 	}
-	while (*p != 0 && (*p == ' ' || *p == '\t')) p++;
-	if (*p != 0 && *p != '#') return -1;
+	if (t == q) return nullptr;
+	if (plain) {
+		char *end = nullptr;
+		const float x = strtof(q, &end);
+		if (end == t) { *v = x; return end; }
+	}
+	char tok[512];
+	const size_t len = std::min<size_t>(t - q, sizeof(tok) - 1);
+	memcpy(tok, q, len);
+	tok[len] = 0;
+	int n = 0;
+	if (sscanf(tok, "%f%n", v, &n) < 1) return nullptr;
+	return q + n;
+}
+
+struct LineError { size_t pos = SIZE_MAX; std::string msg; };
+
+// 1: a row, 0: skipped line, -1: parse error (*at = the offending character)
+int parse_line(const char *p, const char *eol, float *target, std::vector<vbfm_entry> &ents, int *maxf, char *at)
+{
+	while (p < eol && (*p == ' ' || *p == '\t')) p++;           // Data.h:196
+	if (p == eol || *p == '#') return 0;                        // :197
+	const char *q = p;
+	while (q < eol && scan_ws(*q)) q++;
+	float y = 0.f;
+	const char *end = scan_float(q, eol, &y);
+	if (!end) { *at = *p; return -1; }                          // sscanf("%f") < 1
+	*target = y;
+	p = end;
+	for (;;) {                                                  // sscanf("%d:%f%n") >= 2
+		q = p;
+		while (q < eol && scan_ws(*q)) q++;
+		if (q == eol) break;
+		char *e1 = nullptr;
+		const long fid = strtol(q, &e1, 10);
+		if (e1 == q || *e1 != ':') break;
+		const char *r = e1 + 1;
+		while (r < eol && scan_ws(*r)) r++;
+		float x = 0.f;
+		end = scan_float(r, eol, &x);
+		if (!end) break;
+		const int id = (int)fid;
+		if (id < 0) { *at = *q; return -1; }
+		if (id > *maxf) *maxf = id;
+		ents.push_back(vbfm_entry{(uint32_t)id, x});
+		p = end;
+	}
+	while (p < eol && (*p == ' ' || *p == '\t')) p++;           // :207
+	if (p < eol && *p != '#') { *at = *p; return -1; }          // :208-210
 	return 1;
 }
 
 template <class T> T *xalloc(size_t n) { return (T *)malloc((n ? n : 1) * sizeof(T)); }
 
-// Data::create_data_t (Data.h:457-509): stable counting transpose, ascending rows per column
-void transpose(vbfm_host_data *d)
+int num_threads()
 {
-	const uint32_t nf = d->num_feature;
-	d->col_ptr = xalloc<uint64_t>((size_t)nf + 1);
-	d->col_ent = xalloc<vbfm_entry>(d->nnz);
-	std::vector<uint64_t> cnt((size_t)nf + 1, 0);
-	for (uint64_t j = 0; j < d->nnz; j++) cnt[d->row_ent[j].id]++;
-	d->col_ptr[0] = 0;
-	for (uint32_t i = 0; i < nf; i++) d->col_ptr[i + 1] = d->col_ptr[i] + cnt[i];
-	for (uint32_t i = 0; i < nf; i++) cnt[i] = d->col_ptr[i];
-	for (uint32_t r = 0; r < d->num_rows; r++)
-		for (uint64_t j = d->row_ptr[r]; j < d->row_ptr[r + 1]; j++) {
-			const vbfm_entry &e = d->row_ent[j];
-			d->col_ent[cnt[e.id]++] = vbfm_entry{r, e.value};
-		}
+	const char *env = getenv("VBFM_LOADER_THREADS");
+	if (env && atoi(env) > 0) return atoi(env);
+	const unsigned hw = std::thread::hardware_concurrency();
+	return (int)std::max(1u, std::min(hw ? hw : 1u, 16u));      // the GPU box's CPU share is 16
 }
 
+// run fn(t) on T threads (t = 0 on the caller)
+template <class F> void parallel(int T, F &&fn)
+{
+	std::vector<std::thread> th;
+	for (int t = 1; t < T; t++) th.emplace_back(fn, t);
+	fn(0);
+	for (auto &x : th) x.join();
+}
+
+// Data::create_data_t (Data.h:457-509): stable counting transpose, ascending rows per column.
+// Parallel over row ranges: per-range column counts give every range its own slot in every
+// column, so each range scatters its rows in order and the result is the sequential one.
+void transpose(vbfm_host_data *d)
+{
+	const uint32_t nf = d->num_feature, n = d->num_rows;
+	d->col_ptr = xalloc<uint64_t>((size_t)nf + 1);
+	d->col_ent = xalloc<vbfm_entry>(d->nnz);
+	int T = num_threads();
+	if ((uint64_t)T * nf > (uint64_t)1 << 31 || d->nnz < ((uint64_t)1 << 20)) T = 1;   // count-table memory / tiny sets
+	std::vector<uint32_t> lo(T + 1);
+	for (int t = 0; t <= T; t++) lo[t] = (uint32_t)((uint64_t)n * t / T);
+	std::vector<uint64_t> cnt((size_t)T * nf, 0);
+	parallel(T, [&](int t) {
+		uint64_t *c = cnt.data() + (size_t)t * nf;
+		for (uint64_t j = d->row_ptr[lo[t]]; j < d->row_ptr[lo[t + 1]]; j++) c[d->row_ent[j].id]++;
+	});
+	uint64_t acc = 0;
+	for (uint32_t i = 0; i < nf; i++) {
+		d->col_ptr[i] = acc;
+		for (int t = 0; t < T; t++) {
+			const uint64_t v = cnt[(size_t)t * nf + i];
+			cnt[(size_t)t * nf + i] = acc;
+			acc += v;
+		}
+	}
+	d->col_ptr[nf] = acc;
+	parallel(T, [&](int t) {
+		uint64_t *c = cnt.data() + (size_t)t * nf;
+		for (uint32_t r = lo[t]; r < lo[t + 1]; r++)
+			for (uint64_t j = d->row_ptr[r]; j < d->row_ptr[r + 1]; j++) {
+				const vbfm_entry &e = d->row_ent[j];
+				d->col_ent[c[e.id]++] = vbfm_entry{r, e.value};
+			}
+	});
+}
+
+// the file in chunks of whole lines, parsed in parallel, concatenated in file order
 int load_text(const char *fn, vbfm_host_data *out)
 {
-	FILE *fp = fopen(fn, "r");
+	FILE *fp = fopen(fn, "rb");
 	if (!fp) { g_host_err = std::string("unable to open ") + fn; return -1; }
-	std::vector<vbfm_entry> ents;
-	std::vector<float> target;
-	std::vector<uint64_t> row_ptr(1, 0);
+	fseeko(fp, 0, SEEK_END);
+	const size_t size = (size_t)ftello(fp);
+	fseeko(fp, 0, SEEK_SET);
+	char *buf = xalloc<char>(size + 1);
+	if (size && fread(buf, 1, size, fp) != size) {
+		free(buf); fclose(fp);
+		g_host_err = std::string("unable to read ") + fn;
+		return -1;
+	}
+	fclose(fp);
+	buf[size] = 0;
+	const int T = size < ((size_t)1 << 20) ? 1 : num_threads();
+	std::vector<size_t> cut(T + 1, size);
+	cut[0] = 0;
+	for (int t = 1; t < T; t++) {
+		size_t c = std::max(cut[t - 1], size * t / T);
+		while (c < size && c > 0 && buf[c - 1] != '\n') c++;
+		cut[t] = c;
+	}
+	struct Part {
+		std::vector<vbfm_entry> ents;
+		std::vector<float> target;
+		std::vector<uint32_t> len;
+		int maxf = -1;
+		bool has_feature = false;
+		float mn = 3.40282347e+38f, mx = -3.40282347e+38f;
+		LineError err;
+	};
+	std::vector<Part> part(T);
+	parallel(T, [&](int t) {
+		Part &P = part[t];
+		const char *p = buf + cut[t], *stop = buf + cut[t + 1];
+		while (p < stop) {
+			const char *eol = (const char *)memchr(p, '\n', stop - p);
+			if (!eol) eol = stop;
+			float y = 0.f;
+			char at = 0;
+			const size_t before = P.ents.size();
+			const int rc = parse_line(p, eol, &y, P.ents, &P.maxf, &at);
+			if (rc < 0) {
+				P.err.pos = p - buf;
+				P.err.msg = "cannot parse line \"" + std::string(p, eol) + "\" at character " + std::string(1, at);
+				return;
+			}
+			if (rc > 0) {
+				if (P.ents.size() > before) P.has_feature = true;
+				P.mn = std::min(y, P.mn);
+				P.mx = std::max(y, P.mx);
+				P.target.push_back(y);
+				P.len.push_back((uint32_t)(P.ents.size() - before));
+			}
+			p = eol + 1;
+		}
+	});
+	free(buf);
+	for (const Part &P : part)
+		if (P.err.pos != SIZE_MAX) { g_host_err = P.err.msg; return -1; }
+	memset(out, 0, sizeof(*out));
+	uint64_t nrows = 0, nnz = 0;
 	int maxf = -1;
 	bool has_feature = false;
 	float mn = 3.40282347e+38f, mx = -3.40282347e+38f;
-	char *line = nullptr;
-	size_t cap = 0;
-	ssize_t len;
-	while ((len = getline(&line, &cap, fp)) >= 0) {
-		if (len > 0 && line[len - 1] == '\n') line[len - 1] = 0;
-		float y;
-		const size_t before = ents.size();
-		const int rc = parse_line(line, &y, ents, &maxf);
-		if (rc < 0) {
-			g_host_err = std::string("cannot parse line \"") + line + "\"";
-			free(line); fclose(fp);
-			return -1;
-		}
-		if (rc == 0) continue;
-		if (ents.size() > before) has_feature = true;
-		mn = std::min(y, mn);
-		mx = std::max(y, mx);
-		target.push_back(y);
-		row_ptr.push_back(ents.size());
+	std::vector<uint64_t> row0(T + 1, 0), ent0(T + 1, 0);
+	for (int t = 0; t < T; t++) {
+		row0[t + 1] = row0[t] + part[t].target.size();
+		ent0[t + 1] = ent0[t] + part[t].ents.size();
+		maxf = std::max(maxf, part[t].maxf);
+		has_feature |= part[t].has_feature;
+		if (!part[t].target.empty()) { mn = std::min(part[t].mn, mn); mx = std::max(part[t].mx, mx); }
 	}
-	free(line);
-	fclose(fp);
-	memset(out, 0, sizeof(*out));
-	out->num_rows = (uint32_t)target.size();
-	out->nnz = ents.size();
+	nrows = row0[T]; nnz = ent0[T];
+	if (nrows > 0xFFFFFFFFull) { g_host_err = "too many rows"; return -1; }
+	out->num_rows = (uint32_t)nrows;
+	out->nnz = nnz;
 	out->num_feature = has_feature ? (uint32_t)maxf + 1 : 0;   // Data.h:220-222
 	out->min_target = mn;
 	out->max_target = mx;
-	out->target = xalloc<float>(target.size());
-	memcpy(out->target, target.data(), target.size() * sizeof(float));
-	out->row_ptr = xalloc<uint64_t>(row_ptr.size());
-	memcpy(out->row_ptr, row_ptr.data(), row_ptr.size() * sizeof(uint64_t));
-	out->row_ent = xalloc<vbfm_entry>(ents.size());
-	memcpy(out->row_ent, ents.data(), ents.size() * sizeof(vbfm_entry));
+	out->target = xalloc<float>(nrows);
+	out->row_ptr = xalloc<uint64_t>(nrows + 1);
+	out->row_ent = xalloc<vbfm_entry>(nnz);
+	out->row_ptr[0] = 0;
+	parallel(T, [&](int t) {
+		const Part &P = part[t];
+		memcpy(out->target + row0[t], P.target.data(), P.target.size() * sizeof(float));
+		memcpy(out->row_ent + ent0[t], P.ents.data(), P.ents.size() * sizeof(vbfm_entry));
+		uint64_t a = ent0[t];
+		for (size_t i = 0; i < P.len.size(); i++) { a += P.len[i]; out->row_ptr[row0[t] + i + 1] = a; }
+	});
+	part.clear();
 	transpose(out);
 	return 0;
 }
@@ -191,9 +334,41 @@ int load_binary(const std::string &base, const char *ex, const char *ext, const 
 	return 0;
 }
 
+// LargeSparseMatrix::saveToBinaryFile (fmatrix.h:67-86): header, then per row {uint32 size, entries}
+int write_sparse(const std::string &fn, uint32_t nrows, uint32_t ncols, uint64_t nnz, const uint64_t *ptr,
+                 const vbfm_entry *ent)
+{
+	FILE *fp = fopen(fn.c_str(), "wb");
+	if (!fp) { g_host_err = "could not open " + fn; return -1; }
+	sparse_header h{2u, (uint32_t)sizeof(float), nnz, nrows, ncols};
+	bool ok = fwrite(&h, sizeof(h), 1, fp) == 1;
+	for (uint32_t r = 0; ok && r < nrows; r++) {
+		const uint32_t sz = (uint32_t)(ptr[r + 1] - ptr[r]);
+		ok = fwrite(&sz, 4, 1, fp) == 1 && (sz == 0 || fwrite(ent + ptr[r], sizeof(vbfm_entry), sz, fp) == sz);
+	}
+	ok = (fclose(fp) == 0) && ok;
+	if (!ok) { g_host_err = "could not write " + fn; return -1; }
+	return 0;
+}
+
 }  // namespace
 
 extern "C" {
+
+int vbfm_save_data(const char *basename, const vbfm_host_data *d)
+{
+	if (!basename || !d) { g_host_err = "vbfm_save_data: null argument"; return -1; }
+	const std::string base(basename);
+	// DVector::saveToBinaryFile (matrix.h:280-293): uint32 version 1, size 4, n; floats
+	FILE *fp = fopen((base + ".y").c_str(), "wb");
+	if (!fp) { g_host_err = "could not open " + base + ".y"; return -1; }
+	const uint32_t hdr[3] = {1u, (uint32_t)sizeof(float), d->num_rows};
+	bool ok = fwrite(hdr, 4, 3, fp) == 3 && (d->num_rows == 0 || fwrite(d->target, 4, d->num_rows, fp) == d->num_rows);
+	ok = (fclose(fp) == 0) && ok;
+	if (!ok) { g_host_err = "could not write " + base + ".y"; return -1; }
+	if (write_sparse(base + ".x", d->num_rows, d->num_feature, d->nnz, d->row_ptr, d->row_ent)) return -1;
+	return write_sparse(base + ".xt", d->num_feature, d->num_rows, d->nnz, d->col_ptr, d->col_ent);
+}
 
 const char *vbfm_host_last_error(void) { return g_host_err.c_str(); }
 void vbfm_host_set_error(const char *msg) { g_host_err = msg ? msg : ""; }

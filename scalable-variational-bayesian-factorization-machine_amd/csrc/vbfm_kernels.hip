@@ -859,6 +859,28 @@ __global__ void k_fs_params(double2 *ms, uint32_t stride, const uint32_t *feats,
 	else ms[(size_t)j * stride] = pbuf[j];
 }
 
+// ------------------------------------------------------------------------------------
+// CSR of an uploaded data set from its CSC (Data.h keeps both; the device builds the row copy):
+// each entry's (row; feature, x), then a stable radix sort by row keeps every row's entries in
+// ascending feature order -- the order the reference's column loops visit a row in.
+__global__ __launch_bounds__(256) void k_csc_expand(const uint64_t *col_ptr, const uint2 *csc, uint32_t *rows,
+                                                    uint2 *fx)
+{
+	const uint32_t j = blockIdx.x;
+	const uint64_t b = col_ptr[j], e = col_ptr[j + 1];
+	for (uint64_t p = b + threadIdx.x; p < e; p += 256) {
+		const uint2 ent = csc[p];
+		rows[p] = ent.x & ROW_MASK;
+		fx[p] = make_uint2(j, ent.y);
+	}
+}
+
+__global__ void k_count_u32(const uint32_t *keys, uint64_t n, unsigned long long *counts)
+{
+	const uint64_t i = (uint64_t)blockIdx.x * 256u + threadIdx.x;
+	if (i < n) atomicAdd(&counts[keys[i]], 1ull);
+}
+
 inline unsigned grid_for(uint64_t n, unsigned block = 256) { return (unsigned)((n + block - 1) / block); }
 
 }  // namespace
@@ -1101,6 +1123,49 @@ hipError_t count_features(const uint2 *csr, uint64_t nnz, uint64_t *counts, hipS
 	if (nnz == 0) return hipSuccess;
 	k_count_features<<<grid_for(nnz), 256, 0, s>>>(csr, nnz, reinterpret_cast<unsigned long long *>(counts));
 	return hipGetLastError();
+}
+
+hipError_t build_csr(const uint64_t *col_ptr, const uint2 *csc, uint32_t nf, uint32_t n, uint64_t nnz,
+                     uint64_t *row_ptr, uint2 *csr, hipStream_t s)
+{
+	hipError_t err = hipSuccess;
+	uint32_t *ki = nullptr, *ko = nullptr;
+	uint2 *vi = nullptr;
+	unsigned long long *counts = nullptr;
+	void *tmp = nullptr;
+	size_t tb = 0, tb2 = 0;
+	int bits = 1;
+	while (bits < 32 && (1ull << bits) < n) bits++;
+#define BC(x) do { err = (x); if (err != hipSuccess) goto done; } while (0)
+	BC(hipMalloc(&counts, ((size_t)n + 1) * 8));
+	BC(hipMemsetAsync(counts, 0, ((size_t)n + 1) * 8, s));
+	if (nnz) {
+		BC(hipMalloc(&ki, nnz * 4));
+		BC(hipMalloc(&ko, nnz * 4));
+		BC(hipMalloc(&vi, nnz * 8));
+		if (nf) k_csc_expand<<<nf, 256, 0, s>>>(col_ptr, csc, ki, vi);
+		BC(hipGetLastError());
+		BC(rocprim::radix_sort_pairs(nullptr, tb, ki, ko, vi, csr, (size_t)nnz, 0, bits, s));
+		BC(hipMalloc(&tmp, tb));
+		BC(rocprim::radix_sort_pairs(tmp, tb, ki, ko, vi, csr, (size_t)nnz, 0, bits, s));
+		k_count_u32<<<grid_for(nnz), 256, 0, s>>>(ko, nnz, counts);
+		BC(hipGetLastError());
+		BC(hipStreamSynchronize(s));
+		BC(hipFree(tmp));
+		tmp = nullptr;
+	}
+	BC(exclusive_scan_u64(nullptr, &tb2, reinterpret_cast<uint64_t *>(counts), row_ptr, (size_t)n + 1, s));
+	BC(hipMalloc(&tmp, tb2));
+	BC(exclusive_scan_u64(tmp, &tb2, reinterpret_cast<uint64_t *>(counts), row_ptr, (size_t)n + 1, s));
+	BC(hipStreamSynchronize(s));
+#undef BC
+done:
+	if (ki) (void)hipFree(ki);
+	if (ko) (void)hipFree(ko);
+	if (vi) (void)hipFree(vi);
+	if (counts) (void)hipFree(counts);
+	if (tmp) (void)hipFree(tmp);
+	return err;
 }
 
 hipError_t sort_pairs_u32(void *tmp, size_t *tmp_bytes, const uint32_t *ki, uint32_t *ko, const uint32_t *vi,

@@ -120,7 +120,7 @@ EXPORTS = ["vbfm_abi_version", "vbfm_last_error", "vbfm_create", "vbfm_destroy",
            "vbfm_step_w0", "vbfm_step_w", "vbfm_step_qcache", "vbfm_step_v", "vbfm_step_hyper",
            "vbfm_free_energy", "vbfm_get_rows", "vbfm_get_test_e", "vbfm_factor_sweep", "vbfm_set_profiling",
            "vbfm_set_layout", "vbfm_get_layout", "vbfm_set_shard_mode",
-           "vbfm_comm_unique_id", "vbfm_comm_init", "vbfm_load_data", "vbfm_free_host_data",
+           "vbfm_comm_unique_id", "vbfm_comm_init", "vbfm_load_data", "vbfm_free_host_data", "vbfm_save_data",
            "vbfm_init_params_host", "vbfm_mcmc_init", "vbfm_mcmc_set_params", "vbfm_mcmc_get_params",
            "vbfm_mcmc_init_caches", "vbfm_mcmc_iterate", "vbfm_mcmc_get_test_pred", "vbfm_mcmc_factor_sweep"]
 
@@ -169,6 +169,7 @@ def lib():
         L.vbfm_comm_init.argtypes = [V, C.c_int32, C.c_int32, C.POINTER(C.c_uint8)]
         L.vbfm_load_data.argtypes = [C.c_char_p, C.POINTER(HostData)]
         L.vbfm_free_host_data.argtypes = [C.POINTER(HostData)]
+        L.vbfm_save_data.argtypes = [C.c_char_p, C.POINTER(HostData)]
         L.vbfm_free_host_data.restype = None
         L.vbfm_init_params_host.argtypes = [C.c_uint32, C.c_double, C.c_int32, C.c_uint32, C.c_uint32,
                                             C.POINTER(Params), P_f64, P_f64]
@@ -246,6 +247,18 @@ class DataSubset:
         ent["id"] = rows[order]
         ent["value"] = np.asarray(val, dtype=np.float32)[order]
         return cls(col_ptr, ent, target, num_feature=nf)
+
+    def save_binary(self, basename):
+        """Write <basename>.x/.xt/.y in the reference's binary format (tools/convert +
+        tools/transpose); DataSubset.load(basename) reads it back."""
+        if self.row_ptr is None:
+            raise VbfmError("save_binary needs the row copy (a data set from DataSubset.load)")
+        rp = np.ascontiguousarray(self.row_ptr, dtype=np.uint64)
+        re = np.ascontiguousarray(self.row_ent, dtype=ENTRY_DTYPE)
+        h = HostData(self.num_cases, self.num_feature, len(self.col_ent), self.min_target, self.max_target,
+                     _ptr(self.target, P_f32), _ptr(rp, P_u64), re.ctypes.data if len(re) else None,
+                     _ptr(self.col_ptr, P_u64), self.col_ent.ctypes.data if len(self.col_ent) else None)
+        _check(lib().vbfm_save_data(basename.encode(), C.byref(h)))
 
     def _csc(self):
         c = Csc(self.num_cases, self.num_feature, len(self.col_ent), _ptr(self.col_ptr, P_u64),

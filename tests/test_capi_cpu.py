@@ -133,3 +133,63 @@ def test_init_params_host_movielens_draws():
     t, a = load_case("sa_k8")
     p, _, _, _ = _host_init(42, 0.1, 8, int(t["nums"]["D"]))
     np.testing.assert_array_equal(p["mu_w"], a["init_mu_w"])
+
+
+WEIRD_LINES = ["3 1: 2.5", "+3 +1:+2", "4 2:1e-3\t", "  \t5 0:1 1:2#c", "1 7:1 7:2", "2", "2 \t # only target",
+               "1.5e1 3:.5 4:5.", "-0 1:-0", "3 1:1\r", "\r", "3 1:1 junk", "3 0x1p3:1", "3 1:x", "3 1:1:2",
+               "3 -1:1", "0x1p2 1:1", "3 1:1e", "inf 1:1", "3 70000:1"]
+
+
+@pytest.mark.parametrize("line", WEIRD_LINES)
+def test_loader_line_semantics_vs_oracle(line, tmp_path):
+    """Each odd line on its own, against the oracle's sscanf-based Data::load restatement:
+    both accept it with the same entries, or both reject it."""
+    p = tmp_path / "l.libfm"
+    p.write_text("1 0:1\n" + line + "\n")
+    try:
+        od = oc.Data(str(p))
+    except ValueError:
+        od = None
+    if od is None:
+        with pytest.raises(vbfm.VbfmError, match="cannot parse line"):
+            vbfm.DataSubset.load(str(p))
+        return
+    ds = vbfm.DataSubset.load(str(p))
+    assert ds.num_cases == od.num_rows and ds.num_feature == od.num_feature
+    np.testing.assert_array_equal(ds.target, od.csr()[3])
+    np.testing.assert_array_equal(ds.col_ptr, od.csc()[0])
+    np.testing.assert_array_equal(ds.col_ent["id"], od.csc()[1])
+    np.testing.assert_array_equal(ds.col_ent["value"], od.csc()[2])
+
+
+def test_loader_threads_agree(tmp_path, monkeypatch):
+    """The parallel parse and transpose (several MB, split at line boundaries) give the
+    single-threaded result exactly."""
+    rp, f, v, y = synth.generate(60000, 12, 400, 21, 1)
+    path = str(tmp_path / "big.libfm")
+    synth.write_libfm(path, rp, f, v, y)
+    out = {}
+    for t in ("1", "7"):
+        monkeypatch.setenv("VBFM_LOADER_THREADS", t)
+        out[t] = vbfm.DataSubset.load(path)
+    a, b = out["1"], out["7"]
+    for key in ("col_ptr", "col_ent", "target", "row_ptr", "row_ent"):
+        np.testing.assert_array_equal(getattr(a, key), getattr(b, key), err_msg=key)
+    np.testing.assert_array_equal(b.col_ent["id"], oc.Data(path).csc()[1])
+
+
+def test_save_binary_round_trip(tmp_path):
+    """vbfm_save_data writes the reference's .x/.xt/.y; loading it gives the text data set."""
+    rp, f, v, y = synth.generate(5000, 7, 60, 5, 1)
+    path = str(tmp_path / "d.libfm")
+    synth.write_libfm(path, rp, f, v, y)
+    dt = vbfm.DataSubset.load(path)
+    base = str(tmp_path / "bin")
+    dt.save_binary(base)
+    ref = str(tmp_path / "ref")
+    synth.write_binary(ref, dt.num_feature, rp, f, v, y)   # tests/synth.py's independent writer
+    for ext in (".x", ".xt", ".y"):
+        assert open(base + ext, "rb").read() == open(ref + ext, "rb").read(), ext
+    db = vbfm.DataSubset.load(base)
+    for key in ("col_ptr", "col_ent", "target", "row_ptr", "row_ent"):
+        np.testing.assert_array_equal(getattr(dt, key), getattr(db, key), err_msg=key)
