@@ -364,3 +364,30 @@ def test_feature_shards_vs_oracle(P):
     close(g.rows()["e"], o.rows()["e"])
     close(g.get_params()["mu_v"], o.params()["mu_v"])
     close(g.get_params()["mu_w"], o.params()["mu_w"])
+
+
+def test_full_size_layouts_and_split_agree():
+    """Size-independent properties at C3 shape (1e7 rows x 40 one-hot fields, 1e6 features;
+    k = 4 to keep it short): the level-ordered and the column-gather layouts, fused and split
+    (multi-rank) kernels, agree to summation order over two iterations."""
+    n, F, S, k = 10_000_000, 40, 25_000, 4
+    res = {}
+    for layout, split in (("level", "0"), ("column", "0"), ("level", "1")):
+        os.environ["VBFM_FORCE_SPLIT"] = split
+        try:
+            g = vbfm.FMLearnVB(1, 1, k, F * S + 1, min_target=1.0, max_target=5.0, layout=layout)
+            g.init_device(42)
+            g.synth(0, n, F, S, 1000, 0)
+            g.synth(1, 100_000, F, S, 500000, 0)
+            g.init_caches()
+            assert g.layout() == layout
+            st = [g.iterate() for _ in range(2)]
+            res[(layout, split)] = ([s.free_energy for s in st], [s.rmse for s in st], g.get_params()["mu_v"])
+            g.close()
+        finally:
+            os.environ.pop("VBFM_FORCE_SPLIT", None)
+    base = res[("level", "0")]
+    for key, r in res.items():
+        close(r[0], base[0], 1e-11)
+        close(r[1], base[1], 1e-11)
+        close(r[2], base[2], 1e-11)
