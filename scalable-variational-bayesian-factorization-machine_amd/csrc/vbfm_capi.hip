@@ -284,6 +284,26 @@ void fs_pass(vbfm_ctx *c, bool is_w, int f)
 	HIPCHK(vbk::fs_unpack(c->rows, n, c->fs_base, c->fs_buf, next, c->s));
 }
 
+// VBFM_CHECK=1: verify on the device that no level lets two columns touch one row (the
+// property that makes the concurrent level kernels race-free and equal to the sequential sweep)
+void check_schedule(vbfm_ctx *c)
+{
+	const uint32_t n = c->tr.n;
+	uint32_t *owner = dalloc<uint32_t>(n), *bad = dalloc<uint32_t>(1);
+	HIPCHK(hipMemsetAsync(bad, 0, 4, c->s));
+	for (uint32_t l = 0; l < nlevels(c); l++) {
+		HIPCHK(hipMemsetAsync(owner, 0xFF, (size_t)n * 4, c->s));
+		HIPCHK(vbk::check_level(c->level_feats + c->level_ptr[l], c->level_ptr[l + 1] - c->level_ptr[l], c->tr.col_ptr,
+		                        c->tr.csc, c->dup, owner, bad, c->s));
+	}
+	uint32_t nb = 0;
+	HIPCHK(hipMemcpyAsync(&nb, bad, 4, hipMemcpyDeviceToHost, c->s));
+	sync(c);
+	dfree(owner);
+	dfree(bad);
+	if (nb) throw std::string("VBFM_CHECK: dependency schedule violated (") + std::to_string(nb) + " row claims)";
+}
+
 // Dependency levels of the train features (see vbfm_kernels.hip header). With several
 // row shards every round's levels are max-reduced over the shards, so all ranks share one
 // schedule: the one the un-sharded data set defines.
@@ -343,6 +363,8 @@ void build_schedule(vbfm_ctx *c)
 		c->stats_cap = maxlev;
 	}
 	c->sched_ready = true;
+	const char *chk = getenv("VBFM_CHECK");
+	if (chk && chk[0] == '1') check_schedule(c);
 	build_fshards(c);
 	build_lorder(c, cp, feats);
 }
@@ -452,6 +474,7 @@ void sweep_level(vbfm_ctx *c, uint32_t l, bool is_w, int f)
 {
 	LevelArgs a = level_args(c, l, is_w, f);
 	if (a.nfeat == 0) return;
+	Range r("level", 2);
 	const size_t p = prof_begin(c, is_w ? 1 : 0);
 	if (c->lord) {
 		// level-ordered store: stream this level's records, move them to the next level's order
@@ -1071,21 +1094,33 @@ int vbfm_iterate(vbfm_ctx *c, vbfm_iter_stats *o)
 		HIPCHK(hipMemsetAsync(c->counters, 0, CNT_N * 4, c->s));
 		c->pev_used = 0;
 		c->spans.clear();
+		Range r_it("vbfm_iterate");
 		HIPCHK(hipEventRecord(c->ev[EV_BEGIN], c->s));
 		// update_all (fm_learn_vb.h:383-501)
-		if (c->k0) step_w0(c);
+		if (c->k0) { Range r("update_w0"); step_w0(c); }
 		HIPCHK(hipEventRecord(c->ev[EV_W0], c->s));
-		if (c->k1) step_w(c);
+		if (c->k1) { Range r("update_w sweep"); step_w(c); }
 		HIPCHK(hipEventRecord(c->ev[EV_W], c->s));
 		if (c->D > 0)
-			for (int f = 0; f < c->k; f++) { step_qcache(c, f); step_v(c, f); }
+			for (int f = 0; f < c->k; f++) {
+				char nm[32];
+				snprintf(nm, sizeof(nm), "factor %d", f);
+				Range r(nm);
+				step_qcache(c, f);
+				step_v(c, f);
+			}
 		HIPCHK(hipEventRecord(c->ev[EV_V], c->s));
 		double energy = 0.0;
-		const bool early = step_hyper(c, &energy, &st.nan_alpha, &st.inf_alpha);
-		st.free_energy_valid = early ? 0 : 1;
-		st.free_energy = early ? NAN : free_energy(c, energy);
+		bool early;
+		{
+			Range r("hyper + free energy");
+			early = step_hyper(c, &energy, &st.nan_alpha, &st.inf_alpha);
+			st.free_energy_valid = early ? 0 : 1;
+			st.free_energy = early ? NAN : free_energy(c, energy);
+		}
 		HIPCHK(hipEventRecord(c->ev[EV_HYPER], c->s));
 		// test prediction and metrics (fm_learn_vb_simultaneous.h:125-222)
+		Range r_test("test prediction");
 		test_predict(c);
 		const double mn = c->min_target, mx = c->max_target;
 		HIPCHK(vbk::test_metrics(c->e_test, c->te.target, c->te.n, mn, mx, c->pred_test, c->red_d, c->RED_BLOCKS, c->s));

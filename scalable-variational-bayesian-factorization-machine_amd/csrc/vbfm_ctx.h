@@ -6,6 +6,8 @@
 #include "../../include/vbfm.h"
 
 #include <rccl/rccl.h>
+#include <rocprofiler-sdk-roctx/roctx.h>
+#include <cstdlib>
 
 #include <string>
 #include <vector>
@@ -60,6 +62,20 @@ template <class T> inline void dfree(T *&p)
 }
 
 enum { EV_BEGIN, EV_W0, EV_W, EV_V, EV_HYPER, EV_TEST, EV_N };
+
+// roctx ranges around the phases of an iteration (VBFM_ROCTX=1; 2 adds one per level launch)
+// for rocprofv3 --marker-trace timelines
+inline int roctx_level()
+{
+	static const int lvl = [] { const char *e = getenv("VBFM_ROCTX"); return e ? atoi(e) : 0; }();
+	return lvl;
+}
+
+struct Range {
+	bool on;
+	Range(const char *name, int lvl = 1) : on(roctx_level() >= lvl) { if (on) roctxRangePushA(name); }
+	~Range() { if (on) roctxRangePop(); }
+};
 
 }  // namespace vbi
 

@@ -182,6 +182,9 @@ hipError_t synth_field_keys(const uint2 *csr, uint32_t n, uint32_t F, uint32_t S
 hipError_t synth_field_scatter(const uint32_t *sorted_rows, const uint2 *csr, uint32_t n, uint32_t F,
                                uint32_t field, uint2 *csc_field, hipStream_t s);
 hipError_t count_features(const uint2 *csr, uint64_t nnz, uint64_t *counts, hipStream_t s);
+// schedule check: owner[n] preset to ~0; *bad counts rows claimed by two columns of the level
+hipError_t check_level(const uint32_t *feats, uint32_t nfeat, const uint64_t *col_ptr, const uint2 *csc,
+                       const uint8_t *dup, uint32_t *owner, uint32_t *bad, hipStream_t s);
 // row copy (row_ptr [n+1], feature-sorted csr [nnz]) of a CSC data set, built on the device
 hipError_t build_csr(const uint64_t *col_ptr, const uint2 *csc, uint32_t nf, uint32_t n, uint64_t nnz,
                      uint64_t *row_ptr, uint2 *csr, hipStream_t s);

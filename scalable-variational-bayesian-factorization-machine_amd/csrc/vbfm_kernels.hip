@@ -881,6 +881,22 @@ __global__ void k_count_u32(const uint32_t *keys, uint64_t n, unsigned long long
 	if (i < n) atomicAdd(&counts[keys[i]], 1ull);
 }
 
+// ------------------------------------------------------------------------------------
+// schedule check (VBFM_CHECK=1): within one level every row may be touched by one column at
+// most (a column listing a row twice is corrected sequentially and counted once), or two
+// workgroups of the level would update the same row concurrently
+__global__ __launch_bounds__(256) void k_check_level(const uint32_t *feats, const uint64_t *col_ptr, const uint2 *csc,
+                                                     const uint8_t *dup, uint32_t *owner, uint32_t *bad)
+{
+	const uint32_t j = feats[blockIdx.x];
+	const uint64_t b = col_ptr[j], e = col_ptr[j + 1];
+	for (uint64_t p = b + threadIdx.x; p < e; p += 256) {
+		const uint32_t r = csc[p].x & ROW_MASK;
+		const uint32_t prev = atomicCAS(&owner[r], 0xFFFFFFFFu, j);
+		if (prev != 0xFFFFFFFFu && !(prev == j && dup[j])) atomicAdd(bad, 1u);
+	}
+}
+
 inline unsigned grid_for(uint64_t n, unsigned block = 256) { return (unsigned)((n + block - 1) / block); }
 
 }  // namespace
@@ -1166,6 +1182,14 @@ done:
 	if (counts) (void)hipFree(counts);
 	if (tmp) (void)hipFree(tmp);
 	return err;
+}
+
+hipError_t check_level(const uint32_t *feats, uint32_t nfeat, const uint64_t *col_ptr, const uint2 *csc,
+                       const uint8_t *dup, uint32_t *owner, uint32_t *bad, hipStream_t s)
+{
+	if (nfeat == 0) return hipSuccess;
+	k_check_level<<<nfeat, 256, 0, s>>>(feats, col_ptr, csc, dup, owner, bad);
+	return hipGetLastError();
 }
 
 hipError_t sort_pairs_u32(void *tmp, size_t *tmp_bytes, const uint32_t *ki, uint32_t *ko, const uint32_t *vi,

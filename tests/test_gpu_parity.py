@@ -391,3 +391,22 @@ def test_full_size_layouts_and_split_agree():
         close(r[0], base[0], 1e-11)
         close(r[1], base[1], 1e-11)
         close(r[2], base[2], 1e-11)
+
+
+@pytest.mark.parametrize("case", ["tiny", "tiny_dup"])
+def test_schedule_check_and_markers(case, monkeypatch):
+    """VBFM_CHECK=1 verifies on the device that no level lets two columns touch one row (a
+    repeated row inside one column is allowed: it is corrected sequentially); VBFM_ROCTX=2
+    wraps phases and level launches in roctx ranges. Neither changes the results."""
+    monkeypatch.setenv("VBFM_CHECK", "1")
+    monkeypatch.setenv("VBFM_ROCTX", "2")
+    d = os.path.join(GOLDEN, case)
+    train = vbfm.DataSubset.load(os.path.join(d, "train.libfm"))
+    test = vbfm.DataSubset.load(os.path.join(d, "test.libfm"))
+    g = gpu_learner(train, test, "1,1,3", 5, 0.1)
+    g.init_caches()
+    a = [g.iterate().rmse for _ in range(2)]
+    monkeypatch.delenv("VBFM_CHECK")
+    g2 = gpu_learner(train, test, "1,1,3", 5, 0.1)
+    g2.init_caches()
+    assert a == [g2.iterate().rmse for _ in range(2)]
