@@ -67,8 +67,8 @@ enum { EV_BEGIN, EV_W0, EV_W, EV_V, EV_HYPER, EV_TEST, EV_N };
 // for rocprofv3 --marker-trace timelines
 inline int roctx_level()
 {
-	static const int lvl = [] { const char *e = getenv("VBFM_ROCTX"); return e ? atoi(e) : 0; }();
-	return lvl;
+	const char *e = getenv("VBFM_ROCTX");
+	return e ? atoi(e) : 0;
 }
 
 struct Range {
