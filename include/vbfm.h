@@ -128,6 +128,13 @@ int vbfm_get_params(vbfm_ctx *ctx, vbfm_params *p);
  * sigma_* = .02, hyper parameters and scalars at their fm_learn_vb::init values. */
 int vbfm_init_params_device(vbfm_ctx *ctx, uint64_t seed);
 
+/* The reference's initial draws -- exactly what vbfm_init_params_host + vbfm_set_params
+ * produce (srand(seed); fm.v, fm.w ~ N(0, init_stdev); mu_w_dash, mu_v_dash = 0.1 N(0,1);
+ * glibc rand() with Leva normals) -- generated on the device: the glibc stream split into
+ * chunks by jump-ahead, Leva's rejection as a stream compaction. fm_v [k*D] (f-major) and
+ * fm_w [D] receive the model draws (v_file.txt) when not NULL. */
+int vbfm_init_params_replay(vbfm_ctx *ctx, uint32_t seed, double init_stdev, double *fm_v, double *fm_w);
+
 /* ---- learning (fm_learn_vb_simultaneous::_learn, fm_learn_vb_simultaneous.h:18-259) ---- */
 int vbfm_init_caches(vbfm_ctx *ctx);                     /* :37-44 */
 int vbfm_iterate(vbfm_ctx *ctx, vbfm_iter_stats *out);   /* one pass of :75-258 */

@@ -185,6 +185,7 @@ void prof_end(vbfm_ctx *c, size_t a);
 int blocked_predict(const vbfm_ctx *c, const DevData &d);
 float ev_ms(vbfm_ctx *c, int a, int b);
 void mc_free(vbfm_ctx *c);   // vbfm_mcmc_capi.hip
+void upload_hyp(vbfm_ctx *c);
 void lord_release(vbfm_ctx *c, bool keep_rows);
 void rows_level_order(vbfm_ctx *c);   // records in level-0 order before a sweep (no-op without the store)
 void rows_row_order(vbfm_ctx *c);     // records back in row order (row-indexed kernels, readback)   // level-ordered store freed (rows back to row order)

@@ -85,10 +85,23 @@ public:
 		}
 	}
 	double gamma(double a, double b) { return gamma(a) / b; }   // random.h:150-152 form
+	// the generator as the recurrence y_n = y_{n-31} + y_{n-3} (mod 2^32), output y_n >> 1:
+	// st[i] = y_{n-31+i}, the 31 sums preceding the next output
+	void chrono_state(uint32_t st[31]) const
+	{
+		for (int i = 0; i < 31; i++) st[i] = (uint32_t)r_[(f_ + i) % 31];
+	}
 
 private:
 	int32_t r_[31];
 	int f_ = 3, b_ = 0;
 };
+
+// the state right after srand(seed) and glibc's 310 discarded outputs (vbfm_replay.hip)
+inline void glibc_warm_state(uint32_t seed, uint32_t st[31])
+{
+	Glibc g(seed);
+	g.chrono_state(st);
+}
 
 }  // namespace vbrng

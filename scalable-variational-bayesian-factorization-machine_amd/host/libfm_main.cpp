@@ -339,12 +339,29 @@ int main(int argc, char **argv)
 			return 0;
 		}
 
-		// fm.init + fm.w.init_normal + fml->init draws (libfm.cpp:123-366) on the host
+		vbfm_config cfg{k0, k1, k, D, G, cmd.has(p_meta) ? groups.data() : nullptr, train.h.min_target,
+		                train.h.max_target, (int32_t)cmd.geti(p_dev, 0), 0};
+		check(vbfm_create(&ctx, &cfg), nullptr);
+		const vbfm_csc tr = train.csc(), te = test.csc();
+		check(vbfm_set_train(ctx, &tr), ctx);
+		check(vbfm_set_test(ctx, &te), ctx);
+
+		// fm.init + fm.w.init_normal + fml->init draws (libfm.cpp:123-366): the same stream on
+		// the host (small models) or generated on the device (VBFM_INIT=host|replay overrides)
 		const size_t kd = (size_t)k * D;
-		std::vector<double> mu_w(D), sig_w(D), mu_v(kd), sig_v(kd), hw(G), hv((size_t)G * k), fm_v(kd);
-		vbfm_params p{mu_w.data(), sig_w.data(), mu_v.data(), sig_v.data(), hw.data(), hv.data(), 0, 0, 0, 0};
-		check(vbfm_init_params_host(seed, init_stdev, k, D, G, &p, fm_v.data(), nullptr), nullptr);
-		if (cmd.geti(p_vfile, 1)) {   // fm_model.h:98 (DMatrix::save, matrix.h:129-152)
+		const bool vfile = cmd.geti(p_vfile, 1) != 0;
+		const char *init_env = getenv("VBFM_INIT");
+		const bool replay = init_env ? std::string(init_env) == "replay" : kd + D >= 2000000;
+		std::vector<double> fm_v(vfile || !replay ? kd : 0);
+		if (replay) {
+			check(vbfm_init_params_replay(ctx, seed, init_stdev, vfile ? fm_v.data() : nullptr, nullptr), ctx);
+		} else {
+			std::vector<double> mu_w(D), sig_w(D), mu_v(kd), sig_v(kd), hw(G), hv((size_t)G * k);
+			vbfm_params p{mu_w.data(), sig_w.data(), mu_v.data(), sig_v.data(), hw.data(), hv.data(), 0, 0, 0, 0};
+			check(vbfm_init_params_host(seed, init_stdev, k, D, G, &p, fm_v.data(), nullptr), nullptr);
+			check(vbfm_set_params(ctx, &p), ctx);
+		}
+		if (vfile) {   // fm_model.h:98 (DMatrix::save, matrix.h:129-152)
 			std::ofstream vf("v_file.txt");
 			for (int f = 0; f < k; f++) {
 				for (uint32_t j = 0; j < D; j++) vf << (j ? "\t" : "") << fm_v[(size_t)f * D + j];
@@ -353,15 +370,6 @@ int main(int argc, char **argv)
 		}
 		fm_v.clear();
 		fm_v.shrink_to_fit();
-
-		vbfm_config cfg{k0, k1, k, D, G, cmd.has(p_meta) ? groups.data() : nullptr, train.h.min_target,
-		                train.h.max_target, (int32_t)cmd.geti(p_dev, 0), 0};
-		check(vbfm_create(&ctx, &cfg), nullptr);
-		const vbfm_csc tr = train.csc(), te = test.csc();
-		check(vbfm_set_train(ctx, &tr), ctx);
-		check(vbfm_set_test(ctx, &te), ctx);
-		check(vbfm_set_params(ctx, &p), ctx);
-		mu_v.clear(); sig_v.clear(); mu_v.shrink_to_fit(); sig_v.shrink_to_fit();
 
 		// -rlog (libfm.cpp:353-363; fields of fm_learn::init and fm_learn_vb::init)
 		std::ofstream *rlog_out = nullptr;

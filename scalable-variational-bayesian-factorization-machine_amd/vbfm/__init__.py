@@ -116,7 +116,7 @@ class HostData(C.Structure):
 # every symbol include/vbfm.h declares (checked by tests/test_capi_cpu.py)
 EXPORTS = ["vbfm_abi_version", "vbfm_last_error", "vbfm_create", "vbfm_destroy", "vbfm_set_train",
            "vbfm_set_test", "vbfm_synth_generate", "vbfm_get_csc", "vbfm_get_shape", "vbfm_get_levels",
-           "vbfm_set_params", "vbfm_get_params", "vbfm_init_params_device", "vbfm_init_caches", "vbfm_iterate", "vbfm_get_test_pred",
+           "vbfm_set_params", "vbfm_get_params", "vbfm_init_params_device", "vbfm_init_params_replay", "vbfm_init_caches", "vbfm_iterate", "vbfm_get_test_pred",
            "vbfm_step_w0", "vbfm_step_w", "vbfm_step_qcache", "vbfm_step_v", "vbfm_step_hyper",
            "vbfm_free_energy", "vbfm_get_rows", "vbfm_get_test_e", "vbfm_factor_sweep", "vbfm_set_profiling",
            "vbfm_set_layout", "vbfm_get_layout", "vbfm_set_shard_mode",
@@ -150,6 +150,7 @@ def lib():
         L.vbfm_get_params.argtypes = [V, C.POINTER(Params)]
         L.vbfm_init_caches.argtypes = [V]
         L.vbfm_init_params_device.argtypes = [V, C.c_uint64]
+        L.vbfm_init_params_replay.argtypes = [V, C.c_uint32, C.c_double, P_f64, P_f64]
         L.vbfm_iterate.argtypes = [V, C.POINTER(IterStats)]
         L.vbfm_get_test_pred.argtypes = [V, P_f64]
         for fn in ("vbfm_step_w0", "vbfm_step_w"):
@@ -334,6 +335,15 @@ class FMLearnVB:
         self.fm_v, self.fm_w = fm_v, fm_w
         self.set_params(p)
         return p
+
+    def init_replay(self, seed, init_stdev=0.1, keep_model_draws=False):
+        """init() with the reference's stream generated on the device (vbfm_init_params_replay):
+        the same parameters bit for bit, without the host's sequential draws."""
+        fm_v = np.zeros(self.k * self.D) if keep_model_draws else None
+        fm_w = np.zeros(self.D) if keep_model_draws else None
+        _check(lib().vbfm_init_params_replay(self._ctx, seed, init_stdev, _ptr(fm_v, P_f64), _ptr(fm_w, P_f64)),
+               self._ctx)
+        self.fm_v, self.fm_w = fm_v, fm_w
 
     def init_device(self, seed):
         """Random init on the device (bench scale; not the reference's RNG stream)."""

@@ -39,8 +39,12 @@ def run_cli(tmp_path, train, test, dim, iters, seed, extra=(), method="vb"):
     return out.stdout
 
 
+@pytest.mark.parametrize("init", ["host", "replay"])
 @pytest.mark.parametrize("case", ["tiny/vb", "tiny/vb_meta"])
-def test_cli_tiny_files_match_reference(case, tmp_path):
+def test_cli_tiny_files_match_reference(case, init, tmp_path, monkeypatch):
+    """init: the initial draws on the host or generated on the device (vbfm_init_params_replay,
+    the CLI's choice for large models)."""
+    monkeypatch.setenv("VBFM_INIT", init)
     t, a = load_case(case)
     m = t["meta"]
     d = os.path.join(GOLDEN, case.split("/")[0])

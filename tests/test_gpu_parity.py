@@ -410,3 +410,23 @@ def test_schedule_check_and_markers(case, monkeypatch):
     g2 = gpu_learner(train, test, "1,1,3", 5, 0.1)
     g2.init_caches()
     assert a == [g2.iterate().rmse for _ in range(2)]
+
+
+# seed 376 draws a zero u at output 820,432 of its stream (Leva redraws it: every later attempt
+# shifts by one); found by a host scan of seeds 1..1300 (tools/find_zero_seed.cpp)
+@pytest.mark.parametrize("seed,init_stdev", [(1, 0.1), (376, 0.1), (376, 0.0), (823, 0.05)])
+def test_init_replay_equals_host_draws(seed, init_stdev):
+    """vbfm_init_params_replay (the glibc stream by jump-ahead chunks on the device, Leva's
+    rejection as a compaction) == vbfm_init_params_host, bit for bit, model draws included."""
+    k, D = 8, 1_000_001 if seed == 823 else 100_001
+    a = vbfm.FMLearnVB(1, 1, k, D)
+    a.init(seed, init_stdev, keep_model_draws=True)
+    b = vbfm.FMLearnVB(1, 1, k, D)
+    b.init_replay(seed, init_stdev, keep_model_draws=True)
+    pa, pb = a.get_params(), b.get_params()
+    for key in ("mu_w", "sigma_w", "mu_v", "sigma_v", "hyp_sigma_w", "hyp_sigma_v"):
+        np.testing.assert_array_equal(pa[key], pb[key], err_msg=key)
+    for key in ("alpha", "sigma_0", "mu_0_dash", "sigma_0_dash"):
+        assert pa[key] == pb[key]
+    np.testing.assert_array_equal(a.fm_v, b.fm_v)
+    np.testing.assert_array_equal(a.fm_w, b.fm_w)
