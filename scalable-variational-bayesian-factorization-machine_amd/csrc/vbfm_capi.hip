@@ -106,6 +106,7 @@ void lord_release(vbfm_ctx *c, bool keep_rows)
 	}
 	sync(c);
 	dfree(c->rows_alt); dfree(c->lcp); dfree(c->lx); dfree(c->lnext); dfree(c->lrow0); dfree(c->lpos0);
+	dfree(c->lpidx); dfree(c->lpx); dfree(c->post_tab);
 	c->lord = false;
 	c->rows_lorder = false;
 }
@@ -174,6 +175,26 @@ void build_lorder(vbfm_ctx *c, const std::vector<uint64_t> &cp, const std::vecto
 		HIPCHK(vbk::lord_fill(f, nfl, lp, (uint64_t)l * n, d.col_ptr, d.csc, pos_next, c->lx, c->lnext,
 		                      l == 0 ? c->lrow0 : nullptr, c->s));
 		if (l > 0) HIPCHK(vbk::lord_pos(f, nfl, lp, (uint64_t)l * n, d.col_ptr, d.csc, tmp, c->s));
+	}
+	// split form (row shards): each entry's previous-level feature and x, for the deferred
+	// correction (VBFM_DEFER=0 keeps the two-pass split)
+	const char *df = getenv("VBFM_DEFER");
+	if ((c->row_comm() || c->force_split) && !(df && df[0] == '0')) {
+		c->lpidx = dalloc<uint32_t>(d.nnz);
+		c->lpx = dalloc<float>(d.nnz);
+		float *tmpx = dalloc<float>(n);
+		uint32_t maxlev = 0;
+		for (uint32_t l = 0; l < L; l++) {
+			const uint32_t pl = (l + L - 1) % L;
+			maxlev = std::max(maxlev, c->level_ptr[l + 1] - c->level_ptr[l]);
+			HIPCHK(vbk::lord_prev_map(c->level_feats + c->level_ptr[pl], c->level_ptr[pl + 1] - c->level_ptr[pl],
+			                          d.col_ptr, d.csc, nullptr, tmp, tmpx, c->s));
+			lev(l, f, nfl, lp);
+			HIPCHK(vbk::lord_prev_fill(f, nfl, lp, d.col_ptr, d.csc, tmp, tmpx, c->lpidx, c->lpx, c->s));
+		}
+		c->post_tab = dalloc<PostT>(maxlev);
+		sync(c);
+		dfree(tmpx);
 	}
 	sync(c);
 	dfree(tmp);
@@ -487,6 +508,23 @@ void sweep_level(vbfm_ctx *c, uint32_t l, bool is_w, int f)
 		a.first_level = l == 0;
 		if (!c->row_comm() && !c->force_split) {
 			HIPCHK(vbk::lord_level(a, is_w, c->s));
+		} else if (c->lpidx) {
+			// deferred: level l-1's correction, level l's statistics and the move in one pass;
+			// level l's correction after the all-reduce, by level l+1 (or the flush)
+			a.lpidx = c->lpidx;
+			a.lpx = c->lpx;
+			a.tab = c->post_tab;
+			a.pending = l > 0;
+			a.first_prev = l == 1;
+			HIPCHK(vbk::lord_defer_level(a, is_w, c->s));
+			if (c->row_comm())
+				NCCLCHK(ncclAllReduce(c->stats, c->stats, 2 * (size_t)a.nfeat, ncclDouble, ncclSum, c->comm, c->s));
+			HIPCHK(vbk::lord_defer_post(a, is_w, c->s));
+			if (l + 1 == nlevels(c)) {   // the sweep's last correction, on level-0-ordered records
+				a.dst = c->rows_alt;      // (swapped below)
+				a.first_prev = l == 0;
+				HIPCHK(vbk::lord_defer_flush(a, is_w, c->tr.n, c->s));
+			}
 		} else {
 			HIPCHK(vbk::lord_level_stats(a, is_w, c->s));
 			if (c->row_comm())

@@ -138,6 +138,9 @@ struct vbfm_ctx {
 	uint32_t *lnext = nullptr;     // [nnz] position of the entry's row in the next level
 	uint32_t *lrow0 = nullptr;     // [n] row at each level-0 position
 	uint32_t *lpos0 = nullptr;     // [n] level-0 position of each row
+	uint32_t *lpidx = nullptr;     // [nnz] split form: the row's previous-level feature (index in its level)
+	float *lpx = nullptr;          // [nnz] ... and its x (deferred correction)
+	PostT *post_tab = nullptr;     // [max level width] posteriors of the last level swept
 	// feature-sharded mode (vbfm_set_shard_mode): shards own column chunks of every level
 	int shard_mode = VBFM_SHARD_ROWS;
 	int fs_req = 1;                // shards requested (no communicator: run one after another here)

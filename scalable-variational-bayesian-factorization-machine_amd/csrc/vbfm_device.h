@@ -41,6 +41,13 @@ enum {
 	CNT_N
 };
 
+// posterior of one feature of a level, as its entries' deferred correction needs it
+// (row-sharded split on the level-ordered store): mu = NaN marks a skipped correction
+struct __attribute__((aligned(64))) PostT {   // one 64-B line per gathered entry
+	double mo, so, mu, sig;
+	double2 nx;                // {mu, sigma} of the next factor (fused q-cache term)
+};
+
 // per-level launch description for the v / w sweeps
 struct LevelArgs {
 	const uint64_t *col_ptr;
@@ -71,6 +78,12 @@ struct LevelArgs {
 	const RowRec *src;         // records in this level's order
 	RowRec *dst;               // records in the next level's order
 	int first_level;           // level 0: every row's smallest feature (q-cache restart)
+	// deferred correction (row-sharded split on the level-ordered store)
+	const uint32_t *lpidx;     // the entry's row: index of its previous-level feature in that level
+	const float *lpx;          // ... and that entry's x
+	PostT *tab;                // posteriors of the previous level (read) / of this level (written)
+	int pending;               // apply the previous level's correction first
+	int first_prev;            // the previous level is level 0 (q-cache restart of its entries)
 };
 
 // per-level launch description for the MCMC / ALS draws (vbfm_mcmc.hip); parameters are
@@ -125,6 +138,16 @@ hipError_t qcache(const uint64_t *row_ptr, const uint2 *csr, const double2 *ms_f
 hipError_t lord_level(const LevelArgs &a, int is_w, hipStream_t s);
 hipError_t lord_level_stats(const LevelArgs &a, int is_w, hipStream_t s);
 hipError_t lord_level_move(const LevelArgs &a, int is_w, hipStream_t s);
+// deferred form of the split (one pass over the records per level): previous level's
+// correction + this level's statistics + move; posteriors into the table; final correction
+hipError_t lord_defer_level(const LevelArgs &a, int is_w, hipStream_t s);
+hipError_t lord_defer_post(const LevelArgs &a, int is_w, hipStream_t s);
+hipError_t lord_defer_flush(const LevelArgs &a, int is_w, uint32_t n, hipStream_t s);
+hipError_t lord_prev_map(const uint32_t *feats, uint32_t nfeat, const uint64_t *col_ptr, const uint2 *csc,
+                         const float *dummy, uint32_t *prev_i, float *prev_x, hipStream_t s);
+hipError_t lord_prev_fill(const uint32_t *feats, uint32_t nfeat, const uint64_t *lcp, const uint64_t *col_ptr,
+                          const uint2 *csc, const uint32_t *prev_i, const float *prev_x, uint32_t *lpidx, float *lpx,
+                          hipStream_t s);
 hipError_t lord_pos(const uint32_t *feats, uint32_t nfeat, const uint64_t *lcp, uint64_t lbase, const uint64_t *col_ptr,
                     const uint2 *csc, uint32_t *pos, hipStream_t s);
 hipError_t lord_fill(const uint32_t *feats, uint32_t nfeat, const uint64_t *lcp, uint64_t lbase, const uint64_t *col_ptr,

@@ -349,6 +349,169 @@ void launch_lord_move(const LevelArgs &a, hipStream_t s)
 	else k_level_lord_move<256, IS_W, P, false><<<a.nfeat, 256, 0, s>>>(a);
 }
 
+
+// ---- deferred correction (row-sharded split) ---------------------------------------------
+// The split form above streams every level's records twice (statistics, then after the
+// all-reduce the move). Deferred: level l's kernel applies level l-1's correction to each
+// record (its posterior from the table the previous post kernel wrote, gathered by the row's
+// level-(l-1) feature; the row's level-(l-1) x rides along in lpx), reduces level l's
+// statistics from the corrected records and moves them, still without level l's own
+// correction, to level l+1's order. After the all-reduce a small kernel turns the statistics
+// into posteriors (parameters + table); the next level applies them, a flush kernel after the
+// last level of a sweep. Same arithmetic per row as the fused kernel: bit-identical results.
+template <bool IS_W, int P, bool NEXT>
+DEVI void apply_pending(Rec &v, const PostT &t, float x, bool first)
+{
+	VbOp<IS_W, P, NEXT> op;
+	op.mo = t.mo; op.so = t.so; op.sig = t.sig; op.nx = t.nx;
+	op.go = !__builtin_isnan(t.mu);
+	op.mu = op.go ? t.mu : t.mo;
+	op.apply(v, x, first);
+}
+
+template <int BLOCK, int R, bool IS_W, int P, bool NEXT>
+__global__ __launch_bounds__(BLOCK) void k_lord_defer(LevelArgs a)
+{
+	constexpr uint32_t CAP = BLOCK * R;
+	__shared__ double2 recs[CAP * 4];
+	__shared__ uint32_t dsts[CAP];
+	__shared__ double lds[2 * (BLOCK / 64)];
+	const uint32_t j = a.feats[blockIdx.x];
+	const uint64_t sb = a.lcp[blockIdx.x];
+	const uint32_t n = (uint32_t)(a.lcp[blockIdx.x + 1] - sb);
+	const RowRec *src = a.src + (sb - a.lbase);
+	const double2 *s = reinterpret_cast<const double2 *>(src);
+	double2 *d = reinterpret_cast<double2 *>(a.dst);
+	const float *lx = a.lx + sb;
+	const uint32_t *nxt = a.lnext + sb;
+	const uint32_t *pidx = a.lpidx + sb;
+	const float *px = a.lpx + sb;
+	const double2 msj = a.ms[(size_t)j * a.ms_stride];
+	VbOp<IS_W, P, NEXT> op;
+	op.mo = msj.x; op.so = msj.y;
+	double s1 = 0.0, s2 = 0.0;
+	for (uint32_t base = 0; base < n; base += CAP) {
+		const uint32_t m = min(CAP, n - base);
+		if (base) __syncthreads();
+		// the posteriors of the records' previous-level features are gathered (L2 / MALL:
+		// one line each) while the run streams into LDS
+		PostT t[R];
+		float pxv[R];
+		if (a.pending) {
+#pragma unroll
+			for (int u = 0; u < R; ++u) {
+				const uint32_t i = threadIdx.x + u * BLOCK;
+				if (i < m) { t[u] = a.tab[pidx[base + i]]; pxv[u] = px[base + i]; }
+			}
+		}
+		stage_in<BLOCK>(recs, s + (size_t)base * 4, m);
+		__syncthreads();
+#pragma unroll
+		for (int u = 0; u < R; ++u) {
+			const uint32_t i = threadIdx.x + u * BLOCK;
+			if (i >= m) continue;
+			Rec v;
+			lds_get(recs, i, v);
+			if (a.pending) {
+				apply_pending<IS_W, P, NEXT>(v, t[u], pxv[u], a.first_prev != 0);
+				lds_put(recs, i, v);
+			}
+			op.stat(v, lx[base + i], s1, s2);
+			dsts[i] = nxt[base + i];
+		}
+		__syncthreads();
+		for (uint32_t t = threadIdx.x; t < m * 4; t += BLOCK) {
+			const uint32_t i = t >> 2, c = t & 3;
+			d[(size_t)dsts[i] * 4 + c] = recs[lslot(i, c)];
+		}
+	}
+	block_sum2<BLOCK>(s1, s2, lds);
+	if (threadIdx.x == 0) a.stats[blockIdx.x] = make_double2(s1, s2);
+}
+
+// posteriors of the level's features from the all-reduced statistics (update_v :597-619 /
+// update_w :540-565): parameters, and the table the next level's kernel reads
+template <bool IS_W, bool NEXT>
+__global__ __launch_bounds__(256) void k_lord_defer_post(LevelArgs a)
+{
+	const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+	if (i >= a.nfeat) return;
+	const uint32_t j = a.feats[i];
+	const double2 msj = a.ms[(size_t)j * a.ms_stride];
+	const double2 st = a.stats[i];
+	const double hyp = a.hyp[(size_t)a.attr_group[j] * a.hyp_stride];
+	double mu, sig;
+	const bool go = vb_post<IS_W>(st.x, st.y, hyp, a.alpha, msj.x, msj.y, mu, sig, a.counters, true);
+	a.ms[(size_t)j * a.ms_stride] = make_double2(mu, sig);
+	PostT t;
+	t.mo = msj.x; t.so = msj.y; t.sig = sig;
+	t.mu = go ? mu : __builtin_nan("");
+	t.nx = NEXT ? a.ms_next[(size_t)j * a.ms_stride_next] : make_double2(0.0, 0.0);
+	a.tab[i] = t;
+}
+
+// the last level's correction, in place on the records (level-0 order after the last move)
+template <bool IS_W, int P, bool NEXT>
+__global__ __launch_bounds__(256) void k_lord_defer_flush(LevelArgs a, uint32_t n)
+{
+	__shared__ double2 recs[256 * 4];
+	const uint32_t b = blockIdx.x * 256u;
+	const uint32_t m = min(256u, n - b);
+	double2 *r = reinterpret_cast<double2 *>(a.dst) + (size_t)b * 4;
+	stage_in<256>(recs, r, m);
+	__syncthreads();
+	if (threadIdx.x < m) {
+		Rec v;
+		lds_get(recs, threadIdx.x, v);
+		apply_pending<IS_W, P, NEXT>(v, a.tab[a.lpidx[b + threadIdx.x]], a.lpx[b + threadIdx.x], a.first_prev != 0);
+		lds_put(recs, threadIdx.x, v);
+	}
+	__syncthreads();
+	for (uint32_t t = threadIdx.x; t < m * 4; t += 256) r[t] = recs[lslot(t >> 2, t & 3)];
+}
+
+// build: prev_i[row] / prev_x[row] = (index within its level, x) of the row's entry in a level
+__global__ __launch_bounds__(256) void k_lord_prev_map(const uint32_t *feats, const uint64_t *col_ptr, const uint2 *csc,
+                                                       uint32_t *prev_i, float *prev_x)
+{
+	const uint32_t j = feats[blockIdx.x];
+	for (uint64_t p = col_ptr[j] + threadIdx.x; p < col_ptr[j + 1]; p += 256) {
+		const uint2 ent = csc[p];
+		prev_i[ent.x & ROW_MASK] = blockIdx.x;
+		prev_x[ent.x & ROW_MASK] = __uint_as_float(ent.y);
+	}
+}
+
+// lpidx / lpx of a level's entries (global positions lcp[i] + k) from the previous level's map
+__global__ __launch_bounds__(256) void k_lord_prev_fill(const uint32_t *feats, const uint64_t *lcp,
+                                                        const uint64_t *col_ptr, const uint2 *csc, const uint32_t *prev_i,
+                                                        const float *prev_x, uint32_t *lpidx, float *lpx)
+{
+	const uint32_t j = feats[blockIdx.x];
+	const uint64_t cb = col_ptr[j], g0 = lcp[blockIdx.x];
+	const uint32_t n = (uint32_t)(col_ptr[j + 1] - cb);
+	for (uint32_t k = threadIdx.x; k < n; k += 256) {
+		const uint32_t r = csc[cb + k].x & ROW_MASK;
+		lpidx[g0 + k] = prev_i[r];
+		lpx[g0 + k] = prev_x[r];
+	}
+}
+
+template <bool IS_W, int P, bool NEXT>
+void launch_defer(const LevelArgs &a, hipStream_t s)
+{
+	if (a.avg_len <= 96) k_lord_defer<64, 2, IS_W, P, NEXT><<<a.nfeat, 64, 0, s>>>(a);
+	else if (a.avg_len <= 320) k_lord_defer<256, 1, IS_W, P, NEXT><<<a.nfeat, 256, 0, s>>>(a);
+	else if (a.avg_len <= 640) k_lord_defer<256, 2, IS_W, P, NEXT><<<a.nfeat, 256, 0, s>>>(a);
+	else k_lord_defer<512, 2, IS_W, P, NEXT><<<a.nfeat, 512, 0, s>>>(a);
+}
+
+template <bool IS_W, int P, bool NEXT>
+void launch_flush(const LevelArgs &a, uint32_t n, hipStream_t s)
+{
+	k_lord_defer_flush<IS_W, P, NEXT><<<(n + 255) / 256, 256, 0, s>>>(a, n);
+}
+
 template <int BLOCK, int R, int MODE>
 void launch_mc_lord(const McArgs &a, int is_w, hipStream_t s)
 {
@@ -414,6 +577,52 @@ hipError_t lord_level_move(const LevelArgs &a, int is_w, hipStream_t s)
 	if (is_w) launch_lord_move<true, 0>(a, s);
 	else if (a.slot == 0) launch_lord_move<false, 0>(a, s);
 	else launch_lord_move<false, 1>(a, s);
+	return hipGetLastError();
+}
+
+hipError_t lord_defer_level(const LevelArgs &a, int is_w, hipStream_t s)
+{
+	if (a.nfeat == 0) return hipSuccess;
+	const bool nx = a.ms_next != nullptr;
+	if (is_w) nx ? launch_defer<true, 0, true>(a, s) : launch_defer<true, 0, false>(a, s);
+	else if (a.slot == 0) nx ? launch_defer<false, 0, true>(a, s) : launch_defer<false, 0, false>(a, s);
+	else nx ? launch_defer<false, 1, true>(a, s) : launch_defer<false, 1, false>(a, s);
+	return hipGetLastError();
+}
+
+hipError_t lord_defer_post(const LevelArgs &a, int is_w, hipStream_t s)
+{
+	if (a.nfeat == 0) return hipSuccess;
+	const unsigned g = (a.nfeat + 255) / 256;
+	if (is_w) { if (a.ms_next) k_lord_defer_post<true, true><<<g, 256, 0, s>>>(a); else k_lord_defer_post<true, false><<<g, 256, 0, s>>>(a); }
+	else { if (a.ms_next) k_lord_defer_post<false, true><<<g, 256, 0, s>>>(a); else k_lord_defer_post<false, false><<<g, 256, 0, s>>>(a); }
+	return hipGetLastError();
+}
+
+hipError_t lord_defer_flush(const LevelArgs &a, int is_w, uint32_t n, hipStream_t s)
+{
+	if (n == 0) return hipSuccess;
+	const bool nx = a.ms_next != nullptr;
+	if (is_w) nx ? launch_flush<true, 0, true>(a, n, s) : launch_flush<true, 0, false>(a, n, s);
+	else if (a.slot == 0) nx ? launch_flush<false, 0, true>(a, n, s) : launch_flush<false, 0, false>(a, n, s);
+	else nx ? launch_flush<false, 1, true>(a, n, s) : launch_flush<false, 1, false>(a, n, s);
+	return hipGetLastError();
+}
+
+hipError_t lord_prev_map(const uint32_t *feats, uint32_t nfeat, const uint64_t *col_ptr, const uint2 *csc,
+                         const float *, uint32_t *prev_i, float *prev_x, hipStream_t s)
+{
+	if (nfeat == 0) return hipSuccess;
+	k_lord_prev_map<<<nfeat, 256, 0, s>>>(feats, col_ptr, csc, prev_i, prev_x);
+	return hipGetLastError();
+}
+
+hipError_t lord_prev_fill(const uint32_t *feats, uint32_t nfeat, const uint64_t *lcp, const uint64_t *col_ptr,
+                          const uint2 *csc, const uint32_t *prev_i, const float *prev_x, uint32_t *lpidx, float *lpx,
+                          hipStream_t s)
+{
+	if (nfeat == 0) return hipSuccess;
+	k_lord_prev_fill<<<nfeat, 256, 0, s>>>(feats, lcp, col_ptr, csc, prev_i, prev_x, lpidx, lpx);
 	return hipGetLastError();
 }
 

@@ -369,11 +369,14 @@ def test_feature_shards_vs_oracle(P):
 def test_full_size_layouts_and_split_agree():
     """Size-independent properties at C3 shape (1e7 rows x 40 one-hot fields, 1e6 features;
     k = 4 to keep it short): the level-ordered and the column-gather layouts, fused and split
-    (multi-rank) kernels, agree to summation order over two iterations."""
+    (multi-rank: deferred one-pass, and the two-pass form) kernels, agree to summation order
+    over two iterations; the deferred split equals the fused kernel bit for bit."""
     n, F, S, k = 10_000_000, 40, 25_000, 4
     res = {}
-    for layout, split in (("level", "0"), ("column", "0"), ("level", "1")):
-        os.environ["VBFM_FORCE_SPLIT"] = split
+    for layout, split in (("level", "0"), ("column", "0"), ("level", "1"), ("level", "nodefer")):
+        os.environ["VBFM_FORCE_SPLIT"] = "0" if split == "0" else "1"
+        if split == "nodefer":
+            os.environ["VBFM_DEFER"] = "0"
         try:
             g = vbfm.FMLearnVB(1, 1, k, F * S + 1, min_target=1.0, max_target=5.0, layout=layout)
             g.init_device(42)
@@ -386,7 +389,11 @@ def test_full_size_layouts_and_split_agree():
             g.close()
         finally:
             os.environ.pop("VBFM_FORCE_SPLIT", None)
+            os.environ.pop("VBFM_DEFER", None)
     base = res[("level", "0")]
+    # the deferred split applies the same per-row arithmetic in the same order: bit-identical
+    assert res[("level", "1")][0] == base[0] and res[("level", "1")][1] == base[1]
+    np.testing.assert_array_equal(res[("level", "1")][2], base[2])
     for key, r in res.items():
         close(r[0], base[0], 1e-11)
         close(r[1], base[1], 1e-11)
