@@ -43,9 +43,8 @@ enum {
 
 // posterior of one feature of a level, as its entries' deferred correction needs it
 // (row-sharded split on the level-ordered store): mu = NaN marks a skipped correction
-struct __attribute__((aligned(64))) PostT {   // one 64-B line per gathered entry
+struct __attribute__((aligned(32))) PostT {   // 32 B: two entries per 64-B line
 	double mo, so, mu, sig;
-	double2 nx;                // {mu, sigma} of the next factor (fused q-cache term)
 };
 
 // per-level launch description for the v / w sweeps

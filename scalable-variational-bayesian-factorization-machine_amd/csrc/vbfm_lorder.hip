@@ -108,6 +108,18 @@ DEVI void stage_in(double2 *recs, const double2 *src, uint32_t m)
 	for (uint32_t t = threadIdx.x; t < m * 4; t += BLOCK) recs[lslot(t >> 2, t & 3)] = src[t];
 }
 
+// the same with non-temporal loads (records read once: keep L2 for gathered tables)
+typedef double ntv2 __attribute__((ext_vector_type(2)));
+template <int BLOCK>
+DEVI void stage_in_nt(double2 *recs, const double2 *src, uint32_t m)
+{
+	const ntv2 *p = reinterpret_cast<const ntv2 *>(src);
+	for (uint32_t t = threadIdx.x; t < m * 4; t += BLOCK) {
+		const ntv2 v = __builtin_nontemporal_load(p + t);
+		recs[lslot(t >> 2, t & 3)] = make_double2(v.x, v.y);
+	}
+}
+
 DEVI void lds_get(const double2 *recs, uint32_t i, Rec &v)
 {
 #pragma unroll
@@ -359,14 +371,24 @@ void launch_lord_move(const LevelArgs &a, hipStream_t s)
 // correction, to level l+1's order. After the all-reduce a small kernel turns the statistics
 // into posteriors (parameters + table); the next level applies them, a flush kernel after the
 // last level of a sweep. Same arithmetic per row as the fused kernel: bit-identical results.
-template <bool IS_W, int P, bool NEXT>
-DEVI void apply_pending(Rec &v, const PostT &t, float x, bool first)
+// the previous level's correction (without its q-cache term: each level adds its own term
+// of the next factor's q-cache in its kernel, in the same per-row order as the fused kernel)
+template <bool IS_W, int P>
+DEVI void apply_pending(Rec &v, const PostT &t, float x)
 {
-	VbOp<IS_W, P, NEXT> op;
-	op.mo = t.mo; op.so = t.so; op.sig = t.sig; op.nx = t.nx;
+	VbOp<IS_W, P, false> op;
+	op.mo = t.mo; op.so = t.so; op.sig = t.sig; op.nx = make_double2(0.0, 0.0);
 	op.go = !__builtin_isnan(t.mu);
 	op.mu = op.go ? t.mu : t.mo;
-	op.apply(v, x, first);
+	op.apply(v, x, false);
+}
+
+// this level's term of the next factor's q-cache (slot 0 after the w sweep, 1-P after v)
+template <bool IS_W, int P>
+DEVI void add_next_q(Rec &v, float x, bool first, double2 nx)
+{
+	if constexpr (IS_W) qacc<0>(v, x, first, nx);
+	else qacc<1 - P>(v, x, first, nx);
 }
 
 template <int BLOCK, int R, bool IS_W, int P, bool NEXT>
@@ -389,6 +411,8 @@ __global__ __launch_bounds__(BLOCK) void k_lord_defer(LevelArgs a)
 	const double2 msj = a.ms[(size_t)j * a.ms_stride];
 	VbOp<IS_W, P, NEXT> op;
 	op.mo = msj.x; op.so = msj.y;
+	const double2 nx = NEXT ? a.ms_next[(size_t)j * a.ms_stride_next] : make_double2(0.0, 0.0);
+	const bool first = a.first_level != 0;
 	double s1 = 0.0, s2 = 0.0;
 	for (uint32_t base = 0; base < n; base += CAP) {
 		const uint32_t m = min(CAP, n - base);
@@ -404,7 +428,8 @@ __global__ __launch_bounds__(BLOCK) void k_lord_defer(LevelArgs a)
 				if (i < m) { t[u] = a.tab[pidx[base + i]]; pxv[u] = px[base + i]; }
 			}
 		}
-		stage_in<BLOCK>(recs, s + (size_t)base * 4, m);
+		if (a.pending) stage_in_nt<BLOCK>(recs, s + (size_t)base * 4, m);
+		else stage_in<BLOCK>(recs, s + (size_t)base * 4, m);
 		__syncthreads();
 #pragma unroll
 		for (int u = 0; u < R; ++u) {
@@ -412,11 +437,11 @@ __global__ __launch_bounds__(BLOCK) void k_lord_defer(LevelArgs a)
 			if (i >= m) continue;
 			Rec v;
 			lds_get(recs, i, v);
-			if (a.pending) {
-				apply_pending<IS_W, P, NEXT>(v, t[u], pxv[u], a.first_prev != 0);
-				lds_put(recs, i, v);
-			}
-			op.stat(v, lx[base + i], s1, s2);
+			const float x = lx[base + i];
+			if (a.pending) apply_pending<IS_W, P>(v, t[u], pxv[u]);
+			if constexpr (NEXT) add_next_q<IS_W, P>(v, x, first, nx);
+			if (a.pending || NEXT) lds_put(recs, i, v);
+			op.stat(v, x, s1, s2);
 			dsts[i] = nxt[base + i];
 		}
 		__syncthreads();
@@ -446,7 +471,6 @@ __global__ __launch_bounds__(256) void k_lord_defer_post(LevelArgs a)
 	PostT t;
 	t.mo = msj.x; t.so = msj.y; t.sig = sig;
 	t.mu = go ? mu : __builtin_nan("");
-	t.nx = NEXT ? a.ms_next[(size_t)j * a.ms_stride_next] : make_double2(0.0, 0.0);
 	a.tab[i] = t;
 }
 
@@ -458,12 +482,12 @@ __global__ __launch_bounds__(256) void k_lord_defer_flush(LevelArgs a, uint32_t 
 	const uint32_t b = blockIdx.x * 256u;
 	const uint32_t m = min(256u, n - b);
 	double2 *r = reinterpret_cast<double2 *>(a.dst) + (size_t)b * 4;
-	stage_in<256>(recs, r, m);
+	stage_in_nt<256>(recs, r, m);
 	__syncthreads();
 	if (threadIdx.x < m) {
 		Rec v;
 		lds_get(recs, threadIdx.x, v);
-		apply_pending<IS_W, P, NEXT>(v, a.tab[a.lpidx[b + threadIdx.x]], a.lpx[b + threadIdx.x], a.first_prev != 0);
+		apply_pending<IS_W, P>(v, a.tab[a.lpidx[b + threadIdx.x]], a.lpx[b + threadIdx.x]);
 		lds_put(recs, threadIdx.x, v);
 	}
 	__syncthreads();
