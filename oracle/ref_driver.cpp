@@ -25,6 +25,10 @@
 //   sweep   : CPU-baseline timing of the factor sweep (add_main_q + update_v over all
 //             features, fm_learn_vb.h:409-440) on a loaded data set; prints one JSON line.
 //   als/mcmc: MCMC/ALS learner (fm_learn_mcmc_simultaneous.h:50-305), per-iteration trace.
+//   vb_online: the reference's own fm_learn_vb_online_simultaneous (OVBFM, -method vb_online)
+//             with the data setup of libfm.cpp:159-171 (train never loaded, find_max_feature,
+//             libfm.cpp:528-600, restated below); it writes its batch files next to --train, so
+//             callers pass a private copy. "#Iter=" / "free energy" lines + final parameters.
 
 #include <cstdlib>
 #include <cstdio>
@@ -44,6 +48,7 @@
 #include "libfm/src/fm_learn.h"
 #include "libfm/src/fm_learn_mcmc_simultaneous.h"
 #include "libfm/src/fm_learn_vb_simultaneous.h"
+#include "libfm/src/fm_learn_vb_online_simultaneous.h"
 
 static std::string g_dump;
 
@@ -234,6 +239,63 @@ public:
 	}
 };
 
+class RefOVB : public fm_learn_vb_online_simultaneous {
+public:
+	void dump_params(const std::string& tag) {
+		dump_arr(tag + "_mu_w", mu_w_dash.value, mu_w_dash.dim);
+		dump_arr(tag + "_sigma_w", sigma_w_dash.value, sigma_w_dash.dim);
+		dump_arr(tag + "_mu_v", mu_v_dash.value[0], (size_t)mu_v_dash.dim1 * mu_v_dash.dim2);
+		dump_arr(tag + "_sigma_v", sigma_v_dash.value[0], (size_t)sigma_v_dash.dim1 * sigma_v_dash.dim2);
+		dump_arr(tag + "_hyp_sigma_w", sigma_w.value, sigma_w.dim);
+		if (sigma_v.dim1 * sigma_v.dim2 > 0)
+			dump_arr(tag + "_hyp_sigma_v", sigma_v.value[0], (size_t)sigma_v.dim1 * sigma_v.dim2);
+		dump_arr(tag + "_nat_mu_w", natural_mu_w_dash.value, natural_mu_w_dash.dim);
+		dump_arr(tag + "_nat_sigma_w", natural_sigma_w_dash.value, natural_sigma_w_dash.dim);
+		dump_arr(tag + "_nat_mu_v", natural_mu_v_dash.value[0], (size_t)natural_mu_v_dash.dim1 * natural_mu_v_dash.dim2);
+		dump_arr(tag + "_nat_sigma_v", natural_sigma_v_dash.value[0],
+		         (size_t)natural_sigma_v_dash.dim1 * natural_sigma_v_dash.dim2);
+		std::vector<double> steps;
+		for (uint i = 0; i < new_wj.dim; i++) steps.push_back(new_wj(i));
+		for (uint i = 0; i < new_vj.dim; i++) steps.push_back(new_vj(i));
+		dump_arr(tag + "_steps", steps.data(), steps.size());
+		double sc[8] = {alpha, sigma_0, mu_0_dash, sigma_0_dash, natural_mu_0_dash, natural_sigma_0_dash, new_w0, (double)t_w0};
+		dump_arr(tag + "_scalars", sc, 8);
+		dump_arr(tag + "_pred", pred_this.value, pred_this.dim);
+	}
+};
+
+// find_max_feature (libfm.cpp:528-600): counts, largest feature ids and targets of the text files
+static void max_feature_of(const std::string& fn, DataSubset& d) {
+	std::ifstream f(fn.c_str());
+	d.num_cases = 0;
+	d.num_feature = 0;
+	d.min_target = +std::numeric_limits<DATA_FLOAT>::max();
+	d.max_target = -std::numeric_limits<DATA_FLOAT>::max();
+	while (!f.eof()) {
+		int nchar;
+		float rating;
+		uint feature;
+		double value;
+		std::string line;
+		std::getline(f, line);
+		const char* pline = line.c_str();
+		while ((*pline == ' ') || (*pline == 9)) pline++;
+		if ((*pline == 0) || (*pline == '#')) continue;
+		if (sscanf(pline, "%f%n", &rating, &nchar) >= 1) {
+			d.min_target = std::min(rating, d.min_target);
+			d.max_target = std::max(rating, d.max_target);
+			pline += nchar;
+			while (sscanf(pline, "%u:%lf%n", &feature, &value, &nchar) >= 2) {
+				pline += nchar;
+				d.num_feature = std::max(feature, (uint)d.num_feature);
+			}
+		} else {
+			throw "cannot parse line \"" + line + "\"";
+		}
+		d.num_cases++;
+	}
+}
+
 class RefMCMC : public fm_learn_mcmc_simultaneous {
 	// as the reference, trace lines come from _learn's "#Iter=" output at 17 digits
 };
@@ -263,10 +325,17 @@ int main(int argc, char** argv) {
 
 		srand(seed);
 		bool is_mcmc = (mode == "als" || mode == "mcmc");
+		bool is_online = (mode == "vb_online");
 		DataSubset train(0, !is_mcmc, true);
 		DataSubset test(0, !is_mcmc, true);
-		train.load(train_f);
-		test.load(test_f);
+		if (is_online) {   // libfm.cpp:159-171
+			test.load(test_f);
+			max_feature_of(train_f, train);
+			max_feature_of(test_f, test);
+		} else {
+			train.load(train_f);
+			test.load(test_f);
+		}
 		uint num_all_attribute = std::max(train.num_feature, test.num_feature) + 1;
 		DataMetaInfo meta_main(num_all_attribute);
 		if (!meta_f.empty()) meta_main.loadGroupsFromFile(meta_f);
@@ -302,7 +371,16 @@ int main(int argc, char** argv) {
 		dump_arr("init_fm_w", fm.w.value, fm.w.dim);
 		fm_learn* fml;
 		RefVB* vb = NULL;
-		if (is_mcmc) {
+		RefOVB* ovb = NULL;
+		if (is_online) {   // libfm.cpp:312-320
+			ovb = new RefOVB();
+			ovb->num_iter = num_iter;
+			ovb->num_eval_cases = test.num_cases;
+			ovb->training_file = train_f;
+			ovb->testing_file = test_f;
+			ovb->num_batch = atoi(arg(argc, argv, "--batch", "50").c_str());
+			fml = ovb;
+		} else if (is_mcmc) {
 			RefMCMC* m = new RefMCMC();
 			m->num_iter = num_iter;
 			m->num_eval_cases = test.num_cases;
@@ -349,10 +427,15 @@ int main(int argc, char** argv) {
 				m->w_lambda.init(fm.regw);
 				m->v_lambda.init(fm.regv);
 			}
+		} else if (ovb) {
+			ovb->dump_params("init");   // pred_this is not sized yet: an empty dump
 		} else {
 			vb->dump_params("init");
 		}
 		fml->learn(train, test);
+		if (ovb) {
+			ovb->dump_params("final");
+		}
 		if (is_mcmc) {
 			fm_learn_mcmc* m = (fm_learn_mcmc*)fml;
 			dump_arr("final_fm_v", fm.v.value[0], (size_t)fm.v.dim1 * fm.v.dim2);

@@ -600,6 +600,307 @@ void or_vb_update_all(or_vb *st, const or_data *train)
 	if (!st->hyper_skipped) or_vb_free_energy(st, train);
 }
 
+/* ---- OVBFM (see vbfm_oracle.h) ------------------------------------------------------------ */
+int or_ovb_create(or_ovb *st, int k0, int k1, int k, uint32_t D, const uint32_t *attr_group, uint32_t num_batch)
+{
+	memset(st, 0, sizeof(*st));
+	or_vb_create(&st->vb, k0, k1, k, D, attr_group);
+	st->num_batch = num_batch;
+	st->nat_mu_w = (double *)xcalloc(D, 8); st->nat_sig_w = (double *)xcalloc(D, 8);
+	st->nat_mu_v = (double *)xcalloc((size_t)k * D, 8); st->nat_sig_v = (double *)xcalloc((size_t)k * D, 8);
+	st->new_wj = (double *)xcalloc(D, 8); st->new_vj = (double *)xcalloc(D, 8);
+	st->t_wj = (uint32_t *)xcalloc(D, 4); st->t_vj = (uint32_t *)xcalloc(D, 4);
+	st->col_count = (uint32_t *)xcalloc(D, 4);
+	return 0;
+}
+
+void or_ovb_destroy(or_ovb *st)
+{
+	or_vb_destroy(&st->vb);
+	free(st->nat_mu_w); free(st->nat_sig_w); free(st->nat_mu_v); free(st->nat_sig_v);
+	free(st->new_wj); free(st->new_vj); free(st->t_wj); free(st->t_vj); free(st->col_count); free(st->shuffle);
+	memset(st, 0, sizeof(*st));
+}
+
+void or_ovb_init(or_ovb *st, uint32_t seed, double init_stdev, const or_data *train, const or_data *test)
+{
+	or_vb *vb = &st->vb;
+	uint32_t i, D = vb->D;
+	uint64_t p;
+	size_t kd = (size_t)vb->k * D;
+	or_vb_init_params(vb, seed, init_stdev);     /* same draws and order as fm_learn_vb */
+	/* fm_learn_vb_online.h:686-700: learning rates */
+	st->lamda = 0.5;
+	st->t0_w0 = 1; st->t0_wj = 1; st->t0_vj = 1; st->t_w0 = 0;
+	st->new_w0 = pow((double)(st->t0_w0 + st->t_w0), -st->lamda);
+	for (i = 0; i < D; i++) {
+		st->new_wj[i] = pow((double)(st->t0_wj + 0), -st->lamda);
+		st->new_vj[i] = pow((double)(st->t0_vj + 0), -st->lamda);
+		st->t_wj[i] = 0; st->t_vj[i] = 0;
+	}
+	st->nat_mu0 = 0.0;
+	st->nat_sig0 = 1 / vb->sigma_0_dash;
+	/* :706-730: col_count over the train file (every "%u:%lf" entry) */
+	for (i = 0; i < D; i++) st->col_count[i] = 0;
+	for (p = 0; p < train->nnz; p++)
+		if (train->row_feat[p] < D) st->col_count[train->row_feat[p]] += 1;
+	/* :745-758: natural parameters */
+	for (i = 0; i < D; i++) { st->nat_mu_w[i] = vb->mu_w[i] / 0.02; st->nat_sig_w[i] = 1 / vb->sig_w[i]; }
+	for (p = 0; p < kd; p++) { st->nat_mu_v[p] = vb->mu_v[p] / 0.02; st->nat_sig_v[p] = 1 / vb->sig_v[p]; }
+	/* _learn (fm_learn_vb_online_simultaneous.h:55-62) */
+	st->n_total = train->num_rows;
+	st->size_except_last = (uint32_t)ceil((double)train->num_rows / st->num_batch);
+	st->shuffle = (uint32_t *)xcalloc(train->num_rows, 4);
+	for (i = 0; i < train->num_rows; i++) st->shuffle[i] = i + 1;
+	vb->n_test = test->num_rows;
+	vb->e_test = (double *)xcalloc(test->num_rows, 8);
+	vb->q_test = (double *)xcalloc(test->num_rows, 8);
+	vb->pred_test = (double *)xcalloc(test->num_rows, 8);
+	vb->min_target = train->min_target;
+	vb->max_target = train->max_target;
+}
+
+/* update_w0 (fm_learn_vb_online.h:471-497) */
+static void ovb_update_w0(or_ovb *st, const or_data *b, uint32_t size)
+{
+	or_vb *vb = &st->vb;
+	double sigma_dash = vb->sigma_0_dash, mu_dash = vb->mu_0_dash, mu_old = st->nat_mu0, sigma_old = st->nat_sig0;
+	double eta1 = 0.0, eta2 = 0.0, w0_temp;
+	uint32_t i;
+	for (i = 0; i < b->num_rows; i++) {
+		w0_temp = vb->e[i] + vb->mu_0_dash;
+		st->nat_sig0 = ((1 - st->new_w0) * sigma_old) + st->new_w0 * (vb->sigma_0 + size * vb->alpha);
+		st->nat_mu0 = ((1 - st->new_w0) * mu_old) + st->new_w0 * size * vb->alpha * w0_temp;
+		eta1 += st->nat_mu0;
+		eta2 += st->nat_sig0;
+	}
+	st->nat_mu0 = eta1 / b->num_rows;
+	st->nat_sig0 = eta2 / b->num_rows;
+	vb->mu_0_dash = st->nat_mu0 / st->nat_sig0;
+	vb->sigma_0_dash = 1.0 / st->nat_sig0;
+	for (i = 0; i < b->num_rows; i++) {
+		vb->e[i] = vb->e[i] + (mu_dash - vb->mu_0_dash);
+		vb->t[i] = vb->t[i] + (vb->sigma_0_dash - sigma_dash);
+	}
+}
+
+/* update_w (fm_learn_vb_online.h:499-556) for one non-empty column of the batch */
+static void ovb_update_w(or_ovb *st, uint32_t col, double sigma_w, const uint32_t *rows, const float *vals, uint64_t n)
+{
+	or_vb *vb = &st->vb;
+	double *mu = &vb->mu_w[col], *sigma = &vb->sig_w[col];
+	double mu_dash = *mu, sigma_dash = *sigma, mu_old = st->nat_mu_w[col], sigma_old = st->nat_sig_w[col];
+	double eta1 = 0.0, eta2 = 0.0, w_mean, w_sigma_sqr;
+	uint64_t p;
+	for (p = 0; p < n; p++) {
+		float x = vals[p];
+		w_mean = x * (vb->e[rows[p]] + x * *mu);
+		w_sigma_sqr = x * x;
+		st->nat_sig_w[col] = ((1 - st->new_wj[col]) * sigma_old) +
+		                     st->new_wj[col] * (sigma_w + vb->alpha * st->col_count[col] * w_sigma_sqr);
+		st->nat_mu_w[col] = ((1 - st->new_wj[col]) * mu_old) + st->new_wj[col] * st->col_count[col] * vb->alpha * w_mean;
+		eta1 += st->nat_mu_w[col];
+		eta2 += st->nat_sig_w[col];
+	}
+	st->t_wj[col] += (uint32_t)n;
+	st->new_wj[col] = pow((double)(st->t0_wj + st->t_wj[col]), -st->lamda);
+	st->nat_mu_w[col] = eta1 / (uint32_t)n;
+	st->nat_sig_w[col] = eta2 / (uint32_t)n;
+	*mu = st->nat_mu_w[col] / st->nat_sig_w[col];
+	*sigma = 1 / st->nat_sig_w[col];
+	if (isnan(*sigma) || isinf(*sigma)) { vb->nan_sigma_w++; *sigma = sigma_dash; }
+	if (isnan(*mu)) { vb->nan_mu_w++; *mu = mu_dash; return; }
+	if (isinf(*mu)) { vb->inf_mu_w++; *mu = mu_dash; return; }
+	for (p = 0; p < n; p++) {
+		double h = vals[p];
+		uint32_t r = rows[p];
+		vb->e[r] += h * (mu_dash - *mu);
+		vb->t[r] += h * h * (*sigma - sigma_dash);
+	}
+}
+
+/* update_v (fm_learn_vb_online.h:558-627) for one non-empty column of the batch */
+static void ovb_update_v(or_ovb *st, int f, uint32_t col, double sigma_v_g, const uint32_t *rows, const float *vals,
+                         uint64_t n)
+{
+	or_vb *vb = &st->vb;
+	const size_t ix = (size_t)f * vb->D + col;
+	double *mu = &vb->mu_v[ix], *sigma = &vb->sig_v[ix];
+	double mu_dash = *mu, sigma_dash = *sigma, mu_old = st->nat_mu_v[ix], sigma_old = st->nat_sig_v[ix];
+	double eta1 = 0.0, eta2 = 0.0, v_mean, v_sigma_sqr;
+	uint64_t p;
+	for (p = 0; p < n; p++) {
+		uint32_t r = rows[p];
+		float x = vals[p];
+		double h = vb->q[r] - x * *mu;
+		double h1 = vb->tq[r] - x * x * *sigma;
+		v_mean = x * h * (vb->e[r] + x * *mu * h);
+		v_sigma_sqr = x * x * h * h + x * x * h1;
+		st->nat_sig_v[ix] = (1 - st->new_vj[col]) * sigma_old +
+		                    st->new_vj[col] * (sigma_v_g + vb->alpha * st->col_count[col] * v_sigma_sqr);
+		st->nat_mu_v[ix] = ((1 - st->new_vj[col]) * mu_old) + st->new_vj[col] * st->col_count[col] * vb->alpha * v_mean;
+		eta1 += st->nat_mu_v[ix];
+		eta2 += st->nat_sig_v[ix];
+	}
+	st->nat_mu_v[ix] = eta1 / (uint32_t)n;
+	st->nat_sig_v[ix] = eta2 / (uint32_t)n;
+	*mu = st->nat_mu_v[ix] / st->nat_sig_v[ix];
+	*sigma = 1 / st->nat_sig_v[ix];
+	if (isnan(*sigma) || isinf(*sigma)) { *sigma = sigma_dash; vb->nan_sigma_v++; }
+	if (isnan(*mu)) { vb->nan_mu_v++; *mu = mu_dash; return; }
+	if (isinf(*mu)) { vb->inf_mu_v++; *mu = mu_dash; return; }
+	for (p = 0; p < n; p++) {
+		uint32_t r = rows[p];
+		float x = vals[p];
+		double h = x * (vb->q[r] - x * mu_dash);
+		double h1 = x * x * (vb->tq[r] - x * x * sigma_dash);
+		double h2 = x * x * (vb->tz[r] - x * x * mu_dash * mu_dash);
+		vb->q[r] += x * (*mu - mu_dash);
+		vb->tq[r] += x * x * (*sigma - sigma_dash);
+		vb->tz[r] += x * x * (*mu * *mu - mu_dash * mu_dash);
+		vb->e[r] += h * (mu_dash - *mu);
+		vb->t[r] += (h1 + h2) * (*sigma - sigma_dash);
+		vb->t[r] += h1 * (*mu * *mu - mu_dash * mu_dash);
+	}
+}
+
+/* update_all (fm_learn_vb_online.h:354-469) on one batch; _size = all train rows */
+static void ovb_update_all(or_ovb *st, const or_data *b, uint32_t size)
+{
+	or_vb *vb = &st->vb;
+	uint32_t i, g, c;
+	int f;
+	if (vb->k0) ovb_update_w0(st, b, size);
+	if (vb->k1)
+		for (i = 0; i < b->num_feature; i++) {
+			uint64_t cb = b->col_ptr[i], n = b->col_ptr[i + 1] - cb;
+			if (n == 0) continue;
+			ovb_update_w(st, i, vb->sigma_w[vb->attr_group[i]], b->col_row + cb, b->col_val + cb, n);
+		}
+	if (vb->D > 0) {
+		for (f = 0; f < vb->k; f++) {
+			or_vb_add_main_q(vb, b, f);   /* zeroes q, tq, tz first */
+			for (i = 0; i < b->num_feature; i++) {
+				uint64_t cb = b->col_ptr[i], n = b->col_ptr[i + 1] - cb;
+				if (n == 0) continue;
+				ovb_update_v(st, f, i, vb->sigma_v[(size_t)vb->attr_group[i] * vb->k + f], b->col_row + cb,
+				             b->col_val + cb, n);
+				if (f == 0) st->t_vj[i] += (uint32_t)n;
+			}
+		}
+		for (i = 0; i < b->num_feature; i++) st->new_vj[i] = pow((double)(st->t0_vj + st->t_vj[i]), -st->lamda);
+	}
+	{   /* alpha (:413-433) */
+		double alpha_temp = 0.0, alpha_old;
+		for (c = 0; c < b->num_rows; c++) alpha_temp += vb->e[c] * vb->e[c] + vb->t[c];
+		alpha_old = vb->alpha;
+		vb->alpha = (1 - st->new_w0) * alpha_old + st->new_w0 * ((double)b->num_rows / alpha_temp);
+		if (isnan(vb->alpha)) { vb->nan_alpha++; vb->alpha = alpha_old; st->hyper_skipped_any = 1; return; }
+		if (isinf(vb->alpha)) { vb->inf_alpha++; vb->alpha = alpha_old; st->hyper_skipped_any = 1; return; }
+	}
+	vb->sigma_0 = (1 - st->new_w0) * vb->sigma_0 + st->new_w0 * (1.0 / (vb->mu_0_dash * vb->mu_0_dash + vb->sigma_0_dash));
+	{
+		double *tmp = (double *)xcalloc(vb->G, 8);
+		for (i = 0; i < vb->D; i++) tmp[vb->attr_group[i]] += vb->mu_w[i] * vb->mu_w[i] + vb->sig_w[i];
+		for (g = 0; g < vb->G; g++)
+			vb->sigma_w[g] = (1 - st->new_w0) * vb->sigma_w[g] + st->new_w0 * ((double)vb->num_attr_per_group[g] / tmp[g]);
+		for (f = 0; f < vb->k; f++) {
+			const double *v = vb->mu_v + (size_t)f * vb->D, *v1 = vb->sig_v + (size_t)f * vb->D;
+			for (g = 0; g < vb->G; g++) tmp[g] = 0.0;
+			for (i = 0; i < vb->D; i++) tmp[vb->attr_group[i]] += v[i] * v[i] + v1[i];
+			for (g = 0; g < vb->G; g++)
+				vb->sigma_v[(size_t)g * vb->k + f] = (1 - st->new_w0) * vb->sigma_v[(size_t)g * vb->k + f] +
+				                                     st->new_w0 * ((double)vb->num_attr_per_group[g] / tmp[g]);
+		}
+		free(tmp);
+	}
+	st->t_w0 += 1;
+	st->new_w0 = pow((double)(st->t0_w0 + st->t_w0), -st->lamda);
+}
+
+/* the rows of one batch (ascending, the order they are written to the batch file) as a data
+ * set with num_attribute columns (Data::load(file, num_attribute), Data.h:287-454) */
+static void ovb_batch_data(const or_data *train, const uint32_t *rows, uint32_t n, uint32_t D, or_data *out)
+{
+	uint64_t nnz = 0, p, q;
+	uint32_t i, *feat;
+	uint64_t *rp = (uint64_t *)xcalloc((size_t)n + 1, 8);
+	float *val, *y = (float *)xcalloc(n, 4);
+	for (i = 0; i < n; i++) nnz += train->row_ptr[rows[i] + 1] - train->row_ptr[rows[i]];
+	feat = (uint32_t *)xcalloc(nnz, 4);
+	val = (float *)xcalloc(nnz, 4);
+	for (i = 0, q = 0; i < n; i++) {
+		y[i] = train->target[rows[i]];
+		for (p = train->row_ptr[rows[i]]; p < train->row_ptr[rows[i] + 1]; p++, q++) {
+			feat[q] = train->row_feat[p];
+			val[q] = train->row_val[p];
+		}
+		rp[i + 1] = q;
+	}
+	or_data_from_csr(n, nnz, rp, feat, val, y, out);
+	if (out->num_feature < D) {   /* pad the transposed copy to num_attribute columns */
+		uint64_t *cp = (uint64_t *)xcalloc((size_t)D + 1, 8);
+		memcpy(cp, out->col_ptr, ((size_t)out->num_feature + 1) * 8);
+		for (i = out->num_feature + 1; i <= D; i++) cp[i] = cp[out->num_feature];
+		free(out->col_ptr);
+		out->col_ptr = cp;
+		out->num_feature = D;
+	}
+	free(rp); free(feat); free(val); free(y);
+}
+
+void or_ovb_epoch(or_ovb *st, const or_data *train, const or_data *test, double *rmse, double *mae)
+{
+	or_vb *vb = &st->vb;
+	const uint32_t N = st->n_total;
+	uint32_t i, j, c, *rows = (uint32_t *)xcalloc(N, 4);
+	double s_rmse = 0.0, s_mae = 0.0, mx = vb->max_target, mn = vb->min_target;
+	/* std::random_shuffle (libstdc++ stl_algo.h): i from 1, j = rand() % (i + 1) */
+	for (i = 1; i < N; i++) {
+		uint32_t k2 = (uint32_t)(or_rand() % (int32_t)(i + 1));
+		if (k2 != i) { uint32_t t = st->shuffle[i]; st->shuffle[i] = st->shuffle[k2]; st->shuffle[k2] = t; }
+	}
+	for (j = 1; j <= st->num_batch; j++) {
+		uint32_t n = 0;
+		or_data b;
+		for (i = 0; i < N; i++)
+			if ((uint32_t)ceil((double)st->shuffle[i] / st->size_except_last) == j) rows[n++] = i;
+		ovb_batch_data(train, rows, n, vb->D, &b);
+		free(vb->e); free(vb->q); free(vb->t); free(vb->tq); free(vb->tz);
+		vb->e = (double *)xcalloc(n, 8); vb->q = (double *)xcalloc(n, 8); vb->t = (double *)xcalloc(n, 8);
+		vb->tq = (double *)xcalloc(n, 8); vb->tz = (double *)xcalloc(n, 8);
+		vb->n_train = n;
+		or_vb_predict_eterms(vb, &b, vb->e, vb->q);
+		or_vb_predict_t(vb, &b, vb->t, vb->tq, vb->tz);
+		for (c = 0; c < n; c++) vb->e[c] = b.target[c] - vb->e[c];
+		ovb_update_all(st, &b, N);
+		if (j == st->num_batch || j == 1) {
+			const double fe = or_vb_free_energy(vb, &b);
+			if (j == 1) st->fe_first = fe;
+			if (j == st->num_batch) st->fe_last = fe;
+		}
+		or_free_data(&b);
+	}
+	free(rows);
+	or_vb_predict_eterms(vb, test, vb->e_test, vb->q_test);
+	for (c = 0; c < test->num_rows; c++) {
+		double p = vb->e_test[c];
+		p = p < mx ? p : mx;
+		p = mn > p ? mn : p;
+		vb->pred_test[c] = p;
+		p = vb->pred_test[c] * 1.0;
+		p = p < mx ? p : mx;
+		p = mn > p ? mn : p;
+		{
+			double err = p - test->target[c];
+			s_rmse += err * err;
+			s_mae += fabs(err);
+		}
+	}
+	*rmse = sqrt(s_rmse / test->num_rows);
+	*mae = s_mae / test->num_rows;
+}
+
 /* ---- feature-sharded update_all (see vbfm_oracle.h) ----------------------------------- */
 /* partial q-cache of factor f over the features of one shard, ascending id (the order the
  * fused kernels add a row's own entries in), from 0.0 */

@@ -100,6 +100,36 @@ void or_vb_update_all_sharded(or_vb *st, const or_data *train, uint32_t n_train_
  * next factor are summed in shard order. */
 void or_vb_update_all_fsharded(or_vb *st, const or_data *train, int nshards, const int32_t *shard);
 
+/* Online VB (OVBFM, -method vb_online): fm_learn_vb_online (fm_learn_vb_online.h) driven by
+ * fm_learn_vb_online_simultaneous::_learn (fm_learn_vb_online_simultaneous.h:20-270): per
+ * epoch the rows are shuffled into num_batch mini-batches (libstdc++ random_shuffle on the
+ * rand() stream), every batch gets its own caches and one Robbins-Monro natural-gradient
+ * update_all with step sizes (t0 + t)^-0.5. */
+typedef struct {
+	or_vb vb;                        /* parameters, hyper parameters, row caches of the batch */
+	double *nat_mu_w, *nat_sig_w;    /* [D] natural_mu_w_dash, natural_sigma_w_dash */
+	double *nat_mu_v, *nat_sig_v;    /* [k*D] [f][j] */
+	double nat_mu0, nat_sig0;
+	double new_w0, lamda;
+	double *new_wj, *new_vj;         /* [D] */
+	uint32_t *t_wj, *t_vj;           /* [D] */
+	uint32_t t_w0, t0_w0, t0_wj, t0_vj;
+	uint32_t *col_count;             /* [D] entries of each attribute in the whole train file */
+	uint32_t num_batch, n_total, size_except_last;
+	uint32_t *shuffle;               /* [n_total], kept across epochs like the reference's */
+	double fe_first, fe_last;        /* free energy of the epoch's first / last batch */
+	int hyper_skipped_any;
+} or_ovb;
+
+int or_ovb_create(or_ovb *st, int k0, int k1, int k, uint32_t D, const uint32_t *attr_group, uint32_t num_batch);
+void or_ovb_destroy(or_ovb *st);
+/* srand(seed) + the draws of or_vb_init_params, then fm_learn_vb_online::init
+ * (fm_learn_vb_online.h:668-760): natural parameters, step sizes, col_count of `train`.
+ * test sizes the test caches. */
+void or_ovb_init(or_ovb *st, uint32_t seed, double init_stdev, const or_data *train, const or_data *test);
+/* one epoch: shuffle, batches, update_all per batch, test RMSE / MAE */
+void or_ovb_epoch(or_ovb *st, const or_data *train, const or_data *test, double *rmse, double *mae);
+
 /* MCMC / ALS learner state (fm_learn_mcmc.h); ALS = mcmc without sampling / multilevel
  * (libfm.cpp:131-135). Draws come from the or_srand stream, as the reference's rand(). */
 typedef struct {

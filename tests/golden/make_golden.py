@@ -35,6 +35,12 @@ def run_ref(ref, mode, train, test, dim, iters, seed, extra=(), env_extra=None):
     env = dict(os.environ)
     if env_extra:
         env.update(env_extra)
+    if mode == "vb_online":
+        # the reference writes <train>batch<j> next to the train file and opens them through a
+        # dangling c_str() (fm_learn_vb_online_simultaneous.h:80-82): a private copy under a
+        # short (small-string-optimised) name keeps that well defined
+        shutil.copy(train, os.path.join(out, "t"))
+        train = "t"
     cmd = [ref, mode, "--train", train, "--test", test, "--dim", dim, "--iter", str(iters),
            "--seed", str(seed), "--dump", out] + list(extra)
     res = subprocess.run(cmd, cwd=out, env=env, capture_output=True, text=True, check=True)
@@ -80,6 +86,67 @@ def parse_mcmc(stdout):
             trace.append({"iter": int(m.group(1)), "train": float(m.group(2)),
                           "rmse_all": float(m.group(3))})
     return nums, trace
+
+
+def parse_online(stdout):
+    nums, trace, fe = {}, [], []
+    for line in stdout.splitlines():
+        if line.startswith("NUMS "):
+            t = line.split()[1:]
+            nums = {t[i]: float(t[i + 1]) for i in range(0, len(t), 2)}
+        elif line.startswith("free energy "):
+            fe.append(float(line.split()[2]))
+        m = re.match(r"#Iter=\s*(\d+)\s+Test=(\S+)", line)
+        if m:
+            trace.append({"iter": int(m.group(1)), "rmse": float(m.group(2)), "free_energy": fe})
+            fe = []
+    return nums, trace
+
+
+def online_cases(ref):
+    """-method vb_online (OVBFM): fm_learn_vb_online_simultaneous.h, run by the reference itself."""
+    keep = ("final_", "init_mu", "init_nat")
+    for case in ("tiny", "tiny_dup"):
+        d = os.path.join(HERE, case)
+        tr, te = os.path.join(d, "train.libfm"), os.path.join(d, "test.libfm")
+        for nb, it in ((3, 4), (5, 3), (1, 2)):
+            out, arr = run_ref(ref, "vb_online", tr, te, "1,1,3", it, 5, extra=["--batch", str(nb)])
+            nums, trace = parse_online(out)
+            save_case("%s/online_b%d" % (case, nb), nums, trace, {k: arr[k] for k in arr if k.startswith(keep)},
+                      {"dim": "1,1,3", "seed": 5, "init_stdev": 0.1, "iter": it, "batch": nb})
+    d = os.path.join(HERE, "tiny")
+    tr, te, meta = (os.path.join(d, n) for n in ("train.libfm", "test.libfm", "groups.meta"))
+    out, arr = run_ref(ref, "vb_online", tr, te, "0,1,2", 3, 11,
+                       extra=["--meta", meta, "--init_stdev", "0.2", "--batch", "4"])
+    nums, trace = parse_online(out)
+    save_case("tiny/online_meta", nums, trace, {k: arr[k] for k in arr if k.startswith(keep)},
+              {"dim": "0,1,2", "seed": 11, "init_stdev": 0.2, "iter": 3, "batch": 4, "meta": "groups.meta"})
+    tmp = tempfile.mkdtemp()
+    spec = {"n_rows": 20000, "n_fields": 10, "ids_per_field": 200, "seed": 7, "xmode": 1,
+            "test_rows": 2000, "test_seed": 8}
+    rp, f, v, y = synth.generate(spec["n_rows"], spec["n_fields"], spec["ids_per_field"], spec["seed"], 1)
+    synth.write_libfm(os.path.join(tmp, "tr.libfm"), rp, f, v, y)
+    rp, f, v, y = synth.generate(spec["test_rows"], spec["n_fields"], spec["ids_per_field"], spec["test_seed"], 1)
+    synth.write_libfm(os.path.join(tmp, "te.libfm"), rp, f, v, y)
+    out, arr = run_ref(ref, "vb_online", os.path.join(tmp, "tr.libfm"), os.path.join(tmp, "te.libfm"), "1,1,4", 3, 7)
+    nums, trace = parse_online(out)
+    save_case("synth_online", nums, trace, {k: arr[k] for k in arr if k.startswith("final_scalars")},
+              dict(spec, dim="1,1,4", init_stdev=0.1, iter=3, batch=50,
+                   array_sums={k: [float(np.sum(arr[k])), float(np.sum(arr[k] ** 2))] for k in arr}))
+    shutil.rmtree(tmp)
+    sa = os.path.join(HERE, "sa_split")
+    tmp = tempfile.mkdtemp()
+    for part in ("train", "test"):
+        with gzip.open(os.path.join(sa, part + ".libfm.gz"), "rt") as fi, \
+                open(os.path.join(tmp, part + ".libfm"), "w") as fo:
+            fo.write(fi.read())
+    out, arr = run_ref(ref, "vb_online", os.path.join(tmp, "train.libfm"), os.path.join(tmp, "test.libfm"),
+                       "1,1,8", 5, 42)
+    nums, trace = parse_online(out)
+    save_case("sa_online", nums, trace, {k: arr[k] for k in arr if k.startswith("final_scalars")},
+              {"dim": "1,1,8", "seed": 42, "init_stdev": 0.1, "iter": 5, "batch": 50,
+               "array_sums": {k: [float(np.sum(arr[k])), float(np.sum(arr[k] ** 2))] for k in arr}})
+    shutil.rmtree(tmp)
 
 
 def save_case(name, nums, trace, arrays, meta):
@@ -184,7 +251,7 @@ def mcmc_cases(ref):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--ref", default=os.path.join(HERE, "..", "..", "oracle", "_ref", "ref_driver"))
-    ap.add_argument("--only", default="", help="comma list of groups: rng,tiny,meta,synth,sa,mcmc")
+    ap.add_argument("--only", default="", help="comma list of groups: rng,tiny,meta,synth,sa,mcmc,online")
     args = ap.parse_args()
     ref = os.path.abspath(args.ref)
     only = set(filter(None, args.only.split(",")))
@@ -194,7 +261,9 @@ def main():
 
     if want("mcmc"):
         mcmc_cases(ref)
-    if only == {"mcmc"}:
+    if want("online"):
+        online_cases(ref)
+    if only and not only - {"mcmc", "online"}:
         return
 
     # --- RNG known answers: glibc rand() as the reference calls it (random.h:174-176)

@@ -50,6 +50,17 @@ class OrALS(C.Structure):
                 ("tmp_g", P_f64)]
 
 
+class OrOVB(C.Structure):
+    _fields_ = [("vb", OrVB), ("nat_mu_w", P_f64), ("nat_sig_w", P_f64), ("nat_mu_v", P_f64),
+                ("nat_sig_v", P_f64), ("nat_mu0", C.c_double), ("nat_sig0", C.c_double),
+                ("new_w0", C.c_double), ("lamda", C.c_double), ("new_wj", P_f64), ("new_vj", P_f64),
+                ("t_wj", P_u32), ("t_vj", P_u32), ("t_w0", C.c_uint32), ("t0_w0", C.c_uint32),
+                ("t0_wj", C.c_uint32), ("t0_vj", C.c_uint32), ("col_count", P_u32),
+                ("num_batch", C.c_uint32), ("n_total", C.c_uint32), ("size_except_last", C.c_uint32),
+                ("shuffle", P_u32), ("fe_first", C.c_double), ("fe_last", C.c_double),
+                ("hyper_skipped_any", C.c_int)]
+
+
 ALLREDUCE_FN = C.CFUNCTYPE(None, P_f64, C.c_int, C.c_void_p)
 
 _lib = None
@@ -92,6 +103,10 @@ def lib():
                                      P_f64, P_f64, P_f64]
         L.or_als_destroy.argtypes = [C.POINTER(OrALS)]
         L.or_als_configure.argtypes = [C.POINTER(OrALS), C.c_int, C.c_int, C.c_double]
+        L.or_ovb_create.argtypes = [C.POINTER(OrOVB), C.c_int, C.c_int, C.c_int, C.c_uint32, P_u32, C.c_uint32]
+        L.or_ovb_destroy.argtypes = [C.POINTER(OrOVB)]
+        L.or_ovb_init.argtypes = [C.POINTER(OrOVB), C.c_uint32, C.c_double, C.POINTER(OrData), C.POINTER(OrData)]
+        L.or_ovb_epoch.argtypes = [C.POINTER(OrOVB), C.POINTER(OrData), C.POINTER(OrData), P_f64, P_f64]
         L.or_ran_gamma.argtypes = [C.c_double]
         L.or_ran_gamma.restype = C.c_double
         _lib = L
@@ -250,3 +265,41 @@ class ALS:
 def num_all_attribute(train, test):
     """libfm.cpp:215"""
     return max(train.num_feature, test.num_feature) + 1
+
+
+class OVB:
+    """Oracle online VB learner (fm_learn_vb_online + _simultaneous::_learn restated)."""
+
+    def __init__(self, k0, k1, k, D, num_batch, attr_group=None):
+        self.s = OrOVB()
+        self._g = None if attr_group is None else np.ascontiguousarray(attr_group, np.uint32)
+        lib().or_ovb_create(C.byref(self.s), int(k0), int(k1), int(k), int(D),
+                            None if self._g is None else self._g.ctypes.data_as(P_u32), int(num_batch))
+
+    def init(self, seed, init_stdev, train, test):
+        self.train, self.test = train, test
+        lib().or_ovb_init(C.byref(self.s), seed, init_stdev, C.byref(train.d), C.byref(test.d))
+
+    def epoch(self):
+        r, m = C.c_double(), C.c_double()
+        lib().or_ovb_epoch(C.byref(self.s), C.byref(self.train.d), C.byref(self.test.d), C.byref(r), C.byref(m))
+        return r.value, m.value, self.s.fe_first, self.s.fe_last
+
+    def params(self):
+        v, s = self.s.vb, self.s
+        kd = v.k * v.D
+        return {"mu_w": arr(v.mu_w, v.D), "sigma_w": arr(v.sig_w, v.D), "mu_v": arr(v.mu_v, kd),
+                "sigma_v": arr(v.sig_v, kd), "hyp_sigma_w": arr(v.sigma_w, v.G),
+                "hyp_sigma_v": arr(v.sigma_v, v.G * v.k), "nat_mu_w": arr(s.nat_mu_w, v.D),
+                "nat_sigma_w": arr(s.nat_sig_w, v.D), "nat_mu_v": arr(s.nat_mu_v, kd),
+                "nat_sigma_v": arr(s.nat_sig_v, kd),
+                "steps": np.concatenate([arr(s.new_wj, v.D), arr(s.new_vj, v.D)]),
+                "scalars": np.array([v.alpha, v.sigma_0, v.mu_0_dash, v.sigma_0_dash, s.nat_mu0, s.nat_sig0,
+                                     s.new_w0, float(s.t_w0)]),
+                "pred": arr(v.pred_test, v.n_test)}
+
+    def __del__(self):
+        try:
+            lib().or_ovb_destroy(C.byref(self.s))
+        except Exception:
+            pass

@@ -253,3 +253,55 @@ def test_feature_shards_match_level_schedule():
     lv = levels(rp, f, 180)
     present = np.bincount(f, minlength=180) > 0
     np.testing.assert_array_equal(lv[present], (np.arange(180) // 30 + 1)[present])
+
+
+ONLINE_CASES = ["tiny/online_b3", "tiny/online_b5", "tiny/online_b1", "tiny_dup/online_b3", "tiny_dup/online_b5",
+                "tiny_dup/online_b1", "tiny/online_meta", "synth_online", "sa_online"]
+
+
+def run_online_oracle(case, synth_files, sa_split):
+    """OVBFM (-method vb_online) on the oracle. D = largest feature id of train/test + 1: the
+    online path sizes the model from find_max_feature (libfm.cpp:167-170, 528-600)."""
+    t, a = load_case(case)
+    m = t["meta"]
+    if case.startswith("synth"):
+        tr, te = oc.Data(synth_files["train"]), oc.Data(synth_files["test"])
+    elif case.startswith("sa_"):
+        tr, te = oc.Data(sa_split["train"]), oc.Data(sa_split["test"])
+    else:
+        tr, te = _tiny(case.split("/")[0])
+    k0, k1, k = [int(x) for x in m["dim"].split(",")]
+    D = max(tr.num_feature, te.num_feature)
+    assert D == t["nums"]["D"]
+    groups = None
+    if "meta" in m:
+        groups = np.loadtxt(os.path.join(GOLDEN, case.split("/")[0], m["meta"]), dtype=np.uint32)[:D]
+    ovb = oc.OVB(k0, k1, k, D, m["batch"], groups)
+    ovb.init(m["seed"], m["init_stdev"], tr, te)
+    return t, a, ovb, tr, te
+
+
+@pytest.mark.parametrize("case", ONLINE_CASES)
+def test_online_vb_trace_bit_exact(case, synth_files, sa_split):
+    """fm_learn_vb_online_simultaneous::_learn: epoch shuffle (std::random_shuffle on rand()),
+    mini-batches in file order, natural-gradient steps, hyper-parameters, free energy of the
+    first and last batch and the test RMSE -- all equal to the reference's."""
+    t, a, ovb, tr, te = run_online_oracle(case, synth_files, sa_split)
+    if "init_mu_w" in a:
+        p = ovb.params()
+        np.testing.assert_array_equal(p["mu_w"], a["init_mu_w"])
+        np.testing.assert_array_equal(p["nat_mu_v"], a["init_nat_mu_v"])
+    for it, ref in enumerate(t["trace"]):
+        rmse, mae, fe1, fe2 = ovb.epoch()
+        assert rmse == ref["rmse"], (it, rmse, ref["rmse"])
+        fe = [fe1] if t["meta"]["batch"] == 1 else [fe1, fe2]
+        assert fe == ref["free_energy"], (it, fe, ref["free_energy"])
+    p = ovb.params()
+    for key in ("mu_w", "sigma_w", "mu_v", "sigma_v", "hyp_sigma_w", "hyp_sigma_v", "nat_mu_w", "nat_sigma_w",
+                "nat_mu_v", "nat_sigma_v", "steps", "scalars", "pred"):
+        if "final_" + key in a:
+            np.testing.assert_array_equal(p[key], a["final_" + key], err_msg=key)
+    for key, (s1, s2) in t["meta"].get("array_sums", {}).items():
+        if key.startswith("final_"):
+            v = p[key[len("final_"):]]
+            assert float(np.sum(v)) == s1 and float(np.sum(v ** 2)) == s2, key
