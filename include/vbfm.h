@@ -195,6 +195,50 @@ int vbfm_comm_init(vbfm_ctx *ctx, int32_t nranks, int32_t rank, const uint8_t ui
 #define VBFM_SHARD_FEATURES 1
 int vbfm_set_shard_mode(vbfm_ctx *ctx, int32_t mode, int32_t num_shards);
 
+/* ---- online VB learner (-method vb_online, OVBFM) -------------------------------------
+ * Replaces fm_learn_vb_online + fm_learn_vb_online_simultaneous (src/libfm/src/
+ * fm_learn_vb_online.h, fm_learn_vb_online_simultaneous.h:20-290; selected at
+ * src/libfm/libfm.cpp:312-320). vbfm_online_init turns a context made by vbfm_create that holds
+ * its train and test sets into the online learner: the VB learner's initial draws (host or
+ * device replay, the same values), then fm_learn_vb_online::init (natural parameters, step
+ * sizes, col_count). Each vbfm_online_epoch is one iteration of _learn's loop: a
+ * std::random_shuffle of the rows on the reference's rand() stream, num_batch mini-batches
+ * (row r in batch ceil(shuffle[r] / ceil(N / num_batch))), update_all on each batch in turn,
+ * then the test RMSE. num_attribute follows the online CLI: largest feature id of train and
+ * test + 1 (find_max_feature, libfm.cpp:167-170, 528-600). One GPU. A num_batch that leaves a
+ * batch empty is refused (the reference divides by its zero size). */
+#define VBFM_ONLINE_INIT_HOST 0    /* draws on the host (glibc restatement) */
+#define VBFM_ONLINE_INIT_REPLAY 1  /* the same draws on the device (vbfm_init_params_replay) */
+typedef struct {
+	uint32_t num_batch;       /* -batch (libfm.cpp:320; default 50) */
+	uint32_t seed;            /* srand(seed) (libfm.cpp:123-124) */
+	double init_stdev;        /* -init_stdev (draws of fm.v / fm.w that precede the learner's) */
+	int32_t init_mode;        /* VBFM_ONLINE_INIT_* */
+} vbfm_online_config;
+
+typedef struct {
+	double rmse, mae;                              /* test, clipped (:206-245) */
+	double free_energy_first, free_energy_last;    /* "free energy" of batch 1 and batch num_batch (:143-146) */
+	double alpha, sigma_0, mu_0_dash, sigma_0_dash;
+	uint32_t nan_mu_w, nan_sigma_w, inf_mu_w;
+	uint32_t nan_mu_v, nan_sigma_v, inf_mu_v;
+	uint32_t nan_alpha, inf_alpha;
+	uint32_t num_batch;
+	int32_t num_levels;
+	/* device time: regrouping into batches, the batches' update_all, test; ms */
+	double ms_regroup, ms_batches, ms_test, ms_total;
+	uint64_t nnz_train;
+} vbfm_online_stats;
+
+int vbfm_online_init(vbfm_ctx *ctx, const vbfm_online_config *cfg);
+int vbfm_online_epoch(vbfm_ctx *ctx, vbfm_online_stats *out);
+/* the learner's own state: natural parameters ([D], [k*D] f-major as vbfm_params), step sizes
+ * new_wj / new_vj [D], scalars {alpha, sigma_0, mu_0_dash, sigma_0_dash, natural_mu_0_dash,
+ * natural_sigma_0_dash, new_w0, t_w0}; NULL arrays are skipped. vbfm_get_params and
+ * vbfm_get_test_pred serve the online learner as the VB one. */
+int vbfm_online_get_state(vbfm_ctx *ctx, double *nat_mu_w, double *nat_sigma_w, double *nat_mu_v,
+                          double *nat_sigma_v, double *new_wj, double *new_vj, double scalars[8]);
+
 /* ---- MCMC / ALS learner (-method mcmc | als) -------------------------------------------
  * Replaces fm_learn_mcmc / fm_learn_mcmc_simultaneous (src/libfm/src/fm_learn_mcmc.h,
  * src/libfm/src/fm_learn_mcmc_simultaneous.h), regression, without relation blocks.

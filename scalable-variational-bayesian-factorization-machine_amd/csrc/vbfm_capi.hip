@@ -127,7 +127,7 @@ void build_lorder(vbfm_ctx *c, const std::vector<uint64_t> &cp, const std::vecto
 {
 	lord_release(c, true);
 	const int req = layout_request(c);
-	if (req == VBFM_LAYOUT_COLUMN) return;
+	if (req == VBFM_LAYOUT_COLUMN || c->ov) return;   // the online learner sweeps mini-batch columns
 	if (c->shard_mode == VBFM_SHARD_FEATURES) {
 		if (req == VBFM_LAYOUT_LEVEL) throw std::string("the level-ordered row layout does not combine with feature shards");
 		return;
@@ -497,6 +497,13 @@ void sweep_level(vbfm_ctx *c, uint32_t l, bool is_w, int f)
 	if (a.nfeat == 0) return;
 	Range r("level", 2);
 	const size_t p = prof_begin(c, is_w ? 1 : 0);
+	if (c->ov) {
+		// online VB: the level's columns restricted to the mini-batch (column layout, one GPU)
+		ov_level_args(c, a, is_w, f);
+		HIPCHK(vbk::ov_level(a, is_w, c->s));
+		prof_end(c, p);
+		return;
+	}
 	if (c->lord) {
 		// level-ordered store: stream this level's records, move them to the next level's order
 		a.lcp = c->lcp + c->level_ptr[l];
@@ -762,6 +769,7 @@ void vbfm_destroy(vbfm_ctx *c)
 	dfree(c->rows_alt); dfree(c->lcp); dfree(c->lx); dfree(c->lnext); dfree(c->lrow0); dfree(c->lpos0);
 	fs_free(c);
 	mc_free(c);
+	ov_free(c);
 	if (c->comm) ncclCommDestroy(c->comm);
 	for (hipEvent_t e : c->pev) (void)hipEventDestroy(e);
 	for (int i = 0; i < EV_N; i++)
@@ -1006,6 +1014,7 @@ int vbfm_init_caches(vbfm_ctx *c)
 	if (!c) return fail(nullptr, "null context");
 	return guarded(c, [&] {
 		if (c->mc) throw std::string("an MCMC / ALS context: use the vbfm_mcmc_* entry points");
+		if (c->ov) throw std::string("an online VB context: use vbfm_online_epoch");
 		require_train(c);
 		// fm_learn_vb_simultaneous.h:37-44: yhat of train and test, T of train, e = y - yhat
 		rows_row_order(c);
@@ -1125,6 +1134,7 @@ int vbfm_iterate(vbfm_ctx *c, vbfm_iter_stats *o)
 	if (!c) return fail(nullptr, "null context");
 	return guarded(c, [&] {
 		if (c->mc) throw std::string("an MCMC / ALS context: use the vbfm_mcmc_* entry points");
+		if (c->ov) throw std::string("an online VB context: use vbfm_online_epoch");
 		require_train(c);
 		if (!c->e_test) throw std::string("no test data set (vbfm_set_test)");
 		vbfm_iter_stats st;

@@ -16,6 +16,7 @@ extern "C" const char *vbfm_host_last_error(void);
 extern "C" void vbfm_host_set_error(const char *msg);
 
 struct McState;   // vbfm_mcmc_capi.hip
+struct OvState;   // vbfm_online.hip
 
 namespace vbi {
 
@@ -154,6 +155,11 @@ struct vbfm_ctx {
 	RowRec *fs_rows0 = nullptr;    // in-process shards: the rows at the start of a pass
 	bool row_comm() const { return comm && shard_mode == VBFM_SHARD_ROWS; }
 	McState *mc = nullptr;         // set by vbfm_mcmc_init: the context runs the MCMC / ALS learner
+	OvState *ov = nullptr;         // set by vbfm_online_init: the context runs the online VB learner
+	// vbfm_init_params_replay: the draws' seed and the glibc outputs they consumed (after the
+	// warm-up), so that a learner can continue the reference's stream (UINT64_MAX: unknown)
+	uint32_t init_stream_seed = 0;
+	uint64_t init_stream_end = ~0ull;
 };
 
 
@@ -188,6 +194,19 @@ void prof_end(vbfm_ctx *c, size_t a);
 int blocked_predict(const vbfm_ctx *c, const DevData &d);
 float ev_ms(vbfm_ctx *c, int a, int b);
 void mc_free(vbfm_ctx *c);   // vbfm_mcmc_capi.hip
+void ov_free(vbfm_ctx *c);   // vbfm_online.hip
+void glibc_state_at(uint32_t seed, uint64_t pos, uint32_t st[31]);   // vbfm_replay.hip
+// online VB: the per-feature fields of LevelArgs for the w sweep or factor f (vbfm_online.hip)
+void ov_level_args(vbfm_ctx *c, LevelArgs &a, bool is_w, int f);
+// steps of update_all shared with the online learner (vbfm_capi.hip)
+void step_w(vbfm_ctx *c);
+void step_qcache(vbfm_ctx *c, int f);
+void step_v(vbfm_ctx *c, int f);
+double rows_energy(vbfm_ctx *c);
+std::vector<double> param_sums(vbfm_ctx *c, int mode);
+double free_energy(vbfm_ctx *c, double energy);
+void test_predict(vbfm_ctx *c);
+void read_counters(vbfm_ctx *c, vbfm_iter_stats *o);
 void upload_hyp(vbfm_ctx *c);
 void lord_release(vbfm_ctx *c, bool keep_rows);
 void rows_level_order(vbfm_ctx *c);   // records in level-0 order before a sweep (no-op without the store)

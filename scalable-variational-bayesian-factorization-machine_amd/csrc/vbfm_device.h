@@ -83,6 +83,11 @@ struct LevelArgs {
 	PostT *tab;                // posteriors of the previous level (read) / of this level (written)
 	int pending;               // apply the previous level's correction first
 	int first_prev;            // the previous level is level 0 (q-cache restart of its entries)
+	// online VB (vbfm_online.hip): natural-gradient steps on a mini-batch; nat == nullptr: VB
+	double2 *nat;              // natural parameters {mu, sigma} of each feature, laid out like ms
+	double *rho;               // step size of each feature (new_wj / new_vj)
+	const uint32_t *ccount;    // entries of each feature in the whole train set (col_count)
+	uint32_t *tcount;          // w: t_wj (+= batch entries, rho refreshed); v of factor 0: t_vj; else nullptr
 };
 
 // per-level launch description for the MCMC / ALS draws (vbfm_mcmc.hip); parameters are
@@ -221,6 +226,8 @@ hipError_t init_normal_pairs(double2 *ms, size_t n, uint64_t seed, uint64_t stre
 // D) and the device's feature-major double2 pairs ([j][f]); rows = 1 for the w arrays
 hipError_t pack_pairs(const double *a, const double *b, double2 *out, uint32_t rows, size_t D, hipStream_t s);
 hipError_t unpack_pairs(const double2 *in, double *a, double *b, uint32_t rows, size_t D, hipStream_t s);
+// online VB (vbfm_online.hip): one level of the w / v sweep on a mini-batch (column layout)
+hipError_t ov_level(const LevelArgs &a, int is_w, hipStream_t s);
 // MCMC / ALS (vbfm_mcmc.hip); mode 0: fused, 1: statistics only (into a.stats),
 // 2: draw + correction from the (all-reduced) a.stats
 hipError_t mc_v_level(const McArgs &a, int mode, hipStream_t s);

@@ -1,0 +1,775 @@
+// vbfm_online.hip -- the online VB learner (OVBFM, `-method vb_online`): fm_learn_vb_online
+// (src/libfm/src/fm_learn_vb_online.h) driven by fm_learn_vb_online_simultaneous::_learn
+// (src/libfm/src/fm_learn_vb_online_simultaneous.h:20-290), citations relative to
+// /root/reference.
+//
+// The reference writes every epoch's mini-batches to text files and re-parses them; here the
+// train set stays resident in HBM and each epoch regroups it on the device:
+//   1. the epoch's permutation: std::random_shuffle on the reference's rand() stream (host,
+//      the swaps are sequential), uploaded once;
+//   2. batch of row r = ceil(shuffle[r] / size) (:87-95), rows grouped by batch in file order
+//      (stable radix sort) and numbered within their batch;
+//   3. the CSC entries re-keyed to (batch, local row) and stably sorted by batch: inside a batch
+//      the entries stay column-major with ascending rows -- the transposed copy
+//      Data::create_data_t(num_attribute) builds for the batch file (Data.h:511-560);
+//      per-(batch, column) counts give every batch's col_ptr as a slice of one prefix sum;
+//   4. per batch: its rows' CSR gathered for the predictions, then fm_learn_vb_online::
+//      update_all on the batch -- the VB learner's level sweeps with the natural-gradient
+//      posterior (k_ov_*_level below), update_w0 and the hyper-parameter steps on the host.
+// Parallel reductions sum a column's per-entry natural-parameter terms in a tree: equal to the
+// reference's sequential sums up to summation order (every term rounded as the reference
+// rounds it). One GPU: the learner refuses a communicator or feature shards.
+#include <rocprim/device/device_radix_sort.hpp>
+#include <rocprim/device/device_scan.hpp>
+
+#include "vbfm_ctx.h"
+#include "vbfm_math.h"
+#include "vbfm_rng.h"
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <string>
+#include <vector>
+
+using namespace vbi;
+
+namespace {
+
+// fm_learn_vb_online::init (fm_learn_vb_online.h:686-700): fixed learning-rate schedule
+constexpr double LAMDA = 0.5;
+constexpr uint32_t T0 = 1;   // t0_w0 = t0_wj = t0_vj
+
+// ---- mini-batch grouping ------------------------------------------------------------------
+// batch of every row: ceil((double)shuffle[r] / size_except_last) - 1 (:91-94)
+__global__ void k_ov_batch(const uint32_t *sh, uint32_t n, uint32_t size, uint32_t *bat, uint32_t *iota)
+{
+	const uint32_t r = blockIdx.x * 256u + threadIdx.x;
+	if (r >= n) return;
+	bat[r] = (uint32_t)ceil((double)sh[r] / size) - 1u;
+	iota[r] = r;
+}
+
+// position of each row inside its batch
+__global__ void k_ov_local(const uint32_t *rows_sorted, const uint32_t *bat, const uint64_t *rstart, uint32_t n,
+                           uint32_t *loc)
+{
+	const uint32_t p = blockIdx.x * 256u + threadIdx.x;
+	if (p >= n) return;
+	const uint32_t r = rows_sorted[p];
+	loc[r] = p - (uint32_t)rstart[bat[r]];
+}
+
+// every CSC entry keyed by its row's batch, its row renumbered within the batch (the
+// first-entry flag kept: a row's smallest feature is the same in the batch), and the
+// (batch, column) histogram
+__global__ __launch_bounds__(256) void k_ov_entries(const uint64_t *col_ptr, const uint2 *csc, const uint32_t *bat,
+                                                    const uint32_t *loc, uint32_t nf, uint16_t *key, uint2 *val,
+                                                    uint32_t *cnt)
+{
+	const uint32_t j = blockIdx.x;
+	const uint64_t b = col_ptr[j], e = col_ptr[j + 1];
+	for (uint64_t p = b + threadIdx.x; p < e; p += 256) {
+		const uint2 ent = csc[p];
+		const uint32_t r = ent.x & ROW_MASK;
+		const uint32_t bb = bat[r];
+		key[p] = (uint16_t)bb;
+		val[p] = make_uint2(loc[r] | (ent.x & ROW_FIRST), ent.y);
+		atomicAdd(&cnt[(size_t)bb * nf + j], 1u);
+	}
+}
+
+// the batch's rows (global ids, ascending) -> lengths of their CSR rows
+__global__ void k_ov_rowlen(const uint32_t *rows, uint32_t n, const uint64_t *row_ptr, uint64_t *len)
+{
+	const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+	if (i < n) len[i] = row_ptr[rows[i] + 1] - row_ptr[rows[i]];
+}
+
+// one wave per batch row: copy its feature-sorted entries and its target
+__global__ __launch_bounds__(256) void k_ov_gather(const uint32_t *rows, uint32_t n, const uint64_t *row_ptr,
+                                                   const uint2 *csr, const float *target, const uint64_t *rp_b,
+                                                   uint2 *csr_b, float *t_b)
+{
+	const uint32_t i = blockIdx.x * 4u + (threadIdx.x >> 6);
+	const uint32_t lane = threadIdx.x & 63;
+	if (i >= n) return;
+	const uint32_t r = rows[i];
+	const uint64_t b = row_ptr[r], len = row_ptr[r + 1] - b, o = rp_b[i];
+	for (uint64_t p = lane; p < len; p += 64) csr_b[o + p] = csr[b + p];
+	if (lane == 0) t_b[i] = target[r];
+}
+
+// ---- update_w0 (fm_learn_vb_online.h:471-497): sum of the per-row natural-mean terms
+// (1 - new_w0) * mu_old + new_w0 * _size * alpha * (e + mu_0_dash)
+template <int BLOCK>
+__global__ __launch_bounds__(BLOCK) void k_ov_w0_sum(const RowRec *rows, uint32_t n, double keep, double scale,
+                                                     double mu0, double *out)
+{
+	__shared__ double lds[BLOCK / 64];
+	double s = 0.0;
+	for (uint32_t r = blockIdx.x * BLOCK + threadIdx.x; r < n; r += gridDim.x * BLOCK) {
+		const double w0_temp = rows[r].e + mu0;
+		s += keep + scale * w0_temp;
+	}
+	s = block_sum1<BLOCK>(s, lds);
+	if (threadIdx.x == 0) out[blockIdx.x] = s;
+}
+
+// fm_learn_vb_online::init (:706-758): col_count from the train set, natural parameters
+// natural_mu = mu / 0.02, natural_sigma = 1 / sigma
+__global__ void k_ov_ccount(const uint64_t *col_ptr, uint32_t nf, uint32_t D, uint32_t *cc)
+{
+	const uint32_t j = blockIdx.x * 256u + threadIdx.x;
+	if (j < D) cc[j] = j < nf ? (uint32_t)(col_ptr[j + 1] - col_ptr[j]) : 0u;
+}
+
+__global__ void k_ov_nat_init(const double2 *ms, size_t n, double2 *nat)
+{
+	const size_t i = (size_t)blockIdx.x * 256u + threadIdx.x;
+	if (i < n) nat[i] = make_double2(ms[i].x / 0.02, 1 / ms[i].y);
+}
+
+__global__ void k_ov_fill(double *p, uint32_t n, double v)
+{
+	const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+	if (i < n) p[i] = v;
+}
+
+// new_vj(i) = pow(t0_vj + t_vj(i), -lamda) for every attribute (:401-403)
+__global__ void k_ov_steps(const uint32_t *t, double *rho, uint32_t D)
+{
+	const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+	if (i < D) rho[i] = pow((double)(T0 + t[i]), -LAMDA);
+}
+
+// ---- the level sweeps ------------------------------------------------------------------------
+// update_v (fm_learn_vb_online.h:558-627) for the batch's entries of one column per workgroup.
+// The per-entry statistics are VB's (v_stat); each becomes the natural-parameter terms
+//   (1 - new_vj) * sigma_old + new_vj * (sigma_v_g + alpha * col_count * v_sigma_sqr)
+//   (1 - new_vj) * mu_old    + new_vj * col_count * alpha * v_mean
+// whose mean over the entries is the new natural parameter; the correction is VB's (v_apply).
+template <int BLOCK, int P, bool NEXT>
+__global__ __launch_bounds__(BLOCK) void k_ov_v_level(LevelArgs a)
+{
+	__shared__ double lds[2 * (BLOCK / 64)];
+	const uint32_t j = a.feats[blockIdx.x];
+	const uint64_t cb = a.col_ptr[j];
+	const uint32_t n = (uint32_t)(a.col_ptr[j + 1] - cb);
+	if (n == 0) return;   // columns without entries in the batch are skipped (:389-394)
+	const uint2 *col = a.csc + cb;
+	const size_t pi = (size_t)j * a.ms_stride;
+	const double2 msj = a.ms[pi], natj = a.nat[pi];
+	const double mo = msj.x, so = msj.y;
+	const double rho = a.rho[j];
+	const uint32_t cc = a.ccount[j];
+	const double sv_g = a.hyp[(size_t)a.attr_group[j] * a.hyp_stride];
+	const double keep_m = (1 - rho) * natj.x, keep_s = (1 - rho) * natj.y;
+	const double acc = a.alpha * cc;          // alpha * col_count(col)
+	const double rca = rho * cc * a.alpha;    // new_vj(col) * col_count(col) * alpha
+	double2 nx = make_double2(0.0, 0.0);
+	if constexpr (NEXT) nx = a.ms_next[(size_t)j * a.ms_stride_next];
+	double eta1 = 0.0, eta2 = 0.0;
+	for (uint32_t i = threadIdx.x; i < n; i += BLOCK) {
+		const uint2 ent = col[i];
+		Rec v;
+		load_rec(a.rows, ent.x & ROW_MASK, v);
+		double vm = 0.0, vs = 0.0;
+		v_stat(ent_x(ent), E(v), Q<P>(v), TQ<P>(v), mo, so, vm, vs);
+		eta2 += keep_s + rho * (sv_g + acc * vs);
+		eta1 += keep_m + rca * vm;
+	}
+	block_sum2<BLOCK>(eta1, eta2, lds);
+	const double nmu = eta1 / n, nsig = eta2 / n;
+	double mu = nmu / nsig, sig = 1 / nsig;
+	bool go = true;
+	const bool leader = threadIdx.x == 0;
+	if (dnan(sig) || dinf(sig)) {
+		sig = so;
+		if (leader) atomicAdd(&a.counters[CNT_NAN_SIGMA_V], 1u);
+	}
+	if (dnan(mu)) {
+		if (leader) atomicAdd(&a.counters[CNT_NAN_MU_V], 1u);
+		mu = mo;
+		go = false;
+	} else if (dinf(mu)) {
+		if (leader) atomicAdd(&a.counters[CNT_INF_MU_V], 1u);
+		mu = mo;
+		go = false;
+	}
+	if (leader) {
+		a.nat[pi] = make_double2(nmu, nsig);
+		a.ms[pi] = make_double2(mu, sig);
+		if (a.tcount) a.tcount[j] += n;   // t_vj(i) += size at factor 0 (:396-399)
+	}
+	if (!go && !NEXT) return;
+	if (a.dup[j]) {
+		__syncthreads();
+		if (leader)
+			for (uint32_t i = 0; i < n; ++i) {
+				const uint2 ent = col[i];
+				Rec v;
+				load_rec(a.rows, ent.x & ROW_MASK, v);
+				v_apply<P, NEXT>(v, ent_x(ent), (ent.x & a.first_mask) != 0, go, mo, so, mu, sig, nx);
+				store_rec(a.rows, ent.x & ROW_MASK, v);
+			}
+		return;
+	}
+	for (uint32_t i = threadIdx.x; i < n; i += BLOCK) {
+		const uint2 ent = col[i];
+		Rec v;
+		load_rec(a.rows, ent.x & ROW_MASK, v);
+		v_apply<P, NEXT>(v, ent_x(ent), (ent.x & a.first_mask) != 0, go, mo, so, mu, sig, nx);
+		store_rec(a.rows, ent.x & ROW_MASK, v);
+	}
+}
+
+// update_w (fm_learn_vb_online.h:499-556): as above with VB's w statistics; t_wj / new_wj are
+// advanced by the column itself (:519-520)
+template <int BLOCK, bool NEXT>
+__global__ __launch_bounds__(BLOCK) void k_ov_w_level(LevelArgs a)
+{
+	__shared__ double lds[2 * (BLOCK / 64)];
+	const uint32_t j = a.feats[blockIdx.x];
+	const uint64_t cb = a.col_ptr[j];
+	const uint32_t n = (uint32_t)(a.col_ptr[j + 1] - cb);
+	if (n == 0) return;   // (:364-368)
+	const uint2 *col = a.csc + cb;
+	const size_t pi = (size_t)j * a.ms_stride;
+	const double2 msj = a.ms[pi], natj = a.nat[pi];
+	const double mo = msj.x, so = msj.y;
+	const double rho = a.rho[j];
+	const uint32_t cc = a.ccount[j];
+	const double sw_g = a.hyp[(size_t)a.attr_group[j] * a.hyp_stride];
+	const double keep_m = (1 - rho) * natj.x, keep_s = (1 - rho) * natj.y;
+	const double acc = a.alpha * cc;
+	const double rca = rho * cc * a.alpha;
+	double2 nx = make_double2(0.0, 0.0);
+	if constexpr (NEXT) nx = a.ms_next[(size_t)j * a.ms_stride_next];
+	double eta1 = 0.0, eta2 = 0.0;
+	for (uint32_t i = threadIdx.x; i < n; i += BLOCK) {
+		const uint2 ent = col[i];
+		const float x = ent_x(ent);
+		const double w_mean = x * (a.rows[ent.x & ROW_MASK].e + x * mo);
+		const double w_sigma_sqr = x * x;   // fp32 product
+		eta2 += keep_s + rho * (sw_g + acc * w_sigma_sqr);
+		eta1 += keep_m + rca * w_mean;
+	}
+	block_sum2<BLOCK>(eta1, eta2, lds);
+	const double nmu = eta1 / n, nsig = eta2 / n;
+	double mu = nmu / nsig, sig = 1 / nsig;
+	bool go = true;
+	const bool leader = threadIdx.x == 0;
+	if (dnan(sig) || dinf(sig)) {
+		if (leader) atomicAdd(&a.counters[CNT_NAN_SIGMA_W], 1u);
+		sig = so;
+	}
+	if (dnan(mu)) {
+		if (leader) atomicAdd(&a.counters[CNT_NAN_MU_W], 1u);
+		mu = mo;
+		go = false;
+	} else if (dinf(mu)) {
+		if (leader) atomicAdd(&a.counters[CNT_INF_MU_W], 1u);
+		mu = mo;
+		go = false;
+	}
+	if (leader) {
+		a.nat[pi] = make_double2(nmu, nsig);
+		a.ms[pi] = make_double2(mu, sig);
+		const uint32_t t = a.tcount[j] + n;
+		a.tcount[j] = t;
+		a.rho[j] = pow((double)(T0 + t), -LAMDA);
+	}
+	if (!go && !NEXT) return;
+	if (a.dup[j]) {
+		__syncthreads();
+		if (leader)
+			for (uint32_t i = 0; i < n; ++i) {
+				const uint2 ent = col[i];
+				Rec v;
+				load_rec(a.rows, ent.x & ROW_MASK, v);
+				w_apply<NEXT>(v, ent_x(ent), (ent.x & a.first_mask) != 0, go, mo, so, mu, sig, nx);
+				store_rec(a.rows, ent.x & ROW_MASK, v);
+			}
+		return;
+	}
+	for (uint32_t i = threadIdx.x; i < n; i += BLOCK) {
+		const uint2 ent = col[i];
+		Rec v;
+		load_rec(a.rows, ent.x & ROW_MASK, v);
+		w_apply<NEXT>(v, ent_x(ent), (ent.x & a.first_mask) != 0, go, mo, so, mu, sig, nx);
+		store_rec(a.rows, ent.x & ROW_MASK, v);
+	}
+}
+
+inline unsigned grid_of(uint64_t n, unsigned block = 256) { return (unsigned)((n + block - 1) / block); }
+
+}  // namespace
+
+// ------------------------------------------------------------------------------------------
+namespace vbk {
+hipError_t ov_level(const LevelArgs &a, int is_w, hipStream_t s)
+{
+	if (a.nfeat == 0) return hipSuccess;
+	const bool nx = a.ms_next != nullptr;
+	const bool small = a.avg_len <= 96;
+	if (is_w) {
+		if (small) {
+			if (nx) k_ov_w_level<64, true><<<a.nfeat, 64, 0, s>>>(a);
+			else k_ov_w_level<64, false><<<a.nfeat, 64, 0, s>>>(a);
+		} else {
+			if (nx) k_ov_w_level<256, true><<<a.nfeat, 256, 0, s>>>(a);
+			else k_ov_w_level<256, false><<<a.nfeat, 256, 0, s>>>(a);
+		}
+		return hipGetLastError();
+	}
+#define OV_V(B, P, N) k_ov_v_level<B, P, N><<<a.nfeat, B, 0, s>>>(a)
+	if (small) {
+		if (a.slot == 0) { if (nx) OV_V(64, 0, true); else OV_V(64, 0, false); }
+		else { if (nx) OV_V(64, 1, true); else OV_V(64, 1, false); }
+	} else {
+		if (a.slot == 0) { if (nx) OV_V(256, 0, true); else OV_V(256, 0, false); }
+		else { if (nx) OV_V(256, 1, true); else OV_V(256, 1, false); }
+	}
+#undef OV_V
+	return hipGetLastError();
+}
+}  // namespace vbk
+
+// ------------------------------------------------------------------------------------------
+struct OvState {
+	uint32_t num_batch = 50;
+	uint32_t n_total = 0;          // total_cases
+	uint32_t size = 0;             // size_except_last = ceil(N / num_batch)
+	vbrng::Glibc stream;           // the reference's rand() after the initial draws
+	std::vector<uint32_t> shuffle; // kept across epochs (:58-62)
+	double2 *nat_w = nullptr, *nat_v = nullptr;   // natural_{mu,sigma}_{w,v}_dash, laid out like ms_w / ms_v
+	double *new_wj = nullptr, *new_vj = nullptr;
+	uint32_t *t_wj = nullptr, *t_vj = nullptr, *ccount = nullptr;
+	double nat_mu0 = 0.0, nat_sig0 = 0.0, new_w0 = 1.0;
+	uint32_t t_w0 = 0;
+	// epoch regrouping
+	uint32_t *sh_d = nullptr, *bat_d = nullptr, *iota_d = nullptr, *rows_sorted = nullptr, *bat_sorted = nullptr,
+	         *loc_d = nullptr;
+	uint16_t *key_in = nullptr, *key_out = nullptr;
+	uint2 *ent_sorted = nullptr;   // all entries, batch-major, column-major inside a batch
+	uint2 *ent_tmp = nullptr;
+	uint32_t *cnt = nullptr;       // [num_batch * nf] (batch, column) entry counts
+	uint64_t *gptr = nullptr;      // [num_batch * nf + 1] their prefix sums: col_ptr of every batch
+	std::vector<uint64_t> rstart;  // [num_batch + 1] first sorted row of each batch
+	uint64_t *rstart_d = nullptr;
+	void *tmp = nullptr;
+	size_t tmp_bytes = 0;
+	// the batch being processed
+	uint32_t cap_rows = 0;
+	uint64_t cap_nnz = 0;
+	uint64_t *rp_b = nullptr, *len_b = nullptr;
+	uint2 *csr_b = nullptr;
+	float *t_b = nullptr;
+	RowRec *rows_b = nullptr;
+	hipEvent_t ev[4] = {};
+};
+
+namespace vbi {
+
+void ov_free(vbfm_ctx *c)
+{
+	if (!c->ov) return;
+	OvState &o = *c->ov;
+	dfree(o.nat_w); dfree(o.nat_v); dfree(o.new_wj); dfree(o.new_vj); dfree(o.t_wj); dfree(o.t_vj);
+	dfree(o.ccount); dfree(o.sh_d); dfree(o.bat_d); dfree(o.iota_d); dfree(o.rows_sorted); dfree(o.bat_sorted);
+	dfree(o.loc_d); dfree(o.key_in); dfree(o.key_out); dfree(o.ent_sorted); dfree(o.ent_tmp); dfree(o.cnt);
+	dfree(o.gptr); dfree(o.rstart_d); dfree(o.tmp); dfree(o.rp_b); dfree(o.len_b); dfree(o.csr_b); dfree(o.t_b);
+	dfree(o.rows_b);
+	for (hipEvent_t e : o.ev)
+		if (e) (void)hipEventDestroy(e);
+	delete c->ov;
+	c->ov = nullptr;
+}
+
+void ov_level_args(vbfm_ctx *c, LevelArgs &a, bool is_w, int f)
+{
+	OvState &o = *c->ov;
+	a.nat = is_w ? o.nat_w : o.nat_v + f;
+	a.rho = is_w ? o.new_wj : o.new_vj;
+	a.ccount = o.ccount;
+	a.tcount = is_w ? o.t_wj : (f == 0 ? o.t_vj : nullptr);
+	a.avg_len = a.avg_len / std::max(o.num_batch, 1u);   // the batch's share of the mean column
+}
+
+}  // namespace vbi
+
+namespace {
+
+// temp storage of rocprim calls: grow on demand
+void *ov_tmp(OvState &o, size_t bytes)
+{
+	if (bytes > o.tmp_bytes) {
+		dfree(o.tmp);
+		o.tmp = dalloc<uint8_t>(bytes);
+		o.tmp_bytes = bytes;
+	}
+	return o.tmp;
+}
+
+// steps 1-3 of the file header: the epoch's batches
+void ov_regroup(vbfm_ctx *c)
+{
+	OvState &o = *c->ov;
+	const uint32_t N = o.n_total, nf = c->tr.nf, nb = o.num_batch;
+	const uint64_t nnz = c->tr.nnz;
+	// std::random_shuffle(shuffle, shuffle + N) (libstdc++: i from 1, j = rand() % (i + 1))
+	for (uint32_t i = 1; i < N; i++) {
+		const uint32_t j = (uint32_t)(o.stream.next() % (int32_t)(i + 1));
+		if (j != i) std::swap(o.shuffle[i], o.shuffle[j]);
+	}
+	HIPCHK(hipMemcpyAsync(o.sh_d, o.shuffle.data(), (size_t)N * 4, hipMemcpyHostToDevice, c->s));
+	k_ov_batch<<<grid_of(N), 256, 0, c->s>>>(o.sh_d, N, o.size, o.bat_d, o.iota_d);
+	HIPCHK(hipGetLastError());
+	int bits = 1;
+	while ((1u << bits) < nb) bits++;
+	size_t tb = 0;
+	HIPCHK(rocprim::radix_sort_pairs(nullptr, tb, o.bat_d, o.bat_sorted, o.iota_d, o.rows_sorted, (size_t)N, 0, bits,
+	                                 c->s));
+	HIPCHK(rocprim::radix_sort_pairs(ov_tmp(o, tb), tb, o.bat_d, o.bat_sorted, o.iota_d, o.rows_sorted, (size_t)N, 0,
+	                                 bits, c->s));
+	// batch row counts: the shuffle is a permutation of 1..N, so batch b holds the rows with
+	// shuffle values in (b*size, (b+1)*size]
+	o.rstart.assign((size_t)nb + 1, 0);
+	for (uint32_t b = 0; b <= nb; b++) o.rstart[b] = std::min<uint64_t>((uint64_t)b * o.size, N);
+	HIPCHK(hipMemcpyAsync(o.rstart_d, o.rstart.data(), ((size_t)nb + 1) * 8, hipMemcpyHostToDevice, c->s));
+	k_ov_local<<<grid_of(N), 256, 0, c->s>>>(o.rows_sorted, o.bat_d, o.rstart_d, N, o.loc_d);
+	HIPCHK(hipGetLastError());
+	// entries
+	HIPCHK(hipMemsetAsync(o.cnt, 0, (size_t)nb * nf * 4, c->s));
+	if (nf) k_ov_entries<<<nf, 256, 0, c->s>>>(c->tr.col_ptr, c->tr.csc, o.bat_d, o.loc_d, nf, o.key_in, o.ent_tmp, o.cnt);
+	HIPCHK(hipGetLastError());
+	tb = 0;
+	HIPCHK(rocprim::radix_sort_pairs(nullptr, tb, o.key_in, o.key_out, o.ent_tmp, o.ent_sorted, (size_t)nnz, 0, bits,
+	                                 c->s));
+	HIPCHK(rocprim::radix_sort_pairs(ov_tmp(o, tb), tb, o.key_in, o.key_out, o.ent_tmp, o.ent_sorted, (size_t)nnz, 0,
+	                                 bits, c->s));
+	tb = 0;
+	const size_t ncnt = (size_t)nb * nf;
+	HIPCHK(rocprim::exclusive_scan(nullptr, tb, o.cnt, o.gptr, (uint64_t)0, ncnt, rocprim::plus<uint64_t>(), c->s));
+	HIPCHK(rocprim::exclusive_scan(ov_tmp(o, tb), tb, o.cnt, o.gptr, (uint64_t)0, ncnt, rocprim::plus<uint64_t>(),
+	                               c->s));
+	HIPCHK(hipMemcpyAsync(o.gptr + ncnt, &nnz, 8, hipMemcpyHostToDevice, c->s));
+	sync(c);   // nnz (host) must outlive the copy
+}
+
+void ov_batch_capacity(vbfm_ctx *c, uint32_t n, uint64_t nnz)
+{
+	OvState &o = *c->ov;
+	if (n > o.cap_rows) {
+		dfree(o.rp_b); dfree(o.len_b); dfree(o.t_b); dfree(o.rows_b);
+		o.rp_b = dalloc<uint64_t>((size_t)n + 1);
+		o.len_b = dalloc<uint64_t>((size_t)n + 1);
+		o.t_b = dalloc<float>(n);
+		o.rows_b = dalloc<RowRec>(n);
+		o.cap_rows = n;
+	}
+	if (nnz > o.cap_nnz) {
+		dfree(o.csr_b);
+		o.csr_b = dalloc<uint2>(nnz);
+		o.cap_nnz = nnz;
+	}
+}
+
+// update_w0 (fm_learn_vb_online.h:471-497) on the batch in c->rows / c->tr
+void ov_step_w0(vbfm_ctx *c)
+{
+	OvState &o = *c->ov;
+	const uint32_t n = c->tr.n;
+	const double sigma_dash = c->s0d, mu_dash = c->mu0, mu_old = o.nat_mu0, sigma_old = o.nat_sig0;
+	const double size = (double)o.n_total;
+	// natural_sigma_0_dash is the same every row: the reference adds it n times
+	const double nsig_i = ((1 - o.new_w0) * sigma_old) + o.new_w0 * (c->sigma_0 + o.n_total * c->alpha);
+	double eta2 = 0.0;
+	for (uint32_t i = 0; i < n; i++) eta2 += nsig_i;
+	k_ov_w0_sum<256><<<c->RED_BLOCKS, 256, 0, c->s>>>(c->rows, n, (1 - o.new_w0) * mu_old, o.new_w0 * size * c->alpha,
+	                                                  c->mu0, c->red_d);
+	HIPCHK(hipGetLastError());
+	const double eta1 = finish_sum(c, c->RED_BLOCKS);
+	o.nat_mu0 = eta1 / n;
+	o.nat_sig0 = eta2 / n;
+	c->mu0 = o.nat_mu0 / o.nat_sig0;
+	c->s0d = 1.0 / o.nat_sig0;
+	HIPCHK(vbk::w0_apply(c->rows, n, mu_dash - c->mu0, c->s0d - sigma_dash, c->s));
+}
+
+// the hyper-parameter steps of update_all (fm_learn_vb_online.h:408-467); false on the early
+// return of a NaN / inf alpha
+bool ov_step_hyper(vbfm_ctx *c, uint32_t *nan_alpha, uint32_t *inf_alpha)
+{
+	OvState &o = *c->ov;
+	const double alpha_temp = rows_energy(c);
+	const double alpha_old = c->alpha;
+	c->alpha = (1 - o.new_w0) * alpha_old + o.new_w0 * ((double)c->tr.n / alpha_temp);
+	if (std::isnan(c->alpha)) { (*nan_alpha)++; c->alpha = alpha_old; return false; }
+	if (std::isinf(c->alpha)) { (*inf_alpha)++; c->alpha = alpha_old; return false; }
+	c->sigma_0 = (1 - o.new_w0) * c->sigma_0 + o.new_w0 * (1.0 / (c->mu0 * c->mu0 + c->s0d));
+	std::vector<double> seg = param_sums(c, 0);
+	for (uint32_t g = 0; g < c->G; g++)
+		c->hyp_w[g] = (1 - o.new_w0) * c->hyp_w[g] + o.new_w0 * ((double)c->per_group[g] / seg[g]);
+	for (int f = 0; f < c->k; f++)
+		for (uint32_t g = 0; g < c->G; g++) {
+			double &h = c->hyp_v[(size_t)g * c->k + f];
+			h = (1 - o.new_w0) * h + o.new_w0 * ((double)c->per_group[g] / seg[(size_t)(f + 1) * c->G + g]);
+		}
+	upload_hyp(c);
+	o.t_w0 += 1;
+	o.new_w0 = std::pow((double)(T0 + o.t_w0), -LAMDA);
+	return true;
+}
+
+}  // namespace
+
+// =========================================================================================
+extern "C" {
+
+int vbfm_online_init(vbfm_ctx *c, const vbfm_online_config *cfg)
+{
+	if (!c || !cfg) return fail(c, "vbfm_online_init: null argument");
+	return guarded(c, [&] {
+		if (c->mc) throw std::string("an MCMC / ALS context cannot run the online VB learner");
+		if (c->comm || c->shard_mode == VBFM_SHARD_FEATURES)
+			throw std::string("the online VB learner runs on one GPU (no communicator, no feature shards)");
+		if (!c->rows) throw std::string("no train data set (vbfm_set_train)");
+		if (!c->e_test) throw std::string("no test data set (vbfm_set_test)");
+		if (cfg->init_mode != VBFM_ONLINE_INIT_HOST && cfg->init_mode != VBFM_ONLINE_INIT_REPLAY)
+			throw std::string("unknown init mode");
+		const uint32_t N = c->tr.n, nb = cfg->num_batch;
+		if (nb == 0 || nb > 65536) throw std::string("num_batch must be in 1..65536");
+		if (N == 0) throw std::string("empty train set");
+		const uint32_t size = (uint32_t)std::ceil((double)N / nb);   // :56-57
+		const uint32_t used = (uint32_t)std::ceil((double)N / size);
+		if (used < nb)
+			throw std::string("num_batch ") + std::to_string(nb) + " leaves batches " + std::to_string(used + 1) + ".." +
+			    std::to_string(nb) + " of " + std::to_string(N) +
+			    " rows empty (the reference divides by their zero size and crashes)";
+		ov_free(c);
+		c->ov = new OvState();
+		try {
+			OvState &o = *c->ov;
+			// the column layout (one level sweep per batch, no level-ordered store)
+			lord_release(c, false);
+			c->sched_ready = false;
+			require_train(c);
+			for (hipEvent_t &e : o.ev) HIPCHK(hipEventCreate(&e));
+			o.num_batch = nb;
+			o.n_total = N;
+			o.size = size;
+			// the initial draws (libfm.cpp:123-124, 259-274, 313; fm_learn_vb_online.h:736-741): the
+			// VB learner's, then the stream continues into the epoch shuffles
+			const size_t kd = (size_t)c->k * c->D;
+			if (cfg->init_mode == VBFM_ONLINE_INIT_HOST) {
+				std::vector<double> mw(c->D), sw(c->D, .02), mv(kd), sv(kd, .02), hw(c->G), hv((size_t)c->G * c->k);
+				vbfm_params p = {mw.data(), sw.data(), mv.data(), sv.data(), hw.data(), hv.data(), 0, 0, 0, 0};
+				vbrng::Glibc &rng = o.stream;
+				rng.seed_with(cfg->seed);
+				for (size_t i = 0; i < kd; i++) (void)rng.gaussian(0, cfg->init_stdev);       // fm.v (fm_model.h:97)
+				for (uint32_t i = 0; i < c->D; i++) (void)rng.gaussian(0, cfg->init_stdev);   // fm.w (libfm.cpp:313)
+				for (uint32_t i = 0; i < c->D; i++) mw[i] = 0.1 * rng.gaussian(0, 1);         // mu_w_dash.init_normal
+				for (size_t i = 0; i < kd; i++) mv[i] = 0.1 * rng.gaussian(0, 1);            // mu_v_dash.init_normal
+				std::fill(hw.begin(), hw.end(), 1.0);
+				std::fill(hv.begin(), hv.end(), 1.0);
+				p.alpha = 1.0; p.sigma_0 = 1.0; p.mu_0_dash = 0.0; p.sigma_0_dash = 0.02;
+				if (vbfm_set_params(c, &p)) throw std::string(c->err);
+			} else {
+				if (vbfm_init_params_replay(c, cfg->seed, cfg->init_stdev, nullptr, nullptr)) throw std::string(c->err);
+				uint32_t st[31];
+				glibc_state_at(cfg->seed, c->init_stream_end, st);
+				o.stream.set_chrono_state(st);
+			}
+			// fm_learn_vb_online::init (:686-758)
+			const uint32_t D = c->D, nf = c->tr.nf;
+			o.nat_w = dalloc<double2>(D);
+			o.nat_v = dalloc<double2>(kd);
+			o.new_wj = dalloc<double>(D);
+			o.new_vj = dalloc<double>(D);
+			o.t_wj = dalloc<uint32_t>(D);
+			o.t_vj = dalloc<uint32_t>(D);
+			o.ccount = dalloc<uint32_t>(D);
+			HIPCHK(hipMemsetAsync(o.t_wj, 0, (size_t)D * 4, c->s));
+			HIPCHK(hipMemsetAsync(o.t_vj, 0, (size_t)D * 4, c->s));
+			const double rho0 = std::pow((double)(T0 + 0), -LAMDA);
+			if (D) {
+				k_ov_fill<<<grid_of(D), 256, 0, c->s>>>(o.new_wj, D, rho0);
+				k_ov_fill<<<grid_of(D), 256, 0, c->s>>>(o.new_vj, D, rho0);
+				k_ov_ccount<<<grid_of(D), 256, 0, c->s>>>(c->tr.col_ptr, nf, D, o.ccount);
+				k_ov_nat_init<<<grid_of(D), 256, 0, c->s>>>(c->ms_w, D, o.nat_w);
+			}
+			if (kd) k_ov_nat_init<<<grid_of(kd), 256, 0, c->s>>>(c->ms_v, kd, o.nat_v);
+			HIPCHK(hipGetLastError());
+			o.t_w0 = 0;
+			o.new_w0 = std::pow((double)(T0 + o.t_w0), -LAMDA);
+			o.nat_mu0 = 0.0;
+			o.nat_sig0 = 1 / c->s0d;
+			o.shuffle.resize(N);
+			for (uint32_t i = 0; i < N; i++) o.shuffle[i] = i + 1;
+			// the epoch regrouping buffers
+			const uint64_t nnz = c->tr.nnz;
+			o.sh_d = dalloc<uint32_t>(N); o.bat_d = dalloc<uint32_t>(N); o.iota_d = dalloc<uint32_t>(N);
+			o.rows_sorted = dalloc<uint32_t>(N); o.bat_sorted = dalloc<uint32_t>(N); o.loc_d = dalloc<uint32_t>(N);
+			o.key_in = dalloc<uint16_t>(nnz); o.key_out = dalloc<uint16_t>(nnz);
+			o.ent_tmp = dalloc<uint2>(nnz); o.ent_sorted = dalloc<uint2>(nnz);
+			o.cnt = dalloc<uint32_t>((size_t)nb * nf);
+			o.gptr = dalloc<uint64_t>((size_t)nb * nf + 1);
+			o.rstart_d = dalloc<uint64_t>((size_t)nb + 1);
+			c->q_ready[0] = c->q_ready[1] = -1;
+			sync(c);
+		} catch (...) {
+			ov_free(c);
+			throw;
+		}
+	});
+}
+
+int vbfm_online_epoch(vbfm_ctx *c, vbfm_online_stats *out)
+{
+	if (!c) return fail(nullptr, "null context");
+	return guarded(c, [&] {
+		if (!c->ov) throw std::string("not an online VB context (vbfm_online_init)");
+		OvState &o = *c->ov;
+		vbfm_online_stats st;
+		memset(&st, 0, sizeof(st));
+		HIPCHK(hipMemsetAsync(c->counters, 0, CNT_N * 4, c->s));
+		Range r_ep("vbfm_online_epoch");
+		HIPCHK(hipEventRecord(o.ev[0], c->s));
+		ov_regroup(c);
+		HIPCHK(hipEventRecord(o.ev[1], c->s));
+		const uint32_t nb = o.num_batch, nf = c->tr.nf;
+		std::vector<uint64_t> eoff((size_t)nb + 1);
+		for (uint32_t b = 0; b <= nb; b++)
+			HIPCHK(hipMemcpyAsync(&eoff[b], o.gptr + (size_t)b * nf, 8, hipMemcpyDeviceToHost, c->s));
+		sync(c);
+		const DevData full = c->tr;
+		RowRec *const rows_full = c->rows;
+		const uint64_t n_global_full = c->n_global;
+		auto restore = [&] {
+			c->tr = full;
+			c->rows = rows_full;
+			c->n_global = n_global_full;
+			c->q_ready[0] = c->q_ready[1] = -1;
+		};
+		try {
+			for (uint32_t b = 0; b < nb; b++) {
+				Range r_b("batch");
+				const uint32_t n = (uint32_t)(o.rstart[b + 1] - o.rstart[b]);
+				const uint64_t nnz = eoff[b + 1] - eoff[b];
+				ov_batch_capacity(c, n, nnz);
+				const uint32_t *brows = o.rows_sorted + o.rstart[b];
+				// the batch's CSR (rows ascending = the batch file's order)
+				k_ov_rowlen<<<grid_of(n), 256, 0, c->s>>>(brows, n, full.row_ptr, o.len_b);
+				HIPCHK(hipGetLastError());
+				HIPCHK(hipMemsetAsync(o.len_b + n, 0, 8, c->s));
+				size_t tb = 0;
+				HIPCHK(vbk::exclusive_scan_u64(nullptr, &tb, o.len_b, o.rp_b, (size_t)n + 1, c->s));
+				HIPCHK(vbk::exclusive_scan_u64(ov_tmp(o, tb), &tb, o.len_b, o.rp_b, (size_t)n + 1, c->s));
+				k_ov_gather<<<grid_of(n, 4), 256, 0, c->s>>>(brows, n, full.row_ptr, full.csr, full.target, o.rp_b,
+				                                            o.csr_b, o.t_b);
+				HIPCHK(hipGetLastError());
+				DevData bv = full;
+				bv.n = n;
+				bv.nnz = nnz;
+				bv.col_ptr = o.gptr + (size_t)b * nf;
+				bv.csc = o.ent_sorted;
+				bv.row_ptr = o.rp_b;
+				bv.csr = o.csr_b;
+				bv.target = o.t_b;
+				c->tr = bv;
+				c->rows = o.rows_b;
+				c->n_global = n;
+				c->q_ready[0] = c->q_ready[1] = -1;
+				// fresh caches of the batch (:111-139)
+				const int bl = blocked_predict(c, c->tr);
+				HIPCHK(vbk::predict_e(c->tr.row_ptr, c->tr.csr, c->ms_v, c->ms_w, c->k, c->k1, c->k0, c->mu0,
+				                      c->scratch_n, n, bl, c->s));
+				HIPCHK(vbk::predict_t(c->tr.row_ptr, c->tr.csr, c->ms_v, c->ms_w, c->k, c->k1, c->k0, c->s0d, c->rows,
+				                      n, bl, c->s));
+				HIPCHK(vbk::residual_init(c->rows, c->scratch_n, c->tr.target, n, c->s));
+				// update_all(train1, train.num_cases) (fm_learn_vb_online.h:354-469)
+				if (c->k0) ov_step_w0(c);
+				if (c->k1) step_w(c);
+				if (c->D > 0) {
+					for (int f = 0; f < c->k; f++) {
+						step_qcache(c, f);
+						step_v(c, f);
+					}
+					k_ov_steps<<<grid_of(c->D), 256, 0, c->s>>>(o.t_vj, o.new_vj, c->D);
+					HIPCHK(hipGetLastError());
+				}
+				ov_step_hyper(c, &st.nan_alpha, &st.inf_alpha);
+				// free energy of the first and the last batch (:143-146)
+				if (b == 0 || b + 1 == nb) {
+					const double fe = free_energy(c, rows_energy(c));
+					if (b == 0) st.free_energy_first = fe;
+					if (b + 1 == nb) st.free_energy_last = fe;
+				}
+				restore();
+			}
+		} catch (...) {
+			restore();
+			throw;
+		}
+		HIPCHK(hipEventRecord(o.ev[2], c->s));
+		// test prediction and metrics (:190-245)
+		test_predict(c);
+		const double mn = c->min_target, mx = c->max_target;
+		HIPCHK(vbk::test_metrics(c->e_test, c->te.target, c->te.n, mn, mx, c->pred_test, c->red_d, c->RED_BLOCKS, c->s));
+		HIPCHK(hipMemcpyAsync(c->red_h.data(), c->red_d, 2 * c->RED_BLOCKS * 8, hipMemcpyDeviceToHost, c->s));
+		HIPCHK(hipEventRecord(o.ev[3], c->s));
+		sync(c);
+		double tm[2] = {0.0, 0.0};
+		for (uint32_t i = 0; i < c->RED_BLOCKS; i++) { tm[0] += c->red_h[2 * i]; tm[1] += c->red_h[2 * i + 1]; }
+		st.rmse = std::sqrt(tm[0] / c->te.n);
+		st.mae = tm[1] / c->te.n;
+		st.alpha = c->alpha; st.sigma_0 = c->sigma_0; st.mu_0_dash = c->mu0; st.sigma_0_dash = c->s0d;
+		vbfm_iter_stats it;
+		memset(&it, 0, sizeof(it));
+		read_counters(c, &it);
+		st.nan_mu_w = it.nan_mu_w; st.nan_sigma_w = it.nan_sigma_w; st.inf_mu_w = it.inf_mu_w;
+		st.nan_mu_v = it.nan_mu_v; st.nan_sigma_v = it.nan_sigma_v; st.inf_mu_v = it.inf_mu_v;
+		st.num_batch = nb;
+		st.num_levels = (int32_t)nlevels(c);
+		float ms = 0.f;
+		HIPCHK(hipEventElapsedTime(&ms, o.ev[0], o.ev[1])); st.ms_regroup = ms;
+		HIPCHK(hipEventElapsedTime(&ms, o.ev[1], o.ev[2])); st.ms_batches = ms;
+		HIPCHK(hipEventElapsedTime(&ms, o.ev[2], o.ev[3])); st.ms_test = ms;
+		HIPCHK(hipEventElapsedTime(&ms, o.ev[0], o.ev[3])); st.ms_total = ms;
+		st.nnz_train = c->tr.nnz;
+		if (out) *out = st;
+	});
+}
+
+int vbfm_online_get_state(vbfm_ctx *c, double *nat_mu_w, double *nat_sigma_w, double *nat_mu_v, double *nat_sigma_v,
+                          double *new_wj, double *new_vj, double scalars[8])
+{
+	if (!c) return fail(nullptr, "null context");
+	return guarded(c, [&] {
+		if (!c->ov) throw std::string("not an online VB context (vbfm_online_init)");
+		OvState &o = *c->ov;
+		const size_t kd = (size_t)c->k * c->D;
+		double *tmp = dalloc<double>(2 * std::max(kd, (size_t)c->D));
+		HIPCHK(vbk::unpack_pairs(o.nat_w, tmp, tmp + c->D, 1, c->D, c->s));
+		sync(c);
+		if (nat_mu_w) HIPCHK(hipMemcpy(nat_mu_w, tmp, (size_t)c->D * 8, hipMemcpyDeviceToHost));
+		if (nat_sigma_w) HIPCHK(hipMemcpy(nat_sigma_w, tmp + c->D, (size_t)c->D * 8, hipMemcpyDeviceToHost));
+		if (kd) {
+			HIPCHK(vbk::unpack_pairs(o.nat_v, tmp, tmp + kd, (uint32_t)c->k, c->D, c->s));
+			sync(c);
+			if (nat_mu_v) HIPCHK(hipMemcpy(nat_mu_v, tmp, kd * 8, hipMemcpyDeviceToHost));
+			if (nat_sigma_v) HIPCHK(hipMemcpy(nat_sigma_v, tmp + kd, kd * 8, hipMemcpyDeviceToHost));
+		}
+		dfree(tmp);
+		if (new_wj) HIPCHK(hipMemcpy(new_wj, o.new_wj, (size_t)c->D * 8, hipMemcpyDeviceToHost));
+		if (new_vj) HIPCHK(hipMemcpy(new_vj, o.new_vj, (size_t)c->D * 8, hipMemcpyDeviceToHost));
+		if (scalars) {
+			const double s[8] = {c->alpha, c->sigma_0, c->mu0, c->s0d, o.nat_mu0, o.nat_sig0, o.new_w0, (double)o.t_w0};
+			memcpy(scalars, s, sizeof(s));
+		}
+	});
+}
+
+}  // extern "C"

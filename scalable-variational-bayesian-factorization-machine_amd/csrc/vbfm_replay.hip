@@ -107,6 +107,8 @@ __global__ void k_leva_flags(const int32_t *out, const Seg *seg, uint32_t nseg, 
 struct Route {
 	uint64_t n_fmv, n_fmw, D, k;   // normals of fm.v, fm.w; then D of mu_w, k*D of mu_v
 	double init_stdev;
+	uint64_t total;                // normals drawn in all
+	uint64_t *end;                 // stream position after the last one (the next rand() call)
 };
 
 // the idx-th normal to its destination (fm_model.h:97, libfm.cpp:307, fm_learn_vb.h:709-711)
@@ -118,6 +120,7 @@ __global__ void k_leva_route(const int32_t *out, const Seg *seg, uint32_t nseg, 
 	if (i >= nattempt || !flag[i]) return;
 	uint64_t idx = offs[i];
 	const uint64_t s = attempt_pos(seg, nseg, i);
+	if (idx + 1 == r.total) *r.end = s + 2;
 	const double u = uniform_of(out[s]);
 	const double v = 1.7156 * (uniform_of(out[s + 1]) - 0.5);
 	const double g = v / u;
@@ -169,6 +172,21 @@ Mat jump_matrix(uint64_t p)
 
 }  // namespace
 
+namespace vbi {
+// the glibc window (y_{n-31..n-1}) after srand(seed), the warm-up and `pos` more outputs
+void glibc_state_at(uint32_t seed, uint64_t pos, uint32_t st[31])
+{
+	uint32_t st0[31];
+	vbrng::glibc_warm_state(seed, st0);
+	const Mat J = jump_matrix(pos);
+	for (int i = 0; i < 31; i++) {
+		uint32_t a = 0;
+		for (int j = 0; j < 31; j++) a += J[i * 31 + j] * st0[j];
+		st[i] = a;
+	}
+}
+}  // namespace vbi
+
 extern "C" int vbfm_init_params_replay(vbfm_ctx *c, uint32_t seed, double init_stdev, double *fm_v_out,
                                        double *fm_w_out)
 {
@@ -183,6 +201,10 @@ extern "C" int vbfm_init_params_replay(vbfm_ctx *c, uint32_t seed, double init_s
 		r.D = D;
 		r.k = (uint64_t)c->k;
 		const uint64_t nnorm = r.n_fmv + r.n_fmw + D + kD;
+		r.total = nnorm;
+		uint64_t end_h = 0;
+		r.end = dalloc<uint64_t>(1);
+		HIPCHK(hipMemsetAsync(r.end, 0, 8, c->s));
 		uint32_t st0[31];
 		vbrng::glibc_warm_state(seed, st0);
 		double *fmv_d = fm_v_out && r.n_fmv ? dalloc<double>(r.n_fmv) : nullptr;
@@ -281,6 +303,10 @@ extern "C" int vbfm_init_params_replay(vbfm_ctx *c, uint32_t seed, double init_s
 			nuni = nuni + nuni / 4;
 		}
 		// attributes past the drawn ones keep their values; fm_learn_vb::init scalars (:693-712)
+		HIPCHK(hipMemcpy(&end_h, r.end, 8, hipMemcpyDeviceToHost));
+		dfree(r.end);
+		c->init_stream_seed = seed;
+		c->init_stream_end = end_h;   // outputs after the warm-up that the draws consumed
 		if (fmv_d) HIPCHK(hipMemcpy(fm_v_out, fmv_d, r.n_fmv * 8, hipMemcpyDeviceToHost));
 		if (fmw_d) HIPCHK(hipMemcpy(fm_w_out, fmw_d, r.n_fmw * 8, hipMemcpyDeviceToHost));
 		dfree(fmv_d); dfree(fmw_d);

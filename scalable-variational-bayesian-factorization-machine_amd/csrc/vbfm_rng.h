@@ -91,6 +91,14 @@ public:
 	{
 		for (int i = 0; i < 31; i++) st[i] = (uint32_t)r_[(f_ + i) % 31];
 	}
+	// the inverse: continue from the window st (the front pointer on st[0], the rear 3 ahead of
+	// it wrapped: r[f] + r[b] = y_{n-31} + y_{n-3})
+	void set_chrono_state(const uint32_t st[31])
+	{
+		for (int i = 0; i < 31; i++) r_[i] = (int32_t)st[i];
+		f_ = 0;
+		b_ = 28;
+	}
 
 private:
 	int32_t r_[31];

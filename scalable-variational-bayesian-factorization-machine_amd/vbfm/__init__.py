@@ -1,7 +1,8 @@
 """vbfm -- Python host side of libvbfm.so (the MI355X VB factorization machine).
 
-Mirrors the reference's learner interface for `-method vb` (FMLearnVB) and
-`-method mcmc | als` (FMLearnMCMC) so that driver code reads like
+Mirrors the reference's learner interface for `-method vb` (FMLearnVB),
+`-method vb_online` (FMLearnVBOnline) and `-method mcmc | als` (FMLearnMCMC) so that driver
+code reads like
 the reference's main() (src/libfm/libfm.cpp:137-511):
 
     train = DataSubset.load("train.libfm")            # Data::load          (Data.h:106-283)
@@ -107,6 +108,27 @@ class McmcStats(C.Structure):
         return {k: getattr(self, k) for k, _ in self._fields_}
 
 
+ONLINE_INIT_HOST, ONLINE_INIT_REPLAY = 0, 1
+
+
+class OnlineConfig(C.Structure):
+    _fields_ = [("num_batch", C.c_uint32), ("seed", C.c_uint32), ("init_stdev", C.c_double),
+                ("init_mode", C.c_int32)]
+
+
+class OnlineStats(C.Structure):
+    _fields_ = ([("rmse", C.c_double), ("mae", C.c_double), ("free_energy_first", C.c_double),
+                 ("free_energy_last", C.c_double), ("alpha", C.c_double), ("sigma_0", C.c_double),
+                 ("mu_0_dash", C.c_double), ("sigma_0_dash", C.c_double)]
+                + [(n, C.c_uint32) for n in ("nan_mu_w", "nan_sigma_w", "inf_mu_w", "nan_mu_v", "nan_sigma_v",
+                                             "inf_mu_v", "nan_alpha", "inf_alpha", "num_batch")]
+                + [("num_levels", C.c_int32), ("ms_regroup", C.c_double), ("ms_batches", C.c_double),
+                   ("ms_test", C.c_double), ("ms_total", C.c_double), ("nnz_train", C.c_uint64)])
+
+    def as_dict(self):
+        return {k: getattr(self, k) for k, _ in self._fields_}
+
+
 class HostData(C.Structure):
     _fields_ = [("num_rows", C.c_uint32), ("num_feature", C.c_uint32), ("nnz", C.c_uint64),
                 ("min_target", C.c_float), ("max_target", C.c_float), ("target", P_f32),
@@ -122,7 +144,8 @@ EXPORTS = ["vbfm_abi_version", "vbfm_last_error", "vbfm_create", "vbfm_destroy",
            "vbfm_set_layout", "vbfm_get_layout", "vbfm_set_shard_mode",
            "vbfm_comm_unique_id", "vbfm_comm_init", "vbfm_load_data", "vbfm_free_host_data", "vbfm_save_data",
            "vbfm_init_params_host", "vbfm_mcmc_init", "vbfm_mcmc_set_params", "vbfm_mcmc_get_params",
-           "vbfm_mcmc_init_caches", "vbfm_mcmc_iterate", "vbfm_mcmc_get_test_pred", "vbfm_mcmc_factor_sweep"]
+           "vbfm_mcmc_init_caches", "vbfm_mcmc_iterate", "vbfm_mcmc_get_test_pred", "vbfm_mcmc_factor_sweep",
+           "vbfm_online_init", "vbfm_online_epoch", "vbfm_online_get_state"]
 
 _lib = None
 
@@ -181,6 +204,9 @@ def lib():
         L.vbfm_mcmc_iterate.argtypes = [V, C.POINTER(McmcStats)]
         L.vbfm_mcmc_get_test_pred.argtypes = [V, C.c_int32, P_f64]
         L.vbfm_mcmc_factor_sweep.argtypes = [V, P_f64]
+        L.vbfm_online_init.argtypes = [V, C.POINTER(OnlineConfig)]
+        L.vbfm_online_epoch.argtypes = [V, C.POINTER(OnlineStats)]
+        L.vbfm_online_get_state.argtypes = [V, P_f64, P_f64, P_f64, P_f64, P_f64, P_f64, P_f64]
         _lib = L
     return _lib
 
@@ -270,6 +296,12 @@ class DataSubset:
 def num_all_attribute(train, test):
     """libfm.cpp:215"""
     return max(train.num_feature, test.num_feature) + 1
+
+
+def num_all_attribute_online(train, test):
+    """-method vb_online: find_max_feature leaves the largest feature ids in num_feature
+    (libfm.cpp:167-170, 528-600), so num_attribute = largest id of train and test + 1."""
+    return max(train.num_feature, test.num_feature)
 
 
 def load_meta(filename, num_attribute):
@@ -556,3 +588,56 @@ class FMLearnMCMC(FMLearnVB):
         ms = C.c_double()
         _check(lib().vbfm_mcmc_factor_sweep(self._ctx, C.byref(ms)), self._ctx)
         return ms.value
+
+
+class FMLearnVBOnline(FMLearnVB):
+    """fm_learn_vb_online_simultaneous on one MI355X (src/libfm/src/fm_learn_vb_online.h,
+    fm_learn_vb_online_simultaneous.h): OVBFM, mini-batch natural-gradient VB.
+
+        fml = FMLearnVBOnline(1, 1, 8, num_all_attribute_online(train, test), ...)
+        fml.set_data(train, test)
+        fml.init(seed=42, init_stdev=0.1, num_batch=50)   # fm.init ... fml->init()
+        for st in fml.epochs(20): print(st.rmse)           # _learn's loop
+    """
+
+    def __init__(self, k0=1, k1=1, num_factor=8, num_attribute=0, attr_group=None,
+                 min_target=1.0, max_target=5.0, device=0):
+        super().__init__(k0, k1, num_factor, num_attribute, attr_group, min_target, max_target, device,
+                         layout="column")
+
+    def init(self, seed, init_stdev=0.1, num_batch=50, replay=False):
+        """srand(seed); the VB learner's initial draws; fm_learn_vb_online::init (needs set_data first)."""
+        cfg = OnlineConfig(num_batch, seed, init_stdev, ONLINE_INIT_REPLAY if replay else ONLINE_INIT_HOST)
+        _check(lib().vbfm_online_init(self._ctx, C.byref(cfg)), self._ctx)
+        self.num_batch = num_batch
+
+    def epoch(self):
+        st = OnlineStats()
+        _check(lib().vbfm_online_epoch(self._ctx, C.byref(st)), self._ctx)
+        self.num_iter_done += 1
+        return st
+
+    def epochs(self, num_iter):
+        for _ in range(num_iter):
+            yield self.epoch()
+
+    def learn(self, train, test, num_iter, seed=1, init_stdev=0.1, num_batch=50):
+        """fm_learn_vb_online::learn -> _learn: yields the OnlineStats of every epoch."""
+        self.set_data(train, test)
+        self.init(seed, init_stdev, num_batch)
+        return self.epochs(num_iter)
+
+    def iterate(self):
+        return self.epoch()
+
+    def init_caches(self):
+        raise VbfmError("the online learner builds its caches per mini-batch (use epoch())")
+
+    def online_state(self):
+        D, kd = self.D, self.k * self.D
+        out = {"nat_mu_w": np.zeros(D), "nat_sigma_w": np.zeros(D), "nat_mu_v": np.zeros(kd),
+               "nat_sigma_v": np.zeros(kd), "new_wj": np.zeros(D), "new_vj": np.zeros(D), "scalars": np.zeros(8)}
+        _check(lib().vbfm_online_get_state(self._ctx, *[_ptr(out[k], P_f64) for k in
+                                                        ("nat_mu_w", "nat_sigma_w", "nat_mu_v", "nat_sigma_v",
+                                                         "new_wj", "new_vj", "scalars")]), self._ctx)
+        return out

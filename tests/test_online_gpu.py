@@ -1,0 +1,125 @@
+"""Parity of the online VB learner (OVBFM, `-method vb_online`) on the GPU.
+
+Reference: fm_learn_vb_online_simultaneous::_learn run by the compiled reference itself
+(tests/golden/*online*, made by tests/golden/make_golden.py through oracle/_ref/ref_driver);
+the oracle (oracle/vbfm_oracle.c or_ovb_*) reproduces those fixtures bit for bit
+(tests/test_oracle_golden.py::test_online_vb_trace_bit_exact) and serves here for the
+parameters the fixtures do not hold.
+
+Tolerance: the epoch shuffle, the batch grouping and every per-row sum are exact; a column's
+natural-parameter terms and a batch's sums are added in a tree on the device, sequentially in
+the reference -- REL = 1e-9 relative (observed ~1e-13), far inside the north star's 1e-6.
+"""
+import os
+
+import numpy as np
+import pytest
+
+import oracle_ctypes as oc
+import vbfm
+from conftest import GOLDEN, load_case
+
+pytestmark = pytest.mark.gpu
+REL = 1e-9
+
+CASES = ["tiny/online_b3", "tiny/online_b5", "tiny/online_b1", "tiny_dup/online_b3", "tiny_dup/online_b5",
+         "tiny/online_meta", "synth_online", "sa_online"]
+
+
+def rel_err(a, b):
+    a, b = np.asarray(a, dtype=np.float64), np.asarray(b, dtype=np.float64)
+    scale = max(1e-300, float(np.max(np.abs(b))) if b.size else 1.0)
+    return float(np.max(np.abs(a - b))) / scale if b.size else 0.0
+
+
+def close(a, b, tol=REL, what=""):
+    assert rel_err(a, b) <= tol, (what, rel_err(a, b))
+
+
+def case_files(case, synth_files, sa_split):
+    if case.startswith("synth"):
+        return synth_files["train"], synth_files["test"]
+    if case.startswith("sa_"):
+        return sa_split["train"], sa_split["test"]
+    d = os.path.join(GOLDEN, case.split("/")[0])
+    return os.path.join(d, "train.libfm"), os.path.join(d, "test.libfm")
+
+
+def make_learner(case, synth_files, sa_split, replay=False, batch=None):
+    t, a = load_case(case)
+    m = t["meta"]
+    trp, tep = case_files(case, synth_files, sa_split)
+    train, test = vbfm.DataSubset.load(trp), vbfm.DataSubset.load(tep)
+    k0, k1, k = [int(x) for x in m["dim"].split(",")]
+    D = vbfm.num_all_attribute_online(train, test)
+    groups = None
+    if "meta" in m:
+        groups = vbfm.load_meta(os.path.join(GOLDEN, case.split("/")[0], m["meta"]), D)
+    fml = vbfm.FMLearnVBOnline(k0, k1, k, D, attr_group=groups, min_target=train.min_target,
+                               max_target=train.max_target)
+    fml.set_data(train, test)
+    fml.init(m["seed"], m["init_stdev"], batch or m["batch"], replay=replay)
+    return t, a, fml, (trp, tep, groups, D)
+
+
+def oracle_run(trp, tep, groups, D, m, epochs):
+    tr, te = oc.Data(trp), oc.Data(tep)
+    k0, k1, k = [int(x) for x in m["dim"].split(",")]
+    o = oc.OVB(k0, k1, k, D, m["batch"], None if groups is None else groups[:D])
+    o.init(m["seed"], m["init_stdev"], tr, te)
+    out = [o.epoch() for _ in range(epochs)]
+    return o, out, (tr, te)
+
+
+@pytest.mark.parametrize("case", CASES)
+def test_online_trace_vs_reference(case, synth_files, sa_split):
+    """Test RMSE and the two free energies of every epoch against the reference's own run; the
+    final parameters, natural parameters and step sizes against its dumps / the oracle."""
+    t, a, fml, (trp, tep, groups, D) = make_learner(case, synth_files, sa_split)
+    m = t["meta"]
+    for it, ref in enumerate(t["trace"]):
+        st = fml.epoch()
+        close(st.rmse, ref["rmse"], what=("rmse", it))
+        fe = [st.free_energy_first] if m["batch"] == 1 else [st.free_energy_first, st.free_energy_last]
+        close(fe, ref["free_energy"], what=("free energy", it))
+    p, s = fml.get_params(), fml.online_state()
+    o, _, keep = oracle_run(trp, tep, groups, D, m, len(t["trace"]))
+    op = o.params()
+    for key in ("mu_w", "sigma_w", "mu_v", "sigma_v", "hyp_sigma_w", "hyp_sigma_v"):
+        ref = a["final_" + key] if "final_" + key in a else op[key]
+        close(p[key], ref, what=key)
+    for key, okey in (("nat_mu_w", "nat_mu_w"), ("nat_sigma_w", "nat_sigma_w"), ("nat_mu_v", "nat_mu_v"),
+                      ("nat_sigma_v", "nat_sigma_v")):
+        close(s[key], a.get("final_" + okey, op[okey]), what=key)
+    close(np.concatenate([s["new_wj"], s["new_vj"]]), a.get("final_steps", op["steps"]), what="steps")
+    close(s["scalars"], a.get("final_scalars", op["scalars"]), what="scalars")
+    close(fml.predict(), a.get("final_pred", op["pred"]), what="pred")
+
+
+def test_online_replay_init_is_host_init(synth_files, sa_split):
+    """The device replay of the initial draws continues the rand() stream at the same place:
+    the epoch shuffles, hence the whole run, are identical to the host-drawn start."""
+    _, _, f1, _ = make_learner("sa_online", synth_files, sa_split)
+    _, _, f2, _ = make_learner("sa_online", synth_files, sa_split, replay=True)
+    for _ in range(2):
+        s1, s2 = f1.epoch(), f2.epoch()
+        assert s1.rmse == s2.rmse and s1.free_energy_last == s2.free_energy_last
+    np.testing.assert_array_equal(f1.get_params()["mu_v"], f2.get_params()["mu_v"])
+
+
+def test_online_refuses_empty_batches(synth_files, sa_split):
+    """24 rows in 7 batches of ceil(24/7) = 4 leave batch 7 empty: the reference divides by its
+    zero size (NaN, then a crash); the library refuses the configuration up front."""
+    with pytest.raises(vbfm.VbfmError, match="empty"):
+        make_learner("tiny/online_b3", synth_files, sa_split, batch=7)
+
+
+def test_online_deterministic(synth_files, sa_split):
+    """Two runs from the same seed agree bit for bit (fixed reduction trees, host shuffle)."""
+    runs = []
+    for _ in range(2):
+        _, _, f, _ = make_learner("synth_online", synth_files, sa_split)
+        st = [f.epoch() for _ in range(2)]
+        runs.append(([s.rmse for s in st], f.get_params()["mu_v"]))
+    assert runs[0][0] == runs[1][0]
+    np.testing.assert_array_equal(runs[0][1], runs[1][1])
