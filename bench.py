@@ -97,9 +97,11 @@ def main():
     ap.add_argument("--config", default="c4", choices=sorted(CONFIGS))
     ap.add_argument("--rows", type=int, default=0, help="override rows per GPU")
     ap.add_argument("--k", type=int, default=0, help="override factors")
-    ap.add_argument("--method", default="vb", choices=["vb", "mcmc", "als"],
+    ap.add_argument("--method", default="vb", choices=["vb", "mcmc", "als", "vb_online"],
                     help="vb: the metric (fm_learn_vb); mcmc / als: config 5's Gibbs draw_v path "
-                         "(device counter-based RNG streams), reported in the same unit")
+                         "(device counter-based RNG streams); vb_online: OVBFM epochs of --batch "
+                         "mini-batches (one GPU); all reported in the same unit")
+    ap.add_argument("--batch", type=int, default=50, help="vb_online: mini-batches per epoch (-batch)")
     ap.add_argument("--shard", default="rows", choices=["rows", "features"],
                     help="rows: exact row shards, each rank its own rows (weak scaling, default); "
                          "features: the north star's column partition, every rank all rows (strong "
@@ -133,8 +135,13 @@ def main():
     torch.cuda.set_device(local_rank)
 
     t0 = time.time()
-    mc = args.method != "vb"
-    if mc:
+    online = args.method == "vb_online"
+    mc = args.method in ("mcmc", "als")
+    if online:
+        if world > 1:
+            raise SystemExit("vb_online runs on one GPU")
+        fml = vbfm.FMLearnVBOnline(1, 1, k, D, min_target=1.0, max_target=5.0, device=local_rank)
+    elif mc:
         fml = vbfm.FMLearnMCMC(1, 1, k, D, min_target=1.0, max_target=5.0, device=local_rank, method=args.method,
                                layout=args.layout)
     else:
@@ -148,12 +155,19 @@ def main():
         obj = [vbfm.FMLearnVB.comm_unique_id() if rank == 0 else None]
         dist.broadcast_object_list(obj, src=0)
         fml.comm_init(world, rank, obj[0])
-    fml.init_device(42)
+    if not online:
+        fml.init_device(42)
     dseed = 0 if fshard else rank          # feature shards: every rank holds the same rows
     fml.synth(0, N, F, S, seed=1000 + dseed, xmode=0)
     fml.synth(1, n_test, F, S, seed=500000 + dseed, xmode=0)
-    fml.init_caches()
-    fml.set_profiling(True)
+    if online:
+        # the reference's initial draws generated on the device, the rand() stream continued
+        # into the epoch shuffles (vbfm_online_init, VBFM_ONLINE_INIT_REPLAY)
+        fml.init(42, 0.1, args.batch, replay=True)
+    else:
+        fml.init_caches()
+    if not online:   # per-launch event pairs: the online epoch has num_batch * k * levels launches
+        fml.set_profiling(True)
     layout = fml.layout()
     log("rank %d: setup %.1f s (N=%d F=%d S=%d k=%d, %s layout)" % (rank, time.time() - t0, N, F, S, k, layout))
 
@@ -176,8 +190,8 @@ def main():
         stats.append(fml.iterate())
         st = stats[-1]
         log("step %d: %.1f ms (v sweep %.1f, w %.1f, hyper %.1f, %s %.1f) rmse %.6f" % (
-            i, st.ms_total, st.ms_v, st.ms_w, st.ms_hyper, "predict" if mc else "test",
-            st.ms_predict if mc else st.ms_test, rmse_of(st)))
+            i, st.ms_total, st.ms_v, st.ms_w, st.ms_hyper, "predict" if mc or online else "test",
+            st.ms_predict if mc or online else st.ms_test, rmse_of(st)))
     barrier()
     elapsed = time.perf_counter() - t_start
     if world > 1:
@@ -198,10 +212,15 @@ def main():
     # MCMC / ALS draw_v (fm_learn_mcmc.h:780-835), SURVEY §8d: per factor
     # B = 72 B/nnz (q-build 8 + stats 8 CSC + 16 e,q + correction 8 CSC + 32 e,q read/write)
     #   + 8 B/row + 16 B/feature
+    # OVBFM: the same per-factor model per mini-batch; every batch reads the parameters of the
+    # columns it touches (<= all F*S), the level launches are num_batch * k * levels per epoch,
+    # timed as the summed factor-sweep phase of the batches
     n_launch = sum(s.n_vlevel_launches for s in stats)
-    ms_launch = sum(s.ms_vlevel_kernels for s in stats)
+    ms_launch = sum(s.ms_v if online else s.ms_vlevel_kernels for s in stats)
     avg_ms = ms_launch / max(1, n_launch)
-    if mc:
+    if online:
+        bytes_per_launch = (128.0 * nnz + 24.0 * N + 32.0 * (F * S) * args.batch) / max(1, levels * args.batch)
+    elif mc:
         bytes_per_launch = (72.0 * nnz + 8.0 * N + 16.0 * (F * S)) / max(1, levels)
     else:
         bytes_per_launch = (128.0 * nnz + 24.0 * N + 32.0 * (F * S)) / max(1, levels)
@@ -210,11 +229,14 @@ def main():
     achieved = bytes_per_launch / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else 0.0
     sweep_ms = sum(s.ms_v for s in stats) / len(stats)
     traffic = None
-    if mc:
+    if online:
+        kernel = "k_ov_v_level"
+    elif mc:
         kernel = "k_mc_level_lord" if layout == "level" else "k_mc_v_level"
     else:
         kernel = "k_level_lord" if layout == "level" else "k_v_level_fused"
-    tf = os.path.join(ROOT, "profiles", "traffic_%s_%s%s.json" % (args.config, layout, "_" + args.method if mc else ""))
+    tf = os.path.join(ROOT, "profiles", "traffic_%s_%s%s.json" % (args.config, layout,
+                                                                   "_" + args.method if mc or online else ""))
     if os.path.exists(tf):
         with open(tf) as fh:
             traffic = json.load(fh).get("bytes_per_launch")
@@ -228,7 +250,10 @@ def main():
                    "features": F * S, "k": k, "nnz_per_gpu": nnz, "test_rows_per_gpu": n_test,
                    "levels": levels, "method": args.method,
                    "step": ("one full %s iteration (draw_all + train/test re-prediction, device RNG streams)"
-                            % args.method.upper()) if mc else "one full VB iteration (update_all + test RMSE)",
+                            % args.method.upper()) if mc else
+                           ("one OVBFM epoch (shuffle, regroup into %d mini-batches, per batch: predictions + "
+                            "update_all; test RMSE)" % args.batch) if online else
+                           "one full VB iteration (update_all + test RMSE)",
                    "parallelism": ("feature-sharded fs%d" if fshard else "row-sharded dp%d") % world,
                    "row_layout": layout},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -237,13 +262,15 @@ def main():
                      "launches": n_launch, "bytes_per_launch": bytes_per_launch},
         "factor_sweep_ms_per_step": sweep_ms,
         "factor_sweep_nnz_k_per_s": units * nnz * k / (sweep_ms * 1e-3),
-        "test_rmse": rmse_of(stats[-1]), "free_energy": None if mc else stats[-1].free_energy,
+        "test_rmse": rmse_of(stats[-1]),
+        "free_energy": None if mc else stats[-1].free_energy_last if online else stats[-1].free_energy,
         "phase_ms": {kk: getattr(stats[-1], kk) for kk in (
             ("ms_hyper", "ms_w", "ms_v", "ms_predict", "ms_total") if mc else
+            ("ms_regroup", "ms_predict", "ms_w0", "ms_w", "ms_v", "ms_hyper", "ms_test", "ms_total") if online else
             ("ms_w0", "ms_w", "ms_qcache_kernels", "ms_v", "ms_hyper", "ms_test", "ms_total"))},
         "cpu_baseline": None,
     }
-    if rank == 0 and world == 1 and not args.no_cpu_baseline and not mc:
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and not mc and not online:
         try:
             rows = min(args.cpu_rows, N)
             result["cpu_baseline"] = cpu_baseline(cfg, rows, min(args.cpu_factors, k))

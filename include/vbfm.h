@@ -214,6 +214,7 @@ typedef struct {
 	uint32_t seed;            /* srand(seed) (libfm.cpp:123-124) */
 	double init_stdev;        /* -init_stdev (draws of fm.v / fm.w that precede the learner's) */
 	int32_t init_mode;        /* VBFM_ONLINE_INIT_* */
+	double *fm_v;             /* [k*D] f-major or NULL: receives the fm.v draws (v_file.txt, fm_model.h:98) */
 } vbfm_online_config;
 
 typedef struct {
@@ -227,6 +228,10 @@ typedef struct {
 	int32_t num_levels;
 	/* device time: regrouping into batches, the batches' update_all, test; ms */
 	double ms_regroup, ms_batches, ms_test, ms_total;
+	/* ... and the batches' phases summed over the epoch: batch CSR + predictions, update_w0,
+	 * the w sweep, the factor sweeps, the hyper-parameters + free energy */
+	double ms_predict, ms_w0, ms_w, ms_v, ms_hyper;
+	uint32_t n_vlevel_launches;   /* level launches of the factor sweeps */
 	uint64_t nnz_train;
 } vbfm_online_stats;
 

@@ -144,16 +144,36 @@ __global__ void k_ov_steps(const uint32_t *t, double *rho, uint32_t D)
 }
 
 // ---- the level sweeps ------------------------------------------------------------------------
-// update_v (fm_learn_vb_online.h:558-627) for the batch's entries of one column per workgroup.
+// A mini-batch holds ~1/num_batch of every column, so its columns are short: G threads serve one
+// column (G = 4 .. 64 lanes of a wave, several columns per 256-thread workgroup, sums by xor
+// butterflies inside the lane group; or G = 256, one column per workgroup).
+template <int G>
+DEVI void group_sum2(double &a, double &b, double *lds)
+{
+	if constexpr (G <= 64) {
+#pragma unroll
+		for (int o = G / 2; o > 0; o >>= 1) {
+			a += __shfl_xor(a, o, 64);
+			b += __shfl_xor(b, o, 64);
+		}
+	} else {
+		block_sum2<G>(a, b, lds);
+	}
+}
+
+// update_v (fm_learn_vb_online.h:558-627) for the batch's entries of one column per lane group.
 // The per-entry statistics are VB's (v_stat); each becomes the natural-parameter terms
 //   (1 - new_vj) * sigma_old + new_vj * (sigma_v_g + alpha * col_count * v_sigma_sqr)
 //   (1 - new_vj) * mu_old    + new_vj * col_count * alpha * v_mean
 // whose mean over the entries is the new natural parameter; the correction is VB's (v_apply).
-template <int BLOCK, int P, bool NEXT>
-__global__ __launch_bounds__(BLOCK) void k_ov_v_level(LevelArgs a)
+template <int G, int P, bool NEXT>
+__global__ __launch_bounds__(256) void k_ov_v_level(LevelArgs a)
 {
-	__shared__ double lds[2 * (BLOCK / 64)];
-	const uint32_t j = a.feats[blockIdx.x];
+	__shared__ double lds[2 * (256 / 64)];
+	const uint32_t col_i = G <= 64 ? blockIdx.x * (256 / G) + threadIdx.x / G : blockIdx.x;
+	const uint32_t lane = G <= 64 ? threadIdx.x % G : threadIdx.x;
+	if (col_i >= a.nfeat) return;   // whole lane groups (G <= 64) or the whole workgroup
+	const uint32_t j = a.feats[col_i];
 	const uint64_t cb = a.col_ptr[j];
 	const uint32_t n = (uint32_t)(a.col_ptr[j + 1] - cb);
 	if (n == 0) return;   // columns without entries in the batch are skipped (:389-394)
@@ -170,7 +190,7 @@ __global__ __launch_bounds__(BLOCK) void k_ov_v_level(LevelArgs a)
 	double2 nx = make_double2(0.0, 0.0);
 	if constexpr (NEXT) nx = a.ms_next[(size_t)j * a.ms_stride_next];
 	double eta1 = 0.0, eta2 = 0.0;
-	for (uint32_t i = threadIdx.x; i < n; i += BLOCK) {
+	for (uint32_t i = lane; i < n; i += G) {
 		const uint2 ent = col[i];
 		Rec v;
 		load_rec(a.rows, ent.x & ROW_MASK, v);
@@ -179,11 +199,11 @@ __global__ __launch_bounds__(BLOCK) void k_ov_v_level(LevelArgs a)
 		eta2 += keep_s + rho * (sv_g + acc * vs);
 		eta1 += keep_m + rca * vm;
 	}
-	block_sum2<BLOCK>(eta1, eta2, lds);
+	group_sum2<G>(eta1, eta2, lds);
 	const double nmu = eta1 / n, nsig = eta2 / n;
 	double mu = nmu / nsig, sig = 1 / nsig;
 	bool go = true;
-	const bool leader = threadIdx.x == 0;
+	const bool leader = lane == 0;
 	if (dnan(sig) || dinf(sig)) {
 		sig = so;
 		if (leader) atomicAdd(&a.counters[CNT_NAN_SIGMA_V], 1u);
@@ -204,7 +224,8 @@ __global__ __launch_bounds__(BLOCK) void k_ov_v_level(LevelArgs a)
 	}
 	if (!go && !NEXT) return;
 	if (a.dup[j]) {
-		__syncthreads();
+		// a row listed twice: the reference corrects entry after entry
+		if constexpr (G > 64) __syncthreads();
 		if (leader)
 			for (uint32_t i = 0; i < n; ++i) {
 				const uint2 ent = col[i];
@@ -215,7 +236,7 @@ __global__ __launch_bounds__(BLOCK) void k_ov_v_level(LevelArgs a)
 			}
 		return;
 	}
-	for (uint32_t i = threadIdx.x; i < n; i += BLOCK) {
+	for (uint32_t i = lane; i < n; i += G) {
 		const uint2 ent = col[i];
 		Rec v;
 		load_rec(a.rows, ent.x & ROW_MASK, v);
@@ -226,11 +247,14 @@ __global__ __launch_bounds__(BLOCK) void k_ov_v_level(LevelArgs a)
 
 // update_w (fm_learn_vb_online.h:499-556): as above with VB's w statistics; t_wj / new_wj are
 // advanced by the column itself (:519-520)
-template <int BLOCK, bool NEXT>
-__global__ __launch_bounds__(BLOCK) void k_ov_w_level(LevelArgs a)
+template <int G, bool NEXT>
+__global__ __launch_bounds__(256) void k_ov_w_level(LevelArgs a)
 {
-	__shared__ double lds[2 * (BLOCK / 64)];
-	const uint32_t j = a.feats[blockIdx.x];
+	__shared__ double lds[2 * (256 / 64)];
+	const uint32_t col_i = G <= 64 ? blockIdx.x * (256 / G) + threadIdx.x / G : blockIdx.x;
+	const uint32_t lane = G <= 64 ? threadIdx.x % G : threadIdx.x;
+	if (col_i >= a.nfeat) return;
+	const uint32_t j = a.feats[col_i];
 	const uint64_t cb = a.col_ptr[j];
 	const uint32_t n = (uint32_t)(a.col_ptr[j + 1] - cb);
 	if (n == 0) return;   // (:364-368)
@@ -247,7 +271,7 @@ __global__ __launch_bounds__(BLOCK) void k_ov_w_level(LevelArgs a)
 	double2 nx = make_double2(0.0, 0.0);
 	if constexpr (NEXT) nx = a.ms_next[(size_t)j * a.ms_stride_next];
 	double eta1 = 0.0, eta2 = 0.0;
-	for (uint32_t i = threadIdx.x; i < n; i += BLOCK) {
+	for (uint32_t i = lane; i < n; i += G) {
 		const uint2 ent = col[i];
 		const float x = ent_x(ent);
 		const double w_mean = x * (a.rows[ent.x & ROW_MASK].e + x * mo);
@@ -255,11 +279,11 @@ __global__ __launch_bounds__(BLOCK) void k_ov_w_level(LevelArgs a)
 		eta2 += keep_s + rho * (sw_g + acc * w_sigma_sqr);
 		eta1 += keep_m + rca * w_mean;
 	}
-	block_sum2<BLOCK>(eta1, eta2, lds);
+	group_sum2<G>(eta1, eta2, lds);
 	const double nmu = eta1 / n, nsig = eta2 / n;
 	double mu = nmu / nsig, sig = 1 / nsig;
 	bool go = true;
-	const bool leader = threadIdx.x == 0;
+	const bool leader = lane == 0;
 	if (dnan(sig) || dinf(sig)) {
 		if (leader) atomicAdd(&a.counters[CNT_NAN_SIGMA_W], 1u);
 		sig = so;
@@ -282,7 +306,7 @@ __global__ __launch_bounds__(BLOCK) void k_ov_w_level(LevelArgs a)
 	}
 	if (!go && !NEXT) return;
 	if (a.dup[j]) {
-		__syncthreads();
+		if constexpr (G > 64) __syncthreads();
 		if (leader)
 			for (uint32_t i = 0; i < n; ++i) {
 				const uint2 ent = col[i];
@@ -293,7 +317,7 @@ __global__ __launch_bounds__(BLOCK) void k_ov_w_level(LevelArgs a)
 			}
 		return;
 	}
-	for (uint32_t i = threadIdx.x; i < n; i += BLOCK) {
+	for (uint32_t i = lane; i < n; i += G) {
 		const uint2 ent = col[i];
 		Rec v;
 		load_rec(a.rows, ent.x & ROW_MASK, v);
@@ -308,31 +332,36 @@ inline unsigned grid_of(uint64_t n, unsigned block = 256) { return (unsigned)((n
 
 // ------------------------------------------------------------------------------------------
 namespace vbk {
+template <int G>
+hipError_t launch_ov(const LevelArgs &a, int is_w, hipStream_t s)
+{
+	const unsigned grid = G <= 64 ? (a.nfeat + 256 / G - 1) / (256 / G) : a.nfeat;
+	const bool nx = a.ms_next != nullptr;
+	if (is_w) {
+		if (nx) k_ov_w_level<G, true><<<grid, 256, 0, s>>>(a);
+		else k_ov_w_level<G, false><<<grid, 256, 0, s>>>(a);
+	} else if (a.slot == 0) {
+		if (nx) k_ov_v_level<G, 0, true><<<grid, 256, 0, s>>>(a);
+		else k_ov_v_level<G, 0, false><<<grid, 256, 0, s>>>(a);
+	} else {
+		if (nx) k_ov_v_level<G, 1, true><<<grid, 256, 0, s>>>(a);
+		else k_ov_v_level<G, 1, false><<<grid, 256, 0, s>>>(a);
+	}
+	return hipGetLastError();
+}
+
+// lanes per column from the batch's mean column length (LevelArgs::avg_len, set by
+// ov_level_args): about one entry per lane
 hipError_t ov_level(const LevelArgs &a, int is_w, hipStream_t s)
 {
 	if (a.nfeat == 0) return hipSuccess;
-	const bool nx = a.ms_next != nullptr;
-	const bool small = a.avg_len <= 96;
-	if (is_w) {
-		if (small) {
-			if (nx) k_ov_w_level<64, true><<<a.nfeat, 64, 0, s>>>(a);
-			else k_ov_w_level<64, false><<<a.nfeat, 64, 0, s>>>(a);
-		} else {
-			if (nx) k_ov_w_level<256, true><<<a.nfeat, 256, 0, s>>>(a);
-			else k_ov_w_level<256, false><<<a.nfeat, 256, 0, s>>>(a);
-		}
-		return hipGetLastError();
-	}
-#define OV_V(B, P, N) k_ov_v_level<B, P, N><<<a.nfeat, B, 0, s>>>(a)
-	if (small) {
-		if (a.slot == 0) { if (nx) OV_V(64, 0, true); else OV_V(64, 0, false); }
-		else { if (nx) OV_V(64, 1, true); else OV_V(64, 1, false); }
-	} else {
-		if (a.slot == 0) { if (nx) OV_V(256, 0, true); else OV_V(256, 0, false); }
-		else { if (nx) OV_V(256, 1, true); else OV_V(256, 1, false); }
-	}
-#undef OV_V
-	return hipGetLastError();
+	const uint32_t m = a.avg_len;
+	if (m <= 6) return launch_ov<4>(a, is_w, s);
+	if (m <= 12) return launch_ov<8>(a, is_w, s);
+	if (m <= 24) return launch_ov<16>(a, is_w, s);
+	if (m <= 48) return launch_ov<32>(a, is_w, s);
+	if (m <= 160) return launch_ov<64>(a, is_w, s);
+	return launch_ov<256>(a, is_w, s);
 }
 }  // namespace vbk
 
@@ -368,6 +397,8 @@ struct OvState {
 	float *t_b = nullptr;
 	RowRec *rows_b = nullptr;
 	hipEvent_t ev[4] = {};
+	std::vector<hipEvent_t> bev;   // [num_batch * 6] phase marks of every batch
+	uint32_t launches_v = 0;
 };
 
 namespace vbi {
@@ -383,6 +414,7 @@ void ov_free(vbfm_ctx *c)
 	dfree(o.rows_b);
 	for (hipEvent_t e : o.ev)
 		if (e) (void)hipEventDestroy(e);
+	for (hipEvent_t e : o.bev) (void)hipEventDestroy(e);
 	delete c->ov;
 	c->ov = nullptr;
 }
@@ -394,6 +426,7 @@ void ov_level_args(vbfm_ctx *c, LevelArgs &a, bool is_w, int f)
 	a.rho = is_w ? o.new_wj : o.new_vj;
 	a.ccount = o.ccount;
 	a.tcount = is_w ? o.t_wj : (f == 0 ? o.t_vj : nullptr);
+	if (!is_w) o.launches_v++;
 	a.avg_len = a.avg_len / std::max(o.num_batch, 1u);   // the batch's share of the mean column
 }
 
@@ -557,6 +590,8 @@ int vbfm_online_init(vbfm_ctx *c, const vbfm_online_config *cfg)
 			c->sched_ready = false;
 			require_train(c);
 			for (hipEvent_t &e : o.ev) HIPCHK(hipEventCreate(&e));
+			o.bev.resize((size_t)nb * 6);
+			for (hipEvent_t &e : o.bev) HIPCHK(hipEventCreate(&e));
 			o.num_batch = nb;
 			o.n_total = N;
 			o.size = size;
@@ -568,7 +603,10 @@ int vbfm_online_init(vbfm_ctx *c, const vbfm_online_config *cfg)
 				vbfm_params p = {mw.data(), sw.data(), mv.data(), sv.data(), hw.data(), hv.data(), 0, 0, 0, 0};
 				vbrng::Glibc &rng = o.stream;
 				rng.seed_with(cfg->seed);
-				for (size_t i = 0; i < kd; i++) (void)rng.gaussian(0, cfg->init_stdev);       // fm.v (fm_model.h:97)
+				for (size_t i = 0; i < kd; i++) {                                              // fm.v (fm_model.h:97)
+					const double v = rng.gaussian(0, cfg->init_stdev);
+					if (cfg->fm_v) cfg->fm_v[i] = v;
+				}
 				for (uint32_t i = 0; i < c->D; i++) (void)rng.gaussian(0, cfg->init_stdev);   // fm.w (libfm.cpp:313)
 				for (uint32_t i = 0; i < c->D; i++) mw[i] = 0.1 * rng.gaussian(0, 1);         // mu_w_dash.init_normal
 				for (size_t i = 0; i < kd; i++) mv[i] = 0.1 * rng.gaussian(0, 1);            // mu_v_dash.init_normal
@@ -577,7 +615,7 @@ int vbfm_online_init(vbfm_ctx *c, const vbfm_online_config *cfg)
 				p.alpha = 1.0; p.sigma_0 = 1.0; p.mu_0_dash = 0.0; p.sigma_0_dash = 0.02;
 				if (vbfm_set_params(c, &p)) throw std::string(c->err);
 			} else {
-				if (vbfm_init_params_replay(c, cfg->seed, cfg->init_stdev, nullptr, nullptr)) throw std::string(c->err);
+				if (vbfm_init_params_replay(c, cfg->seed, cfg->init_stdev, cfg->fm_v, nullptr)) throw std::string(c->err);
 				uint32_t st[31];
 				glibc_state_at(cfg->seed, c->init_stream_end, st);
 				o.stream.set_chrono_state(st);
@@ -637,6 +675,9 @@ int vbfm_online_epoch(vbfm_ctx *c, vbfm_online_stats *out)
 		HIPCHK(hipMemsetAsync(c->counters, 0, CNT_N * 4, c->s));
 		Range r_ep("vbfm_online_epoch");
 		HIPCHK(hipEventRecord(o.ev[0], c->s));
+		o.launches_v = 0;
+		c->pev_used = 0;   // vbfm_set_profiling: the spans of this epoch only
+		c->spans.clear();
 		ov_regroup(c);
 		HIPCHK(hipEventRecord(o.ev[1], c->s));
 		const uint32_t nb = o.num_batch, nf = c->tr.nf;
@@ -656,6 +697,8 @@ int vbfm_online_epoch(vbfm_ctx *c, vbfm_online_stats *out)
 		try {
 			for (uint32_t b = 0; b < nb; b++) {
 				Range r_b("batch");
+				hipEvent_t *bev = &o.bev[(size_t)b * 6];
+				HIPCHK(hipEventRecord(bev[0], c->s));
 				const uint32_t n = (uint32_t)(o.rstart[b + 1] - o.rstart[b]);
 				const uint64_t nnz = eoff[b + 1] - eoff[b];
 				ov_batch_capacity(c, n, nnz);
@@ -690,8 +733,11 @@ int vbfm_online_epoch(vbfm_ctx *c, vbfm_online_stats *out)
 				                      n, bl, c->s));
 				HIPCHK(vbk::residual_init(c->rows, c->scratch_n, c->tr.target, n, c->s));
 				// update_all(train1, train.num_cases) (fm_learn_vb_online.h:354-469)
+				HIPCHK(hipEventRecord(bev[1], c->s));
 				if (c->k0) ov_step_w0(c);
+				HIPCHK(hipEventRecord(bev[2], c->s));
 				if (c->k1) step_w(c);
+				HIPCHK(hipEventRecord(bev[3], c->s));
 				if (c->D > 0) {
 					for (int f = 0; f < c->k; f++) {
 						step_qcache(c, f);
@@ -700,6 +746,7 @@ int vbfm_online_epoch(vbfm_ctx *c, vbfm_online_stats *out)
 					k_ov_steps<<<grid_of(c->D), 256, 0, c->s>>>(o.t_vj, o.new_vj, c->D);
 					HIPCHK(hipGetLastError());
 				}
+				HIPCHK(hipEventRecord(bev[4], c->s));
 				ov_step_hyper(c, &st.nan_alpha, &st.inf_alpha);
 				// free energy of the first and the last batch (:143-146)
 				if (b == 0 || b + 1 == nb) {
@@ -707,6 +754,7 @@ int vbfm_online_epoch(vbfm_ctx *c, vbfm_online_stats *out)
 					if (b == 0) st.free_energy_first = fe;
 					if (b + 1 == nb) st.free_energy_last = fe;
 				}
+				HIPCHK(hipEventRecord(bev[5], c->s));
 				restore();
 			}
 		} catch (...) {
@@ -738,6 +786,13 @@ int vbfm_online_epoch(vbfm_ctx *c, vbfm_online_stats *out)
 		HIPCHK(hipEventElapsedTime(&ms, o.ev[1], o.ev[2])); st.ms_batches = ms;
 		HIPCHK(hipEventElapsedTime(&ms, o.ev[2], o.ev[3])); st.ms_test = ms;
 		HIPCHK(hipEventElapsedTime(&ms, o.ev[0], o.ev[3])); st.ms_total = ms;
+		double *ph[5] = {&st.ms_predict, &st.ms_w0, &st.ms_w, &st.ms_v, &st.ms_hyper};
+		for (uint32_t b = 0; b < nb; b++)
+			for (int q = 0; q < 5; q++) {
+				HIPCHK(hipEventElapsedTime(&ms, o.bev[(size_t)b * 6 + q], o.bev[(size_t)b * 6 + q + 1]));
+				*ph[q] += ms;
+			}
+		st.n_vlevel_launches = o.launches_v;
 		st.nnz_train = c->tr.nnz;
 		if (out) *out = st;
 	});

@@ -1,4 +1,5 @@
-// host/libfm_main.cpp -- drop-in for the reference's `bin/libFM -method vb | mcmc | als` on MI355X.
+// host/libfm_main.cpp -- drop-in for the reference's `bin/libFM -method vb | vb_online | mcmc | als`
+// on MI355X.
 //
 // Mirrors main() of src/libfm/libfm.cpp (flag surface, defaults, RNG order, output lines and
 // files) and the iteration loop of fm_learn_vb_simultaneous::_learn
@@ -260,6 +261,134 @@ static void run_mcmc(const McmcRun &r, Data &train, Data &test)
 	}
 }
 
+// the reference's NaN reports (fm_learn_vb_simultaneous.h:89-118 and
+// fm_learn_vb_online_simultaneous.h:159-188; labels as printed there)
+static void nan_reports(uint32_t nan_alpha, uint32_t inf_alpha, uint32_t nan_mu_w, uint32_t inf_mu_w,
+                        uint32_t nan_sigma_w, uint32_t nan_mu_v, uint32_t inf_mu_v, uint32_t nan_sigma_v)
+{
+	if (nan_alpha > 0 || inf_alpha > 0)
+		std::cout << "#nans in alpha:\t" << nan_alpha << "\t#inf_in_alpha:\t" << inf_alpha << std::endl;
+	if (nan_mu_w > 0 || inf_mu_w > 0)
+		std::cout << "#nans in alpha:\t" << nan_mu_w << "\t#inf_in_alpha:\t" << inf_mu_w << std::endl;
+	if (nan_sigma_w > 0) std::cout << "#nans in alpha:\t" << nan_sigma_w << "\t#inf_in_alpha:\t" << 0 << std::endl;
+	if (nan_mu_v > 0 || inf_mu_v > 0)
+		std::cout << "#nans in alpha:\t" << nan_mu_v << "\t#inf_in_alpha:\t" << inf_mu_v << std::endl;
+	if (nan_sigma_v > 0) std::cout << "#nans in alpha:\t" << nan_sigma_v << "\t#inf_in_alpha:\t" << 0 << std::endl;
+}
+
+static void write_vfile(const std::vector<double> &fm_v, int k, uint32_t D)
+{
+	// fm_model.h:98 (DMatrix::save, matrix.h:129-152)
+	std::ofstream vf("v_file.txt");
+	for (int f = 0; f < k; f++) {
+		for (uint32_t j = 0; j < D; j++) vf << (j ? "\t" : "") << fm_v[(size_t)f * D + j];
+		vf << std::endl;
+	}
+}
+
+// -method vb_online (libfm.cpp:159-171, 312-320, 494-503; fm_learn_vb_online_simultaneous.h:20-290)
+struct OnlineRun {
+	uint32_t seed;
+	double init_stdev;
+	uint32_t num_iter, num_batch;
+	const uint32_t *groups;
+	uint32_t G, D;
+	int k0, k1, k;
+	int32_t device;
+	bool vfile;
+	std::string rlog_file, out_file;
+};
+
+static void run_online(const OnlineRun &r, Data &train, Data &test)
+{
+	vbfm_ctx *ctx = nullptr;
+	try {
+		vbfm_config cfg{r.k0, r.k1, r.k, r.D, r.G, r.groups, train.h.min_target, train.h.max_target, r.device, 0};
+		check(vbfm_create(&ctx, &cfg), nullptr);
+		const vbfm_csc tr = train.csc(), te = test.csc();
+		check(vbfm_set_train(ctx, &tr), ctx);
+		check(vbfm_set_test(ctx, &te), ctx);
+		const size_t kd = (size_t)r.k * r.D;
+		std::vector<double> fm_v(r.vfile ? kd : 0);
+		const char *init_env = getenv("VBFM_INIT");
+		const bool replay = init_env ? std::string(init_env) == "replay" : kd + r.D >= 2000000;
+		vbfm_online_config oc{r.num_batch, r.seed, r.init_stdev,
+		                      replay ? VBFM_ONLINE_INIT_REPLAY : VBFM_ONLINE_INIT_HOST, r.vfile ? fm_v.data() : nullptr};
+		check(vbfm_online_init(ctx, &oc), ctx);
+		if (r.vfile) write_vfile(fm_v, r.k, r.D);
+		std::ofstream *rlog_out = nullptr;
+		RLog *rlog = nullptr;
+		if (!r.rlog_file.empty()) {   // fm_learn::init + fm_learn_vb_online::init fields (:761-783)
+			rlog_out = new std::ofstream(r.rlog_file.c_str());
+			if (!rlog_out->is_open()) throw std::string("Unable to open file " + r.rlog_file);
+			std::cout << "logging to " << r.rlog_file << std::endl;
+			rlog = new RLog(rlog_out);
+			for (const char *f : {"rmse", "mae", "time_pred", "time_learn", "time_learn2", "time_learn4", "alpha",
+			                      "rmse_mcmc_this", "rmse_mcmc_all"})
+				rlog->add(f);
+			for (uint32_t g = 0; g < r.G; g++) {
+				std::ostringstream ss;
+				ss << "wmu[" << g << "]"; rlog->add(ss.str()); ss.str("");
+				ss << "wlambda[" << g << "]"; rlog->add(ss.str()); ss.str("");
+				for (int f = 0; f < r.k; f++) {
+					ss << "vmu[" << g << "," << f << "]"; rlog->add(ss.str()); ss.str("");
+					ss << "vlambda[" << g << "," << f << "]"; rlog->add(ss.str()); ss.str("");
+				}
+			}
+			rlog->init();
+		}
+		std::cout << "check in fm_learn_vb_online_simultaneous" << std::endl;
+		std::ostringstream tag;
+		tag << r.k0 << r.k1 << r.k;
+		// :37-52: the rmse file and an (always empty) free_energy_..._vb_online are truncated; the
+		// free energies are appended to free_energy_..._vb (fm_learn_vb_online.h:636-662)
+		const std::string f_rmse = "test_rmse_" + tag.str() + "_vb_online", f_fe = "free_energy_" + tag.str() + "_vb";
+		{ std::ofstream a(f_rmse.c_str()); std::ofstream b(("free_energy_" + tag.str() + "_vb_online").c_str()); }
+		for (uint32_t it = 0; it < r.num_iter; it++) {
+			const double t_user = usertime();
+			const clock_t t_clock = clock();
+			const double t_wall = (double)time(NULL);
+			vbfm_online_stats st;
+			check(vbfm_online_epoch(ctx, &st), ctx);
+			{
+				std::ofstream fe(f_fe.c_str(), std::ios_base::app);
+				fe << -st.free_energy_first << "\n";
+				std::cout << "free energy " << st.free_energy_first << std::endl;
+				if (r.num_batch > 1) {
+					fe << -st.free_energy_last << "\n";
+					std::cout << "free energy " << st.free_energy_last << std::endl;
+				}
+			}
+			nan_reports(st.nan_alpha, st.inf_alpha, st.nan_mu_w, st.inf_mu_w, st.nan_sigma_w, st.nan_mu_v, st.inf_mu_v,
+			            st.nan_sigma_v);
+			if (rlog) {
+				rlog->log("time_learn", usertime() - t_user);
+				rlog->log("time_learn2", (double)(clock() - t_clock) / CLOCKS_PER_SEC);
+				rlog->log("time_learn4", (double)time(NULL) - t_wall);
+				rlog->log("rmse_mcmc_this", st.rmse);
+				rlog->newline();
+			}
+			std::ofstream fr(f_rmse.c_str(), std::ios_base::app);
+			fr << st.rmse << "\n";
+			std::cout << "#Iter=" << std::setw(3) << it << "\tTest=" << st.rmse << std::endl;
+		}
+		std::cout << "after learn" << std::endl;                              // libfm.cpp:507
+		std::cout << "Final\tTrain=" << NAN << "\tTest=" << NAN << std::endl;   // evaluate() is NaN (:17)
+		if (!r.out_file.empty()) {
+			std::vector<double> pred(test.h.num_rows);
+			check(vbfm_get_test_pred(ctx, pred.data()), ctx);
+			std::ofstream o(r.out_file.c_str());
+			for (double x : pred) o << x << std::endl;
+		}
+		delete rlog;
+		delete rlog_out;
+		vbfm_destroy(ctx);
+	} catch (...) {
+		if (ctx) vbfm_destroy(ctx);
+		throw;
+	}
+}
+
 int main(int argc, char **argv)
 {
 	vbfm_ctx *ctx = nullptr;
@@ -288,7 +417,7 @@ int main(int argc, char **argv)
 		const std::string p_help = cmd.reg("help", "this screen");
 		const std::string p_rel = cmd.reg("relation", "BS: filenames for the relations, default=''");
 		cmd.reg("cache_size", "cache size for data storage (only applicable if data is in binary format), default=infty");
-		cmd.reg("batch", "How many batches for online algorithm");
+		const std::string p_batch = cmd.reg("batch", "How many batches for online algorithm");
 		const std::string p_dev = cmd.reg("device", "HIP device ordinal; default=0");
 		const std::string p_vfile = cmd.reg("vfile", "write v_file.txt like the reference (1) or not (0); default=1");
 		if (cmd.has(p_help) || argc == 1) { cmd.print_help(); return 0; }
@@ -296,8 +425,8 @@ int main(int argc, char **argv)
 
 		const uint32_t seed = cmd.has(p_seed) ? (uint32_t)cmd.geti(p_seed, 0) : (uint32_t)time(NULL);
 		const std::string method = cmd.get(p_method, "mcmc");
-		if (method != "vb" && method != "mcmc" && method != "als")
-			throw std::string("method " + method + " is not provided by this build (use -method vb, mcmc or als)");
+		if (method != "vb" && method != "vb_online" && method != "mcmc" && method != "als")
+			throw std::string("method " + method + " is not provided by this build (use -method vb, vb_online, mcmc or als)");
 		if (cmd.get(p_task) != "r") throw std::string("unknown task");   // regression only
 		if (!cmd.list(p_rel).empty()) throw std::string("-relation is not supported by this build");
 
@@ -306,8 +435,11 @@ int main(int argc, char **argv)
 		load(cmd.get(p_test), test, "test");
 		if (cmd.geti(p_verb, 0) > 0) std::cout << "seed=" << seed << std::endl;
 
-		// libfm.cpp:215-256: attributes and groups
-		const uint32_t D = std::max(train.h.num_feature, test.h.num_feature) + 1;
+		// libfm.cpp:215-256: attributes and groups. For vb_online the train file is only scanned
+		// (find_max_feature, libfm.cpp:167-170, 528-600), which leaves the largest feature ids in
+		// num_feature: one attribute fewer than -method vb gets on the same files
+		const uint32_t nf_max = std::max(train.h.num_feature, test.h.num_feature);
+		const uint32_t D = method == "vb_online" ? nf_max : nf_max + 1;
 		std::vector<uint32_t> groups(D, 0);
 		uint32_t G = 1;
 		if (cmd.has(p_meta)) {
@@ -329,6 +461,13 @@ int main(int argc, char **argv)
 		const double init_stdev = cmd.getd(p_init, 0.1);
 		const uint32_t num_iter = (uint32_t)cmd.geti(p_iter, 100);
 
+		if (method == "vb_online") {
+			OnlineRun run{seed, init_stdev, num_iter, (uint32_t)cmd.geti(p_batch, 50), cmd.has(p_meta) ? groups.data() : nullptr,
+			              G, D, k0, k1, k, (int32_t)cmd.geti(p_dev, 0), cmd.geti(p_vfile, 1) != 0,
+			              cmd.has(p_rlog) ? cmd.get(p_rlog) : std::string(), cmd.has(p_out) ? cmd.get(p_out) : std::string()};
+			run_online(run, train, test);
+			return 0;
+		}
 		if (method != "vb") {
 			std::vector<double> reg;
 			for (const std::string &r : cmd.list(p_reg)) reg.push_back(atof(r.c_str()));
@@ -361,13 +500,7 @@ int main(int argc, char **argv)
 			check(vbfm_init_params_host(seed, init_stdev, k, D, G, &p, fm_v.data(), nullptr), nullptr);
 			check(vbfm_set_params(ctx, &p), ctx);
 		}
-		if (vfile) {   // fm_model.h:98 (DMatrix::save, matrix.h:129-152)
-			std::ofstream vf("v_file.txt");
-			for (int f = 0; f < k; f++) {
-				for (uint32_t j = 0; j < D; j++) vf << (j ? "\t" : "") << fm_v[(size_t)f * D + j];
-				vf << std::endl;
-			}
-		}
+		if (vfile) write_vfile(fm_v, k, D);
 		fm_v.clear();
 		fm_v.shrink_to_fit();
 
@@ -413,17 +546,8 @@ int main(int argc, char **argv)
 				fe << -st.free_energy << "\n";
 				std::cout << "free energy " << st.free_energy << std::endl;
 			}
-			// the reference's NaN reports (fm_learn_vb_simultaneous.h:89-118; labels as printed there)
-			if (st.nan_alpha > 0 || st.inf_alpha > 0)
-				std::cout << "#nans in alpha:\t" << st.nan_alpha << "\t#inf_in_alpha:\t" << st.inf_alpha << std::endl;
-			if (st.nan_mu_w > 0 || st.inf_mu_w > 0)
-				std::cout << "#nans in alpha:\t" << st.nan_mu_w << "\t#inf_in_alpha:\t" << st.inf_mu_w << std::endl;
-			if (st.nan_sigma_w > 0)
-				std::cout << "#nans in alpha:\t" << st.nan_sigma_w << "\t#inf_in_alpha:\t" << 0 << std::endl;
-			if (st.nan_mu_v > 0 || st.inf_mu_v > 0)
-				std::cout << "#nans in alpha:\t" << st.nan_mu_v << "\t#inf_in_alpha:\t" << st.inf_mu_v << std::endl;
-			if (st.nan_sigma_v > 0)
-				std::cout << "#nans in alpha:\t" << st.nan_sigma_v << "\t#inf_in_alpha:\t" << 0 << std::endl;
+			nan_reports(st.nan_alpha, st.inf_alpha, st.nan_mu_w, st.inf_mu_w, st.nan_sigma_w, st.nan_mu_v, st.inf_mu_v,
+			            st.nan_sigma_v);
 			if (rlog) {
 				rlog->log("time_learn", usertime() - t_user);
 				rlog->log("time_learn2", (double)(clock() - t_clock) / CLOCKS_PER_SEC);

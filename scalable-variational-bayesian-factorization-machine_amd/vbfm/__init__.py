@@ -113,7 +113,7 @@ ONLINE_INIT_HOST, ONLINE_INIT_REPLAY = 0, 1
 
 class OnlineConfig(C.Structure):
     _fields_ = [("num_batch", C.c_uint32), ("seed", C.c_uint32), ("init_stdev", C.c_double),
-                ("init_mode", C.c_int32)]
+                ("init_mode", C.c_int32), ("fm_v", P_f64)]
 
 
 class OnlineStats(C.Structure):
@@ -123,7 +123,9 @@ class OnlineStats(C.Structure):
                 + [(n, C.c_uint32) for n in ("nan_mu_w", "nan_sigma_w", "inf_mu_w", "nan_mu_v", "nan_sigma_v",
                                              "inf_mu_v", "nan_alpha", "inf_alpha", "num_batch")]
                 + [("num_levels", C.c_int32), ("ms_regroup", C.c_double), ("ms_batches", C.c_double),
-                   ("ms_test", C.c_double), ("ms_total", C.c_double), ("nnz_train", C.c_uint64)])
+                   ("ms_test", C.c_double), ("ms_total", C.c_double), ("ms_predict", C.c_double),
+                   ("ms_w0", C.c_double), ("ms_w", C.c_double), ("ms_v", C.c_double), ("ms_hyper", C.c_double),
+                   ("n_vlevel_launches", C.c_uint32), ("nnz_train", C.c_uint64)])
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}
@@ -607,7 +609,7 @@ class FMLearnVBOnline(FMLearnVB):
 
     def init(self, seed, init_stdev=0.1, num_batch=50, replay=False):
         """srand(seed); the VB learner's initial draws; fm_learn_vb_online::init (needs set_data first)."""
-        cfg = OnlineConfig(num_batch, seed, init_stdev, ONLINE_INIT_REPLAY if replay else ONLINE_INIT_HOST)
+        cfg = OnlineConfig(num_batch, seed, init_stdev, ONLINE_INIT_REPLAY if replay else ONLINE_INIT_HOST, None)
         _check(lib().vbfm_online_init(self._ctx, C.byref(cfg)), self._ctx)
         self.num_batch = num_batch
 

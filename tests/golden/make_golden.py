@@ -105,7 +105,7 @@ def parse_online(stdout):
 
 def online_cases(ref):
     """-method vb_online (OVBFM): fm_learn_vb_online_simultaneous.h, run by the reference itself."""
-    keep = ("final_", "init_mu", "init_nat")
+    keep = ("final_", "init_mu", "init_nat", "init_fm_v")
     for case in ("tiny", "tiny_dup"):
         d = os.path.join(HERE, case)
         tr, te = os.path.join(d, "train.libfm"), os.path.join(d, "test.libfm")

@@ -137,3 +137,43 @@ def test_cli_mcmc_als_match_reference(case, tmp_path):
         assert abs(np.sqrt(np.mean((pred - tg) ** 2)) - t["trace"][-1]["rmse_all"]) < 1e-5
     hdr = open(tmp_path / "log.tsv").readline().rstrip("\n").split("\t")
     assert "rmse_mcmc_all" in hdr and "alpha" in hdr
+
+
+@pytest.mark.parametrize("init", ["host", "replay"])
+@pytest.mark.parametrize("case", ["tiny/online_b3", "tiny/online_meta", "tiny/online_b1"])
+def test_cli_online_matches_reference(case, init, tmp_path, monkeypatch):
+    """-method vb_online: "#Iter=  i\\tTest=.." lines, test_rmse_<tag>_vb_online, the free
+    energies of the first and last batch appended (as -F) to free_energy_<tag>_vb and printed as
+    "free energy F", an empty free_energy_<tag>_vb_online, v_file.txt
+    (fm_learn_vb_online_simultaneous.h:37-52, 143-146, 243-244; fm_learn_vb_online.h:636-662)."""
+    monkeypatch.setenv("VBFM_INIT", init)
+    t, a = load_case(case)
+    m = t["meta"]
+    d = os.path.join(GOLDEN, case.split("/")[0])
+    extra = ["-init_stdev", str(m["init_stdev"]), "-batch", str(m["batch"]), "-out", "pred.txt"]
+    if "meta" in m:
+        extra += ["-meta", os.path.join(d, m["meta"])]
+    stdout = run_cli(tmp_path, os.path.join(d, "train.libfm"), os.path.join(d, "test.libfm"), m["dim"],
+                     m["iter"], m["seed"], extra, method="vb_online")
+    tag = m["dim"].replace(",", "")
+    rmse = open(tmp_path / ("test_rmse_%s_vb_online" % tag)).read().split()
+    fe = open(tmp_path / ("free_energy_%s_vb" % tag)).read().split()
+    assert open(tmp_path / ("free_energy_%s_vb_online" % tag)).read() == ""
+    ref_fe = [x for r in t["trace"] for x in r["free_energy"]]
+    assert len(rmse) == m["iter"] and len(fe) == len(ref_fe)
+    for it, ref in enumerate(t["trace"]):
+        assert same6(rmse[it], g6(ref["rmse"])), (it, rmse[it], ref["rmse"])
+    for got, ref in zip(fe, ref_fe):
+        assert same6(got, g6(-ref)), (got, ref)
+    iters = re.findall(r"#Iter=\s*(\d+)\tTest=(\S+)", stdout)
+    assert [int(i) for i, _ in iters] == list(range(m["iter"]))
+    for (_, te), ref in zip(iters, t["trace"]):
+        assert same6(te, g6(ref["rmse"]))
+    printed = [float(x) for x in re.findall(r"^free energy (\S+)$", stdout, re.M)]
+    np.testing.assert_allclose(printed, ref_fe, rtol=1e-5)
+    k = int(m["dim"].split(",")[2])
+    vf = np.loadtxt(tmp_path / "v_file.txt", ndmin=2)
+    assert vf.shape[0] == k
+    np.testing.assert_allclose(vf.ravel(), a["init_fm_v"], rtol=1e-5, atol=1e-7)
+    np.testing.assert_allclose(np.loadtxt(tmp_path / "pred.txt"), a["final_pred"], rtol=1e-5)
+    assert "Final\tTrain=nan\tTest=nan" in stdout
