@@ -521,7 +521,11 @@ void sweep_level(vbfm_ctx *c, uint32_t l, bool is_w, int f)
 			a.lpidx = c->lpidx;
 			a.lpx = c->lpx;
 			a.tab = c->post_tab;
-			a.pending = l > 0;
+			{
+				// non-temporal record loads (default; VBFM_DEFER_NT=0: plain loads, 1.5 % slower at C4)
+				static const int defer_nt = [] { const char *e = getenv("VBFM_DEFER_NT"); return !(e && e[0] == '0'); }();
+				a.pending = (l > 0 ? 1 : 0) | (l > 0 && defer_nt ? 2 : 0);
+			}
 			a.first_prev = l == 1;
 			HIPCHK(vbk::lord_defer_level(a, is_w, c->s));
 			if (c->row_comm())
@@ -1019,11 +1023,8 @@ int vbfm_init_caches(vbfm_ctx *c)
 		// fm_learn_vb_simultaneous.h:37-44: yhat of train and test, T of train, e = y - yhat
 		rows_row_order(c);
 		const int bl = blocked_predict(c, c->tr);
-		HIPCHK(vbk::predict_e(c->tr.row_ptr, c->tr.csr, c->ms_v, c->ms_w, c->k, c->k1, c->k0, c->mu0, c->scratch_n,
-		                      c->tr.n, bl, c->s));
-		HIPCHK(vbk::predict_t(c->tr.row_ptr, c->tr.csr, c->ms_v, c->ms_w, c->k, c->k1, c->k0, c->s0d, c->rows, c->tr.n,
-		                      bl, c->s));
-		HIPCHK(vbk::residual_init(c->rows, c->scratch_n, c->tr.target, c->tr.n, c->s));
+		HIPCHK(vbk::predict_et(c->tr.row_ptr, c->tr.csr, c->ms_v, c->ms_w, c->k, c->k1, c->k0, c->mu0, c->s0d,
+		                       c->tr.target, c->scratch_n, c->rows, c->tr.n, bl, c->s));
 		if (c->e_test) test_predict(c);
 		sync(c);
 	});

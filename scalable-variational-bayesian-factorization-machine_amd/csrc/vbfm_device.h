@@ -81,7 +81,7 @@ struct LevelArgs {
 	const uint32_t *lpidx;     // the entry's row: index of its previous-level feature in that level
 	const float *lpx;          // ... and that entry's x
 	PostT *tab;                // posteriors of the previous level (read) / of this level (written)
-	int pending;               // apply the previous level's correction first
+	int pending;               // bit 0: apply the previous level's correction first; bit 1: non-temporal record loads
 	int first_prev;            // the previous level is level 0 (q-cache restart of its entries)
 	// online VB (vbfm_online.hip): natural-gradient steps on a mini-batch; nat == nullptr: VB
 	double2 *nat;              // natural parameters {mu, sigma} of each feature, laid out like ms
@@ -173,6 +173,9 @@ hipError_t predict_t(const uint64_t *row_ptr, const uint2 *csr, const double2 *m
                      int k, int k1, int k0, double sigma0_dash, RowRec *rows, uint32_t n, int blocked,
                      hipStream_t s);
 hipError_t residual_init(RowRec *rows, const double *yhat, const float *target, uint32_t n, hipStream_t s);
+hipError_t predict_et(const uint64_t *row_ptr, const uint2 *csr, const double2 *ms_v, const double2 *ms_w, int k, int k1,
+                      int k0, double mu0, double s0d, const float *target, double *scratch, RowRec *rows, uint32_t n,
+                      int blocked, hipStream_t s);
 // per-block partial sums over rows; mode 0: e + mu0 ; mode 1: e*e + t ; out[nblocks]
 hipError_t row_sums(const RowRec *rows, uint32_t n, int mode, double mu0, double *out, uint32_t nblocks,
                     hipStream_t s);

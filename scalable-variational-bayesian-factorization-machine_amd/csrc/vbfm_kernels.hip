@@ -583,6 +583,78 @@ __global__ __launch_bounds__(256) void k_predict_t_wave(const uint64_t *__restri
 	}
 }
 
+// Both predictions of a data set's rows in one pass over the parameters (the caches a fresh
+// train set or mini-batch starts from, fm_learn_vb_simultaneous.h:37-44 /
+// fm_learn_vb_online_simultaneous.h:111-139): k_predict_e_wave's and k_predict_t_wave's
+// arithmetic, accumulator by accumulator in the same order (bit-identical to the two kernels),
+// from one read of each entry's {mu, sigma} run; e = y - yhat written with T.
+template <int KP>
+__global__ __launch_bounds__(256) void k_predict_et_wave(const uint64_t *__restrict__ row_ptr,
+                                                          const uint2 *__restrict__ csr,
+                                                          const double2 *__restrict__ ms_v,
+                                                          const double2 *__restrict__ ms_w, int k, int k1, int k0,
+                                                          double mu0, double s0d, const float *__restrict__ target,
+                                                          RowRec *__restrict__ rows, uint32_t n)
+{
+	const uint32_t lane = threadIdx.x & 63;
+	const uint32_t nwaves = gridDim.x * 4;
+	for (uint32_t r = (blockIdx.x * 256 + threadIdx.x) >> 6; r < n; r += nwaves) {
+		const uint64_t b = row_ptr[r], en = row_ptr[r + 1];
+		double qe[KP], q[KP], z[KP];
+#pragma unroll
+		for (int c = 0; c < KP; ++c) { qe[c] = 0.0; q[c] = 0.0; z[c] = 0.0; }
+		double qqe = 0.0, qq = 0.0;
+		for (uint64_t p0 = b; p0 < en; p0 += 64) {
+			const uint32_t cnt = (uint32_t)min<uint64_t>(64, en - p0);
+			const uint2 mine = lane < cnt ? csr[p0 + lane] : make_uint2(0u, 0u);
+			for (uint32_t i = 0; i < cnt; ++i) {
+				const uint32_t j = __shfl(mine.x, (int)i, 64);
+				const float x = __uint_as_float(__shfl(mine.y, (int)i, 64));
+				const double2 *m = ms_v + (size_t)j * k;
+#pragma unroll
+				for (int c = 0; c < KP; ++c) {
+					const int f = (int)lane + 64 * c;
+					if (f < k) {
+						const double2 vm = m[f];
+						qe[c] += vm.x * x;                          // fm_learn_vb.h:93-133
+						qqe -= 0.5 * vm.x * vm.x * x * x;           // :136-163
+						q[c] += vm.x * x * vm.x * x;                // :222-254
+						z[c] += vm.y * x * x;
+						qq -= (vm.x * vm.x * x * x * x * x * vm.y + 0.5 * x * x * x * x * vm.y * vm.y);   // :257-281
+					}
+				}
+			}
+		}
+		double e = 0.0, t = 0.0;
+#pragma unroll
+		for (int c = 0; c < KP; ++c)
+			if ((int)lane + 64 * c < k) {
+				e += 0.5 * qe[c] * qe[c];
+				t += (0.5 * z[c] * z[c] + z[c] * q[c]);
+			}
+		e = wave_sum(e);
+		qqe = wave_sum(qqe);
+		t = wave_sum(t);
+		qq = wave_sum(qq);
+		if (k1)                                                 // :166-188 / :284-301
+			for (uint64_t p = b; p < en; ++p) {
+				const uint2 ent = csr[p];
+				const float x = ent_x(ent);
+				const double2 w = ms_w[ent.x];
+				qqe += w.x * x;
+				qq += w.y * x * x;
+			}
+		e = e + qqe;
+		if (k0) e += mu0;
+		t = t + qq;                                             // :304-311
+		if (k0) t += s0d;
+		if (lane == 0) {
+			rows[r].e = target[r] - e;
+			rows[r].t = t;
+		}
+	}
+}
+
 // e = y - yhat (fm_learn_vb_simultaneous.h:42-44)
 __global__ void k_residual_init(RowRec *rows, const double *yhat, const float *target, uint32_t n)
 {
@@ -1012,6 +1084,25 @@ hipError_t predict_t(const uint64_t *row_ptr, const uint2 *csr, const double2 *m
 	else if (blocked) k_predict_t_blocked<8><<<grid_for(n), 256, 0, s>>>(row_ptr, csr, ms_v, ms_w, k, k1, k0, s0d, rows, n);
 	else k_predict_t<<<grid_for(n), 256, 0, s>>>(row_ptr, csr, ms_v, ms_w, k, k1, k0, s0d, rows, n);
 	return hipGetLastError();
+}
+
+// e = y - yhat and T of a train set's rows; the one-pass kernel where the wave form applies
+hipError_t predict_et(const uint64_t *row_ptr, const uint2 *csr, const double2 *ms_v, const double2 *ms_w, int k, int k1,
+                      int k0, double mu0, double s0d, const float *target, double *scratch, RowRec *rows, uint32_t n,
+                      int blocked, hipStream_t s)
+{
+	if (n == 0) return hipSuccess;
+	const unsigned wg = (unsigned)std::min<uint64_t>(((uint64_t)n + 3) / 4, 8192);
+	if (blocked == 2 && k <= 256) {
+		if (k <= 64) k_predict_et_wave<1><<<wg, 256, 0, s>>>(row_ptr, csr, ms_v, ms_w, k, k1, k0, mu0, s0d, target, rows, n);
+		else if (k <= 128) k_predict_et_wave<2><<<wg, 256, 0, s>>>(row_ptr, csr, ms_v, ms_w, k, k1, k0, mu0, s0d, target, rows, n);
+		else k_predict_et_wave<4><<<wg, 256, 0, s>>>(row_ptr, csr, ms_v, ms_w, k, k1, k0, mu0, s0d, target, rows, n);
+		return hipGetLastError();
+	}
+	hipError_t e = predict_e(row_ptr, csr, ms_v, ms_w, k, k1, k0, mu0, scratch, n, blocked, s);
+	if (e == hipSuccess) e = predict_t(row_ptr, csr, ms_v, ms_w, k, k1, k0, s0d, rows, n, blocked, s);
+	if (e == hipSuccess) e = residual_init(rows, scratch, target, n, s);
+	return e;
 }
 
 hipError_t residual_init(RowRec *rows, const double *yhat, const float *target, uint32_t n, hipStream_t s)

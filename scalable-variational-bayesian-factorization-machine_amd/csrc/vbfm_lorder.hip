@@ -413,6 +413,7 @@ __global__ __launch_bounds__(BLOCK) void k_lord_defer(LevelArgs a)
 	op.mo = msj.x; op.so = msj.y;
 	const double2 nx = NEXT ? a.ms_next[(size_t)j * a.ms_stride_next] : make_double2(0.0, 0.0);
 	const bool first = a.first_level != 0;
+	const bool pending = (a.pending & 1) != 0, nt = (a.pending & 2) != 0;
 	double s1 = 0.0, s2 = 0.0;
 	for (uint32_t base = 0; base < n; base += CAP) {
 		const uint32_t m = min(CAP, n - base);
@@ -421,14 +422,14 @@ __global__ __launch_bounds__(BLOCK) void k_lord_defer(LevelArgs a)
 		// one line each) while the run streams into LDS
 		PostT t[R];
 		float pxv[R];
-		if (a.pending) {
+		if (pending) {
 #pragma unroll
 			for (int u = 0; u < R; ++u) {
 				const uint32_t i = threadIdx.x + u * BLOCK;
 				if (i < m) { t[u] = a.tab[pidx[base + i]]; pxv[u] = px[base + i]; }
 			}
 		}
-		if (a.pending) stage_in_nt<BLOCK>(recs, s + (size_t)base * 4, m);
+		if (nt) stage_in_nt<BLOCK>(recs, s + (size_t)base * 4, m);
 		else stage_in<BLOCK>(recs, s + (size_t)base * 4, m);
 		__syncthreads();
 #pragma unroll
@@ -438,9 +439,9 @@ __global__ __launch_bounds__(BLOCK) void k_lord_defer(LevelArgs a)
 			Rec v;
 			lds_get(recs, i, v);
 			const float x = lx[base + i];
-			if (a.pending) apply_pending<IS_W, P>(v, t[u], pxv[u]);
+			if (pending) apply_pending<IS_W, P>(v, t[u], pxv[u]);
 			if constexpr (NEXT) add_next_q<IS_W, P>(v, x, first, nx);
-			if (a.pending || NEXT) lds_put(recs, i, v);
+			if (pending || NEXT) lds_put(recs, i, v);
 			op.stat(v, x, s1, s2);
 			dsts[i] = nxt[base + i];
 		}

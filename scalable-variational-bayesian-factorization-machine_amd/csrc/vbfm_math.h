@@ -60,16 +60,30 @@ DEVI bool dinf(double v) { return __builtin_isinf(v); }
 // row record access. v[0] = (e, q0), v[1] = (tq0, tz0), v[2] = (t, q1), v[3] = (tq1, tz1)
 typedef double2 Rec[4];
 
+// 16-B vector loads / stores, element-wise into the record: a piece a kernel leaves untouched
+// then stays in registers (a whole-struct copy can leave it as a memcpy through scratch / LDS)
+typedef double rec_v2 __attribute__((ext_vector_type(2)));
 DEVI void load_rec(const RowRec *rows, uint32_t r, Rec &v)
 {
-	const double2 *p = reinterpret_cast<const double2 *>(rows + r);
-	v[0] = p[0]; v[1] = p[1]; v[2] = p[2]; v[3] = p[3];
+	const rec_v2 *p = reinterpret_cast<const rec_v2 *>(rows + r);
+#pragma unroll
+	for (int c = 0; c < 4; ++c) {
+		const rec_v2 t = p[c];
+		v[c].x = t.x;
+		v[c].y = t.y;
+	}
 }
 
 DEVI void store_rec(RowRec *rows, uint32_t r, const Rec &v)
 {
-	double2 *p = reinterpret_cast<double2 *>(rows + r);
-	p[0] = v[0]; p[1] = v[1]; p[2] = v[2]; p[3] = v[3];
+	rec_v2 *p = reinterpret_cast<rec_v2 *>(rows + r);
+#pragma unroll
+	for (int c = 0; c < 4; ++c) {
+		rec_v2 t;
+		t.x = v[c].x;
+		t.y = v[c].y;
+		p[c] = t;
+	}
 }
 
 template <int S> DEVI double &Q(Rec &v) { return S == 0 ? v[0].y : v[2].y; }

@@ -62,20 +62,22 @@ __global__ void k_ov_local(const uint32_t *rows_sorted, const uint32_t *bat, con
 
 // every CSC entry keyed by its row's batch, its row renumbered within the batch (the
 // first-entry flag kept: a row's smallest feature is the same in the batch), and the
-// (batch, column) histogram
-__global__ __launch_bounds__(256) void k_ov_entries(const uint64_t *col_ptr, const uint2 *csc, const uint32_t *bat,
-                                                    const uint32_t *loc, uint32_t nf, uint16_t *key, uint2 *val,
-                                                    uint32_t *cnt)
+// (batch, level position) histogram. The columns are taken in level order (column i of the
+// level-ordered feature list at lvcp[i]), so that after the stable sort by batch a batch's
+// columns are in level order too and its col_ptr is indexed by level position.
+__global__ __launch_bounds__(256) void k_ov_entries(const uint64_t *col_ptr, const uint2 *csc, const uint32_t *feats,
+                                                    const uint64_t *lvcp, const uint32_t *bat, const uint32_t *loc,
+                                                    uint32_t nf, uint16_t *key, uint2 *val, uint32_t *cnt)
 {
-	const uint32_t j = blockIdx.x;
-	const uint64_t b = col_ptr[j], e = col_ptr[j + 1];
+	const uint32_t i = blockIdx.x, j = feats[i];
+	const uint64_t b = col_ptr[j], e = col_ptr[j + 1], o = lvcp[i] - b;
 	for (uint64_t p = b + threadIdx.x; p < e; p += 256) {
 		const uint2 ent = csc[p];
 		const uint32_t r = ent.x & ROW_MASK;
 		const uint32_t bb = bat[r];
-		key[p] = (uint16_t)bb;
-		val[p] = make_uint2(loc[r] | (ent.x & ROW_FIRST), ent.y);
-		atomicAdd(&cnt[(size_t)bb * nf + j], 1u);
+		key[o + p] = (uint16_t)bb;
+		val[o + p] = make_uint2(loc[r] | (ent.x & ROW_FIRST), ent.y);
+		atomicAdd(&cnt[(size_t)bb * nf + i], 1u);
 	}
 }
 
@@ -173,11 +175,26 @@ __global__ __launch_bounds__(256) void k_ov_v_level(LevelArgs a)
 	const uint32_t col_i = G <= 64 ? blockIdx.x * (256 / G) + threadIdx.x / G : blockIdx.x;
 	const uint32_t lane = G <= 64 ? threadIdx.x % G : threadIdx.x;
 	if (col_i >= a.nfeat) return;   // whole lane groups (G <= 64) or the whole workgroup
-	const uint32_t j = a.feats[col_i];
-	const uint64_t cb = a.col_ptr[j];
-	const uint32_t n = (uint32_t)(a.col_ptr[j + 1] - cb);
+	// the batch's col_ptr is indexed by level position (ov_regroup): coalesced, and the
+	// column's entries can be fetched in parallel with its parameters
+	const uint64_t cb = a.col_ptr[col_i];
+	const uint32_t n = (uint32_t)(a.col_ptr[col_i + 1] - cb);
 	if (n == 0) return;   // columns without entries in the batch are skipped (:389-394)
+	const uint32_t j = a.feats[col_i];
 	const uint2 *col = a.csc + cb;
+	// the lane's first two entries stay in registers from the statistics to the correction
+	// (named, not an array: an array of records gets demoted to LDS / scratch)
+	const bool h0 = lane < n, h1 = lane + G < n;
+	uint2 ent0 = make_uint2(0u, 0u), ent1 = make_uint2(0u, 0u);
+	Rec v0, v1;
+	if (h0) {
+		ent0 = col[lane];
+		load_rec(a.rows, ent0.x & ROW_MASK, v0);
+	}
+	if (h1) {
+		ent1 = col[lane + G];
+		load_rec(a.rows, ent1.x & ROW_MASK, v1);
+	}
 	const size_t pi = (size_t)j * a.ms_stride;
 	const double2 msj = a.ms[pi], natj = a.nat[pi];
 	const double mo = msj.x, so = msj.y;
@@ -190,14 +207,19 @@ __global__ __launch_bounds__(256) void k_ov_v_level(LevelArgs a)
 	double2 nx = make_double2(0.0, 0.0);
 	if constexpr (NEXT) nx = a.ms_next[(size_t)j * a.ms_stride_next];
 	double eta1 = 0.0, eta2 = 0.0;
-	for (uint32_t i = lane; i < n; i += G) {
-		const uint2 ent = col[i];
-		Rec v;
-		load_rec(a.rows, ent.x & ROW_MASK, v);
+	auto stat = [&](uint2 e, Rec &r) {
 		double vm = 0.0, vs = 0.0;
-		v_stat(ent_x(ent), E(v), Q<P>(v), TQ<P>(v), mo, so, vm, vs);
+		v_stat(ent_x(e), E(r), Q<P>(r), TQ<P>(r), mo, so, vm, vs);
 		eta2 += keep_s + rho * (sv_g + acc * vs);
 		eta1 += keep_m + rca * vm;
+	};
+	if (h0) stat(ent0, v0);
+	if (h1) stat(ent1, v1);
+	for (uint32_t i = lane + 2 * G; i < n; i += G) {
+		const uint2 e = col[i];
+		Rec r;
+		load_rec(a.rows, e.x & ROW_MASK, r);
+		stat(e, r);
 	}
 	group_sum2<G>(eta1, eta2, lds);
 	const double nmu = eta1 / n, nsig = eta2 / n;
@@ -236,12 +258,20 @@ __global__ __launch_bounds__(256) void k_ov_v_level(LevelArgs a)
 			}
 		return;
 	}
-	for (uint32_t i = lane; i < n; i += G) {
-		const uint2 ent = col[i];
-		Rec v;
-		load_rec(a.rows, ent.x & ROW_MASK, v);
-		v_apply<P, NEXT>(v, ent_x(ent), (ent.x & a.first_mask) != 0, go, mo, so, mu, sig, nx);
-		store_rec(a.rows, ent.x & ROW_MASK, v);
+	if (h0) {
+		v_apply<P, NEXT>(v0, ent_x(ent0), (ent0.x & a.first_mask) != 0, go, mo, so, mu, sig, nx);
+		store_rec(a.rows, ent0.x & ROW_MASK, v0);
+	}
+	if (h1) {
+		v_apply<P, NEXT>(v1, ent_x(ent1), (ent1.x & a.first_mask) != 0, go, mo, so, mu, sig, nx);
+		store_rec(a.rows, ent1.x & ROW_MASK, v1);
+	}
+	for (uint32_t i = lane + 2 * G; i < n; i += G) {
+		const uint2 e = col[i];
+		Rec r;
+		load_rec(a.rows, e.x & ROW_MASK, r);
+		v_apply<P, NEXT>(r, ent_x(e), (e.x & a.first_mask) != 0, go, mo, so, mu, sig, nx);
+		store_rec(a.rows, e.x & ROW_MASK, r);
 	}
 }
 
@@ -254,10 +284,10 @@ __global__ __launch_bounds__(256) void k_ov_w_level(LevelArgs a)
 	const uint32_t col_i = G <= 64 ? blockIdx.x * (256 / G) + threadIdx.x / G : blockIdx.x;
 	const uint32_t lane = G <= 64 ? threadIdx.x % G : threadIdx.x;
 	if (col_i >= a.nfeat) return;
-	const uint32_t j = a.feats[col_i];
-	const uint64_t cb = a.col_ptr[j];
-	const uint32_t n = (uint32_t)(a.col_ptr[j + 1] - cb);
+	const uint64_t cb = a.col_ptr[col_i];
+	const uint32_t n = (uint32_t)(a.col_ptr[col_i + 1] - cb);
 	if (n == 0) return;   // (:364-368)
+	const uint32_t j = a.feats[col_i];
 	const uint2 *col = a.csc + cb;
 	const size_t pi = (size_t)j * a.ms_stride;
 	const double2 msj = a.ms[pi], natj = a.nat[pi];
@@ -384,7 +414,9 @@ struct OvState {
 	uint2 *ent_sorted = nullptr;   // all entries, batch-major, column-major inside a batch
 	uint2 *ent_tmp = nullptr;
 	uint32_t *cnt = nullptr;       // [num_batch * nf] (batch, column) entry counts
-	uint64_t *gptr = nullptr;      // [num_batch * nf + 1] their prefix sums: col_ptr of every batch
+	uint64_t *gptr = nullptr;      // [num_batch * nf + 1] their prefix sums: col_ptr of every batch,
+	                               // indexed by level position (level_feats order)
+	uint64_t *lvcp = nullptr;      // [nf + 1] start of each level-ordered column in the whole train set
 	std::vector<uint64_t> rstart;  // [num_batch + 1] first sorted row of each batch
 	uint64_t *rstart_d = nullptr;
 	void *tmp = nullptr;
@@ -410,7 +442,7 @@ void ov_free(vbfm_ctx *c)
 	dfree(o.nat_w); dfree(o.nat_v); dfree(o.new_wj); dfree(o.new_vj); dfree(o.t_wj); dfree(o.t_vj);
 	dfree(o.ccount); dfree(o.sh_d); dfree(o.bat_d); dfree(o.iota_d); dfree(o.rows_sorted); dfree(o.bat_sorted);
 	dfree(o.loc_d); dfree(o.key_in); dfree(o.key_out); dfree(o.ent_sorted); dfree(o.ent_tmp); dfree(o.cnt);
-	dfree(o.gptr); dfree(o.rstart_d); dfree(o.tmp); dfree(o.rp_b); dfree(o.len_b); dfree(o.csr_b); dfree(o.t_b);
+	dfree(o.gptr); dfree(o.lvcp); dfree(o.rstart_d); dfree(o.tmp); dfree(o.rp_b); dfree(o.len_b); dfree(o.csr_b); dfree(o.t_b);
 	dfree(o.rows_b);
 	for (hipEvent_t e : o.ev)
 		if (e) (void)hipEventDestroy(e);
@@ -428,6 +460,7 @@ void ov_level_args(vbfm_ctx *c, LevelArgs &a, bool is_w, int f)
 	a.tcount = is_w ? o.t_wj : (f == 0 ? o.t_vj : nullptr);
 	if (!is_w) o.launches_v++;
 	a.avg_len = a.avg_len / std::max(o.num_batch, 1u);   // the batch's share of the mean column
+	a.col_ptr += a.feats - c->level_feats;               // the batch's col_ptr by level position
 }
 
 }  // namespace vbi
@@ -475,7 +508,9 @@ void ov_regroup(vbfm_ctx *c)
 	HIPCHK(hipGetLastError());
 	// entries
 	HIPCHK(hipMemsetAsync(o.cnt, 0, (size_t)nb * nf * 4, c->s));
-	if (nf) k_ov_entries<<<nf, 256, 0, c->s>>>(c->tr.col_ptr, c->tr.csc, o.bat_d, o.loc_d, nf, o.key_in, o.ent_tmp, o.cnt);
+	if (nf)
+		k_ov_entries<<<nf, 256, 0, c->s>>>(c->tr.col_ptr, c->tr.csc, c->level_feats, o.lvcp, o.bat_d, o.loc_d, nf, o.key_in,
+		                                   o.ent_tmp, o.cnt);
 	HIPCHK(hipGetLastError());
 	tb = 0;
 	HIPCHK(rocprim::radix_sort_pairs(nullptr, tb, o.key_in, o.key_out, o.ent_tmp, o.ent_sorted, (size_t)nnz, 0, bits,
@@ -654,6 +689,15 @@ int vbfm_online_init(vbfm_ctx *c, const vbfm_online_config *cfg)
 			o.ent_tmp = dalloc<uint2>(nnz); o.ent_sorted = dalloc<uint2>(nnz);
 			o.cnt = dalloc<uint32_t>((size_t)nb * nf);
 			o.gptr = dalloc<uint64_t>((size_t)nb * nf + 1);
+			{
+				std::vector<uint64_t> cp((size_t)nf + 1), lv((size_t)nf + 1, 0);
+				std::vector<uint32_t> feats(nf);
+				HIPCHK(hipMemcpy(cp.data(), c->tr.col_ptr, cp.size() * 8, hipMemcpyDeviceToHost));
+				if (nf) HIPCHK(hipMemcpy(feats.data(), c->level_feats, (size_t)nf * 4, hipMemcpyDeviceToHost));
+				for (uint32_t i = 0; i < nf; i++) lv[i + 1] = lv[i] + (cp[feats[i] + 1] - cp[feats[i]]);
+				o.lvcp = dalloc<uint64_t>(lv.size());
+				HIPCHK(hipMemcpy(o.lvcp, lv.data(), lv.size() * 8, hipMemcpyHostToDevice));
+			}
 			o.rstart_d = dalloc<uint64_t>((size_t)nb + 1);
 			c->q_ready[0] = c->q_ready[1] = -1;
 			sync(c);
@@ -727,11 +771,8 @@ int vbfm_online_epoch(vbfm_ctx *c, vbfm_online_stats *out)
 				c->q_ready[0] = c->q_ready[1] = -1;
 				// fresh caches of the batch (:111-139)
 				const int bl = blocked_predict(c, c->tr);
-				HIPCHK(vbk::predict_e(c->tr.row_ptr, c->tr.csr, c->ms_v, c->ms_w, c->k, c->k1, c->k0, c->mu0,
-				                      c->scratch_n, n, bl, c->s));
-				HIPCHK(vbk::predict_t(c->tr.row_ptr, c->tr.csr, c->ms_v, c->ms_w, c->k, c->k1, c->k0, c->s0d, c->rows,
-				                      n, bl, c->s));
-				HIPCHK(vbk::residual_init(c->rows, c->scratch_n, c->tr.target, n, c->s));
+				HIPCHK(vbk::predict_et(c->tr.row_ptr, c->tr.csr, c->ms_v, c->ms_w, c->k, c->k1, c->k0, c->mu0, c->s0d,
+				                       c->tr.target, c->scratch_n, c->rows, n, bl, c->s));
 				// update_all(train1, train.num_cases) (fm_learn_vb_online.h:354-469)
 				HIPCHK(hipEventRecord(bev[1], c->s));
 				if (c->k0) ov_step_w0(c);

@@ -335,6 +335,30 @@ def test_wave_prediction_many_factors(k, monkeypatch):
     np.testing.assert_allclose(g.test_e(), oc.arr(o.s.e_test, o.s.n_test), rtol=1e-12, atol=1e-12)
 
 
+@pytest.mark.parametrize("k,dim", [(8, (1, 1)), (70, (1, 1)), (130, (0, 1)), (20, (1, 0))])
+def test_fused_train_prediction_equals_test_prediction(k, dim, monkeypatch):
+    """init_caches predicts e and T of the train rows in one pass (k_predict_et_wave); the
+    test set goes through predict_e alone. With the test set = the train set, the fused
+    kernel's y - yhat must equal y - (the separate kernel's yhat) bit for bit."""
+    monkeypatch.setenv("VBFM_PREDICT", "wave")
+    n, F, S, seed = 3000, 6, 80, 41
+    rp, f, v, y = synth.generate(n, F, S, seed, 1)
+    D = F * S + 1
+    g = vbfm.FMLearnVB(dim[0], dim[1], k, D, min_target=float(y.min()), max_target=float(y.max()))
+    g.init(9, 0.1)
+    ds = vbfm.DataSubset.from_csr(rp, f, v, y, F * S)
+    g.set_data(ds, vbfm.DataSubset.from_csr(rp, f, v, y, F * S))
+    g.init_caches()
+    yhat = g.test_e()
+    rows = g.rows()
+    np.testing.assert_array_equal(rows["e"], y.astype(np.float64) - yhat)
+    o = oc.VB(dim[0], dim[1], k, D)
+    o.init_params(9, 0.1)
+    o.attach(oc.Data(csr=(n, rp, f, v, y)), oc.Data(csr=(n, rp, f, v, y)))
+    o.init_caches()
+    close(rows["t"], o.rows()["t"], 1e-12)
+
+
 @pytest.mark.parametrize("P", [1, 2, 3])
 def test_feature_shards_vs_oracle(P):
     """VBFM_SHARD_FEATURES (the north star's column partition) with P shards run one after
