@@ -187,8 +187,10 @@ int or_load_libfm(const char *path, or_data *out, char *err, int errlen)
 			}
 			if (rc == 0) continue;
 			if (pass == 0) {
-				if (tgt < out->min_target) out->min_target = tgt;
-				if (tgt > out->max_target) out->max_target = tgt;
+				/* std::min(_value, min_target) / std::max(_value, max_target) (Data.h:200-201):
+				 * a NaN target resets both, as the reference's std::min / std::max do */
+				out->min_target = (out->min_target < tgt) ? out->min_target : tgt;
+				out->max_target = (tgt < out->max_target) ? out->max_target : tgt;
 				rows++;
 				nnz += n;
 				if (n) has_feature = 1;
@@ -228,8 +230,8 @@ int or_data_from_csr(uint32_t num_rows, uint64_t nnz, const uint64_t *row_ptr,
 	out->min_target = 3.40282347e+38f;
 	out->max_target = -3.40282347e+38f;
 	for (i = 0; i < num_rows; i++) {
-		if (target[i] < out->min_target) out->min_target = target[i];
-		if (target[i] > out->max_target) out->max_target = target[i];
+		out->min_target = (out->min_target < target[i]) ? out->min_target : target[i];   /* Data.h:164-165 */
+		out->max_target = (target[i] < out->max_target) ? out->max_target : target[i];
 	}
 	for (j = 0; j < nnz; j++) if ((int)row_feat[j] > maxf) maxf = (int)row_feat[j];
 	out->num_feature = (uint32_t)(maxf + 1);

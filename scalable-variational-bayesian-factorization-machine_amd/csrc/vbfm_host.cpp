@@ -193,6 +193,7 @@ int load_text(const char *fn, vbfm_host_data *out)
 		std::vector<uint32_t> len;
 		int maxf = -1;
 		bool has_feature = false;
+		bool has_nan = false;   // a NaN target: the fold below restarts there
 		float mn = 3.40282347e+38f, mx = -3.40282347e+38f;
 		LineError err;
 	};
@@ -214,8 +215,9 @@ int load_text(const char *fn, vbfm_host_data *out)
 			}
 			if (rc > 0) {
 				if (P.ents.size() > before) P.has_feature = true;
-				P.mn = std::min(y, P.mn);
+				P.mn = std::min(y, P.mn);   // Data.h:200-201
 				P.mx = std::max(y, P.mx);
+				if (y != y) P.has_nan = true;
 				P.target.push_back(y);
 				P.len.push_back((uint32_t)(P.ents.size() - before));
 			}
@@ -236,7 +238,11 @@ int load_text(const char *fn, vbfm_host_data *out)
 		ent0[t + 1] = ent0[t] + part[t].ents.size();
 		maxf = std::max(maxf, part[t].maxf);
 		has_feature |= part[t].has_feature;
-		if (!part[t].target.empty()) { mn = std::min(part[t].mn, mn); mx = std::max(part[t].mx, mx); }
+		// std::min(y, m) is not associative once a NaN appears (the fold returns the NaN, then
+		// restarts from the next value), so a part holding a NaN target replaces the running
+		// range: its own fold does not depend on where it started
+		if (part[t].has_nan) { mn = part[t].mn; mx = part[t].mx; }
+		else if (!part[t].target.empty()) { mn = std::min(part[t].mn, mn); mx = std::max(part[t].mx, mx); }
 	}
 	nrows = row0[T]; nnz = ent0[T];
 	if (nrows > 0xFFFFFFFFull) { g_host_err = "too many rows"; return -1; }
@@ -251,8 +257,8 @@ int load_text(const char *fn, vbfm_host_data *out)
 	out->row_ptr[0] = 0;
 	parallel(T, [&](int t) {
 		const Part &P = part[t];
-		memcpy(out->target + row0[t], P.target.data(), P.target.size() * sizeof(float));
-		memcpy(out->row_ent + ent0[t], P.ents.data(), P.ents.size() * sizeof(vbfm_entry));
+		if (!P.target.empty()) memcpy(out->target + row0[t], P.target.data(), P.target.size() * sizeof(float));
+		if (!P.ents.empty()) memcpy(out->row_ent + ent0[t], P.ents.data(), P.ents.size() * sizeof(vbfm_entry));
 		uint64_t a = ent0[t];
 		for (size_t i = 0; i < P.len.size(); i++) { a += P.len[i]; out->row_ptr[row0[t] + i + 1] = a; }
 	});

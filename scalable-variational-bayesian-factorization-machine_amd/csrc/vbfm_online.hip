@@ -176,11 +176,12 @@ __global__ __launch_bounds__(256) void k_ov_v_level(LevelArgs a)
 	const uint32_t lane = G <= 64 ? threadIdx.x % G : threadIdx.x;
 	if (col_i >= a.nfeat) return;   // whole lane groups (G <= 64) or the whole workgroup
 	// the batch's col_ptr is indexed by level position (ov_regroup): coalesced, and the
-	// column's entries can be fetched in parallel with its parameters
+	// column's entries can be fetched in parallel with its parameters (the feature id is
+	// loaded with the bounds, before the branch on the column length)
+	const uint32_t j = a.feats[col_i];
 	const uint64_t cb = a.col_ptr[col_i];
 	const uint32_t n = (uint32_t)(a.col_ptr[col_i + 1] - cb);
 	if (n == 0) return;   // columns without entries in the batch are skipped (:389-394)
-	const uint32_t j = a.feats[col_i];
 	const uint2 *col = a.csc + cb;
 	// the lane's first two entries stay in registers from the statistics to the correction
 	// (named, not an array: an array of records gets demoted to LDS / scratch)
