@@ -173,6 +173,11 @@ hipError_t predict_t(const uint64_t *row_ptr, const uint2 *csr, const double2 *m
                      int k, int k1, int k0, double sigma0_dash, RowRec *rows, uint32_t n, int blocked,
                      hipStream_t s);
 hipError_t residual_init(RowRec *rows, const double *yhat, const float *target, uint32_t n, hipStream_t s);
+// predict_e reading the factors' mu from a compact [j*k + f] copy vc (kd = k*D doubles; refresh:
+// copy it from ms_v first); falls back to predict_e where the wave form does not apply
+hipError_t predict_e_compact(const uint64_t *row_ptr, const uint2 *csr, const double2 *ms_v, const double2 *ms_w, int k,
+                             int k1, int k0, double mu0, double *out, uint32_t n, int blocked, double *vc, size_t kd,
+                             bool refresh, hipStream_t s);
 hipError_t predict_et(const uint64_t *row_ptr, const uint2 *csr, const double2 *ms_v, const double2 *ms_w, int k, int k1,
                       int k0, double mu0, double s0d, const float *target, double *scratch, RowRec *rows, uint32_t n,
                       int blocked, hipStream_t s);

@@ -477,6 +477,28 @@ __global__ __launch_bounds__(256) void k_predict_t_blocked(const uint64_t *__res
 	rows[r].t = t;
 }
 
+// entries whose factor runs a wave-form prediction kernel loads before accumulating them (in
+// entry order): several independent gathers in flight per wave instead of one
+constexpr int wave_pu(int KP) { return KP >= 4 ? 2 : (KP == 2 ? 4 : 8); }
+
+template <int KP, int PU>
+DEVI void wave_gather(uint2 mine, uint32_t cnt, uint32_t i0, uint32_t lane, const double2 *__restrict__ ms_v, int k,
+                      double2 (&mv)[PU][KP], float (&xs)[PU])
+{
+#pragma unroll
+	for (int u = 0; u < PU; ++u) {
+		const int i = (int)min(i0 + u, cnt - 1);
+		const uint32_t j = __shfl(mine.x, i, 64);
+		xs[u] = __uint_as_float(__shfl(mine.y, i, 64));
+#pragma unroll
+		for (int c = 0; c < KP; ++c) {
+			const int f = (int)lane + 64 * c;
+			mv[u][c] = make_double2(0.0, 0.0);
+			if (f < k && i0 + u < cnt) mv[u][c] = ms_v[(size_t)j * k + f];
+		}
+	}
+}
+
 // Wave form (large data sets): one 64-lane wave per row, factor f on lane f % 64 (pass
 // f / 64, KP passes). Each entry's k {mu, sigma} pairs are one contiguous run, read by the
 // wave as whole 1 KiB pieces instead of one strided pair per thread; the row's entries are
@@ -484,12 +506,16 @@ __global__ __launch_bounds__(256) void k_predict_t_blocked(const uint64_t *__res
 // row's entries for its factors; the per-factor terms are summed across lanes in a fixed
 // butterfly (~1 ulp from the reference's sequential factor order, like the blocked form),
 // the linear term is added after them in the reference's entry order.
-template <int KP>
+// COMPACT: the factors come from a plain [j*k + f] array of mu (vc) instead of the {mu, sigma}
+// pairs: half the bytes per entry (the MCMC learner's per-iteration re-prediction, where the
+// pairs hold {v, 0})
+template <int KP, bool COMPACT = false>
 __global__ __launch_bounds__(256) void k_predict_e_wave(const uint64_t *__restrict__ row_ptr,
                                                          const uint2 *__restrict__ csr,
                                                          const double2 *__restrict__ ms_v,
                                                          const double2 *__restrict__ ms_w, int k, int k1, int k0,
-                                                         double mu0, double *__restrict__ out, uint32_t n)
+                                                         double mu0, double *__restrict__ out, uint32_t n,
+                                                         const double *__restrict__ vc = nullptr)
 {
 	const uint32_t lane = threadIdx.x & 63;
 	const uint32_t nwaves = gridDim.x * 4;
@@ -499,21 +525,36 @@ __global__ __launch_bounds__(256) void k_predict_e_wave(const uint64_t *__restri
 #pragma unroll
 		for (int c = 0; c < KP; ++c) q[c] = 0.0;
 		double qq = 0.0;
+		constexpr int PU = wave_pu(KP);
 		for (uint64_t p0 = b; p0 < en; p0 += 64) {
 			const uint32_t cnt = (uint32_t)min<uint64_t>(64, en - p0);
 			const uint2 mine = lane < cnt ? csr[p0 + lane] : make_uint2(0u, 0u);
-			for (uint32_t i = 0; i < cnt; ++i) {
-				const uint32_t j = __shfl(mine.x, (int)i, 64);
-				const float x = __uint_as_float(__shfl(mine.y, (int)i, 64));
-				const double2 *m = ms_v + (size_t)j * k;
+			for (uint32_t i0 = 0; i0 < cnt; i0 += PU) {
+				// PU entries' factors in flight at once, then accumulated in entry order
+				double v[PU][KP];
+				float xs[PU];
 #pragma unroll
-				for (int c = 0; c < KP; ++c) {
-					const int f = (int)lane + 64 * c;
-					if (f < k) {
-						const double v = m[f].x;
-						q[c] += v * x;                             // :93-133
-						qq -= 0.5 * v * v * x * x;                 // :136-163
+				for (int u = 0; u < PU; ++u) {
+					const int i = (int)min(i0 + u, cnt - 1);
+					const uint32_t j = __shfl(mine.x, i, 64);
+					xs[u] = __uint_as_float(__shfl(mine.y, i, 64));
+#pragma unroll
+					for (int c = 0; c < KP; ++c) {
+						const int f = (int)lane + 64 * c;
+						v[u][c] = 0.0;
+						if (f < k && i0 + u < cnt) v[u][c] = COMPACT ? vc[(size_t)j * k + f] : ms_v[(size_t)j * k + f].x;
 					}
+				}
+#pragma unroll
+				for (int u = 0; u < PU; ++u) {
+					if (i0 + u >= cnt) break;
+					const float x = xs[u];
+#pragma unroll
+					for (int c = 0; c < KP; ++c)
+						if ((int)lane + 64 * c < k) {
+							q[c] += v[u][c] * x;                       // :93-133
+							qq -= 0.5 * v[u][c] * v[u][c] * x * x;     // :136-163
+						}
 				}
 			}
 		}
@@ -523,8 +564,15 @@ __global__ __launch_bounds__(256) void k_predict_e_wave(const uint64_t *__restri
 			if ((int)lane + 64 * c < k) e += 0.5 * q[c] * q[c];
 		e = wave_sum(e);
 		qq = wave_sum(qq);
-		if (k1)                                                // (3) :166-188
-			for (uint64_t p = b; p < en; ++p) { const uint2 ent = csr[p]; qq += ms_w[ent.x].x * ent_x(ent); }
+		if (k1) {                                              // (3) :166-188
+			// every lane gathers one entry's w, the wave adds them in entry order
+			for (uint64_t p0 = b; p0 < en; p0 += 64) {
+				const uint32_t cnt = (uint32_t)min<uint64_t>(64, en - p0);
+				double pe = 0.0;
+				if (lane < cnt) { const uint2 ent = csr[p0 + lane]; pe = ms_w[ent.x].x * ent_x(ent); }
+				for (uint32_t i = 0; i < cnt; ++i) qq += __shfl(pe, (int)i, 64);
+			}
+		}
 		e = e + qq;
 		if (k0) e += mu0;
 		if (lane == 0) out[r] = e;
@@ -546,22 +594,26 @@ __global__ __launch_bounds__(256) void k_predict_t_wave(const uint64_t *__restri
 #pragma unroll
 		for (int c = 0; c < KP; ++c) { q[c] = 0.0; z[c] = 0.0; }
 		double qq = 0.0;
+		constexpr int PU = wave_pu(KP);
 		for (uint64_t p0 = b; p0 < en; p0 += 64) {
 			const uint32_t cnt = (uint32_t)min<uint64_t>(64, en - p0);
 			const uint2 mine = lane < cnt ? csr[p0 + lane] : make_uint2(0u, 0u);
-			for (uint32_t i = 0; i < cnt; ++i) {
-				const uint32_t j = __shfl(mine.x, (int)i, 64);
-				const float x = __uint_as_float(__shfl(mine.y, (int)i, 64));
-				const double2 *m = ms_v + (size_t)j * k;
+			for (uint32_t i0 = 0; i0 < cnt; i0 += PU) {
+				double2 mv[PU][KP];
+				float xs[PU];
+				wave_gather<KP, PU>(mine, cnt, i0, lane, ms_v, k, mv, xs);
 #pragma unroll
-				for (int c = 0; c < KP; ++c) {
-					const int f = (int)lane + 64 * c;
-					if (f < k) {
-						const double2 vm = m[f];
-						q[c] += vm.x * x * vm.x * x;               // :222-254
-						z[c] += vm.y * x * x;
-						qq -= (vm.x * vm.x * x * x * x * x * vm.y + 0.5 * x * x * x * x * vm.y * vm.y);   // :257-281
-					}
+				for (int u = 0; u < PU; ++u) {
+					if (i0 + u >= cnt) break;
+					const float x = xs[u];
+#pragma unroll
+					for (int c = 0; c < KP; ++c)
+						if ((int)lane + 64 * c < k) {
+							const double2 vm = mv[u][c];
+							q[c] += vm.x * x * vm.x * x;               // :222-254
+							z[c] += vm.y * x * x;
+							qq -= (vm.x * vm.x * x * x * x * x * vm.y + 0.5 * x * x * x * x * vm.y * vm.y);   // :257-281
+						}
 				}
 			}
 		}
@@ -571,12 +623,18 @@ __global__ __launch_bounds__(256) void k_predict_t_wave(const uint64_t *__restri
 			if ((int)lane + 64 * c < k) t += (0.5 * z[c] * z[c] + z[c] * q[c]);
 		t = wave_sum(t);
 		qq = wave_sum(qq);
-		if (k1)                                                // (3) :284-301
-			for (uint64_t p = b; p < en; ++p) {
-				const uint2 ent = csr[p];
-				const float x = ent_x(ent);
-				qq += ms_w[ent.x].y * x * x;
+		if (k1) {                                              // (3) :284-301
+			for (uint64_t p0 = b; p0 < en; p0 += 64) {
+				const uint32_t cnt = (uint32_t)min<uint64_t>(64, en - p0);
+				double pt = 0.0;
+				if (lane < cnt) {
+					const uint2 ent = csr[p0 + lane];
+					const float x = ent_x(ent);
+					pt = ms_w[ent.x].y * x * x;
+				}
+				for (uint32_t i = 0; i < cnt; ++i) qq += __shfl(pt, (int)i, 64);
 			}
+		}
 		t = t + qq;                                            // :304-311
 		if (k0) t += s0d;
 		if (lane == 0) rows[r].t = t;
@@ -604,24 +662,28 @@ __global__ __launch_bounds__(256) void k_predict_et_wave(const uint64_t *__restr
 #pragma unroll
 		for (int c = 0; c < KP; ++c) { qe[c] = 0.0; q[c] = 0.0; z[c] = 0.0; }
 		double qqe = 0.0, qq = 0.0;
+		constexpr int PU = wave_pu(KP);
 		for (uint64_t p0 = b; p0 < en; p0 += 64) {
 			const uint32_t cnt = (uint32_t)min<uint64_t>(64, en - p0);
 			const uint2 mine = lane < cnt ? csr[p0 + lane] : make_uint2(0u, 0u);
-			for (uint32_t i = 0; i < cnt; ++i) {
-				const uint32_t j = __shfl(mine.x, (int)i, 64);
-				const float x = __uint_as_float(__shfl(mine.y, (int)i, 64));
-				const double2 *m = ms_v + (size_t)j * k;
+			for (uint32_t i0 = 0; i0 < cnt; i0 += PU) {
+				double2 mv[PU][KP];
+				float xs[PU];
+				wave_gather<KP, PU>(mine, cnt, i0, lane, ms_v, k, mv, xs);
 #pragma unroll
-				for (int c = 0; c < KP; ++c) {
-					const int f = (int)lane + 64 * c;
-					if (f < k) {
-						const double2 vm = m[f];
-						qe[c] += vm.x * x;                          // fm_learn_vb.h:93-133
-						qqe -= 0.5 * vm.x * vm.x * x * x;           // :136-163
-						q[c] += vm.x * x * vm.x * x;                // :222-254
-						z[c] += vm.y * x * x;
-						qq -= (vm.x * vm.x * x * x * x * x * vm.y + 0.5 * x * x * x * x * vm.y * vm.y);   // :257-281
-					}
+				for (int u = 0; u < PU; ++u) {
+					if (i0 + u >= cnt) break;
+					const float x = xs[u];
+#pragma unroll
+					for (int c = 0; c < KP; ++c)
+						if ((int)lane + 64 * c < k) {
+							const double2 vm = mv[u][c];
+							qe[c] += vm.x * x;                          // fm_learn_vb.h:93-133
+							qqe -= 0.5 * vm.x * vm.x * x * x;           // :136-163
+							q[c] += vm.x * x * vm.x * x;                // :222-254
+							z[c] += vm.y * x * x;
+							qq -= (vm.x * vm.x * x * x * x * x * vm.y + 0.5 * x * x * x * x * vm.y * vm.y);   // :257-281
+						}
 				}
 			}
 		}
@@ -636,14 +698,23 @@ __global__ __launch_bounds__(256) void k_predict_et_wave(const uint64_t *__restr
 		qqe = wave_sum(qqe);
 		t = wave_sum(t);
 		qq = wave_sum(qq);
-		if (k1)                                                 // :166-188 / :284-301
-			for (uint64_t p = b; p < en; ++p) {
-				const uint2 ent = csr[p];
-				const float x = ent_x(ent);
-				const double2 w = ms_w[ent.x];
-				qqe += w.x * x;
-				qq += w.y * x * x;
+		if (k1) {                                               // :166-188 / :284-301
+			for (uint64_t p0 = b; p0 < en; p0 += 64) {
+				const uint32_t cnt = (uint32_t)min<uint64_t>(64, en - p0);
+				double pe = 0.0, pt = 0.0;
+				if (lane < cnt) {
+					const uint2 ent = csr[p0 + lane];
+					const float x = ent_x(ent);
+					const double2 w = ms_w[ent.x];
+					pe = w.x * x;
+					pt = w.y * x * x;
+				}
+				for (uint32_t i = 0; i < cnt; ++i) {
+					qqe += __shfl(pe, (int)i, 64);
+					qq += __shfl(pt, (int)i, 64);
+				}
 			}
+		}
 		e = e + qqe;
 		if (k0) e += mu0;
 		t = t + qq;                                             // :304-311
@@ -1083,6 +1154,28 @@ hipError_t predict_t(const uint64_t *row_ptr, const uint2 *csr, const double2 *m
 	else if (blocked == 2 && k <= 256) k_predict_t_wave<4><<<wg, 256, 0, s>>>(row_ptr, csr, ms_v, ms_w, k, k1, k0, s0d, rows, n);
 	else if (blocked) k_predict_t_blocked<8><<<grid_for(n), 256, 0, s>>>(row_ptr, csr, ms_v, ms_w, k, k1, k0, s0d, rows, n);
 	else k_predict_t<<<grid_for(n), 256, 0, s>>>(row_ptr, csr, ms_v, ms_w, k, k1, k0, s0d, rows, n);
+	return hipGetLastError();
+}
+
+__global__ void k_compact_mu(const double2 *__restrict__ ms, double *__restrict__ out, size_t n)
+{
+	const size_t i = (size_t)blockIdx.x * 256u + threadIdx.x;
+	if (i < n) out[i] = ms[i].x;
+}
+
+// predict_e with the factors' mu compacted into vc ([j*k + f], refreshed here from ms_v) where
+// the wave form applies; otherwise predict_e itself. Same arithmetic and order: bit-identical.
+hipError_t predict_e_compact(const uint64_t *row_ptr, const uint2 *csr, const double2 *ms_v, const double2 *ms_w, int k,
+                             int k1, int k0, double mu0, double *out, uint32_t n, int blocked, double *vc, size_t kd,
+                             bool refresh, hipStream_t s)
+{
+	if (n == 0) return hipSuccess;
+	if (blocked != 2 || k > 256 || !vc) return predict_e(row_ptr, csr, ms_v, ms_w, k, k1, k0, mu0, out, n, blocked, s);
+	if (refresh && kd) k_compact_mu<<<(unsigned)((kd + 255) / 256), 256, 0, s>>>(ms_v, vc, kd);
+	const unsigned wg = (unsigned)std::min<uint64_t>(((uint64_t)n + 3) / 4, 8192);
+	if (k <= 64) k_predict_e_wave<1, true><<<wg, 256, 0, s>>>(row_ptr, csr, ms_v, ms_w, k, k1, k0, mu0, out, n, vc);
+	else if (k <= 128) k_predict_e_wave<2, true><<<wg, 256, 0, s>>>(row_ptr, csr, ms_v, ms_w, k, k1, k0, mu0, out, n, vc);
+	else k_predict_e_wave<4, true><<<wg, 256, 0, s>>>(row_ptr, csr, ms_v, ms_w, k, k1, k0, mu0, out, n, vc);
 	return hipGetLastError();
 }
 

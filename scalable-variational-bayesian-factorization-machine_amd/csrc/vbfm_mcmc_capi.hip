@@ -43,6 +43,7 @@ struct McState {
 	std::vector<double> z_h;
 	std::vector<uint8_t> col_nonempty;                    // [train nf] over all shards
 	double *pred_this = nullptr, *pred_sum = nullptr;     // [test rows]
+	double *vc = nullptr;                                 // [k*D] compact v for the re-prediction
 	double *red_d = nullptr;                              // [4 * MC_RED_BLOCKS]
 	std::vector<double> red_h;
 	uint32_t iter = 0;
@@ -57,7 +58,7 @@ void mc_free(vbfm_ctx *c)
 {
 	McState *m = c->mc;
 	if (!m) return;
-	dfree(m->hyp_d); dfree(m->z_d); dfree(m->pred_this); dfree(m->pred_sum); dfree(m->red_d);
+	dfree(m->hyp_d); dfree(m->z_d); dfree(m->pred_this); dfree(m->pred_sum); dfree(m->red_d); dfree(m->vc);
 	for (int i = 0; i < MEV_N; i++)
 		if (m->ev[i]) (void)hipEventDestroy(m->ev[i]);
 	delete m;
@@ -362,11 +363,18 @@ void mc_step_v(vbfm_ctx *c, int f)
 void mc_predict(vbfm_ctx *c)
 {
 	McState &m = *c->mc;
-	HIPCHK(vbk::predict_e(c->tr.row_ptr, c->tr.csr, c->ms_v, c->ms_w, c->k, c->k1, c->k0, m.w0, c->scratch_n, c->tr.n,
-	                      blocked_predict(c, c->tr), c->s));
+	// the parameters are {v, 0} pairs: the wave-form prediction reads a compact copy of v
+	// (half the bytes of every entry's k factors), refreshed once per re-prediction
+	const size_t kd = (size_t)c->k * c->D;
+	const int btr = blocked_predict(c, c->tr), bte = c->e_test ? blocked_predict(c, c->te) : 0;
+	if ((btr == 2 || bte == 2) && c->k <= 256 && kd && !m.vc) m.vc = dalloc<double>(kd);
+	bool fresh = false;
+	HIPCHK(vbk::predict_e_compact(c->tr.row_ptr, c->tr.csr, c->ms_v, c->ms_w, c->k, c->k1, c->k0, m.w0, c->scratch_n,
+	                              c->tr.n, btr, m.vc, kd, !fresh, c->s));
+	fresh = fresh || (btr == 2 && m.vc);
 	if (c->e_test)
-		HIPCHK(vbk::predict_e(c->te.row_ptr, c->te.csr, c->ms_v, c->ms_w, c->k, c->k1, c->k0, m.w0, c->e_test, c->te.n,
-		                      blocked_predict(c, c->te), c->s));
+		HIPCHK(vbk::predict_e_compact(c->te.row_ptr, c->te.csr, c->ms_v, c->ms_w, c->k, c->k1, c->k0, m.w0, c->e_test,
+		                              c->te.n, bte, m.vc, kd, !fresh, c->s));
 }
 
 void require_test(vbfm_ctx *c)

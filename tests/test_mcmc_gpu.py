@@ -156,3 +156,20 @@ def test_device_rng_layouts_agree(synth_files, monkeypatch):
         fml.close()
     assert rel_err(runs["level"][0], runs["column"][0]) <= 1e-10
     assert rel_err(runs["level"][1], runs["column"][1]) <= 1e-10
+
+
+@pytest.mark.parametrize("case", ["synth_als", "sa_mcmc", "tiny/mcmc_meta"])
+def test_wave_prediction_compact_chain_vs_reference(case, synth_files, sa_split, monkeypatch):
+    """The per-iteration re-prediction in its large-data form (VBFM_PREDICT=wave): the
+    factors read from a compact copy of v (vbk::predict_e_compact, half the bytes of the
+    {v, 0} pairs), the cross-factor sums in a butterfly (~1 ulp from the reference's order).
+    The whole chain still follows the reference's to REL."""
+    monkeypatch.setenv("VBFM_PREDICT", "wave")
+    t, a, fml, stats = run_case(case, synth_files, sa_split)
+    for it, st in enumerate(stats):
+        ref = t["trace"][it]
+        assert abs(st.rmse_all - ref["rmse_all"]) <= REL * ref["rmse_all"], (it, st.rmse_all, ref["rmse_all"])
+        assert abs(st.train_rmse - ref["train"]) <= REL * ref["train"], (it, st.train_rmse, ref["train"])
+    p = fml.get_params()
+    if "final_fm_v" in a:
+        assert rel_err(p["v"], a["final_fm_v"]) <= REL
