@@ -233,6 +233,7 @@ typedef struct {
 	double ms_predict, ms_w0, ms_w, ms_v, ms_hyper;
 	uint32_t n_vlevel_launches;   /* level launches of the factor sweeps */
 	uint64_t nnz_train;
+	uint32_t n_lord_batches;      /* batches swept on their level-ordered store (complete levels) */
 } vbfm_online_stats;
 
 int vbfm_online_init(vbfm_ctx *ctx, const vbfm_online_config *cfg);

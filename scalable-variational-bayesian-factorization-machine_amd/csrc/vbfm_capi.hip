@@ -500,7 +500,7 @@ void sweep_level(vbfm_ctx *c, uint32_t l, bool is_w, int f)
 	if (c->ov) {
 		// online VB: the level's columns restricted to the mini-batch (column layout, one GPU)
 		ov_level_args(c, a, is_w, f);
-		HIPCHK(vbk::ov_level(a, is_w, c->s));
+		ov_launch_level(c, a, l, is_w);
 		prof_end(c, p);
 		return;
 	}

@@ -198,6 +198,7 @@ void ov_free(vbfm_ctx *c);   // vbfm_online.hip
 void glibc_state_at(uint32_t seed, uint64_t pos, uint32_t st[31]);   // vbfm_replay.hip
 // online VB: the per-feature fields of LevelArgs for the w sweep or factor f (vbfm_online.hip)
 void ov_level_args(vbfm_ctx *c, LevelArgs &a, bool is_w, int f);
+void ov_launch_level(vbfm_ctx *c, LevelArgs &a, uint32_t l, bool is_w);
 // steps of update_all shared with the online learner (vbfm_capi.hip)
 void step_w(vbfm_ctx *c);
 void step_qcache(vbfm_ctx *c, int f);

@@ -88,6 +88,8 @@ struct LevelArgs {
 	double *rho;               // step size of each feature (new_wj / new_vj)
 	const uint32_t *ccount;    // entries of each feature in the whole train set (col_count)
 	uint32_t *tcount;          // w: t_wj (+= batch entries, rho refreshed); v of factor 0: t_vj; else nullptr
+	int hyp_uniform;           // one attribute group: the prior is hyp0 (no per-column lookup)
+	double hyp0;
 };
 
 // per-level launch description for the MCMC / ALS draws (vbfm_mcmc.hip); parameters are
@@ -236,6 +238,8 @@ hipError_t pack_pairs(const double *a, const double *b, double2 *out, uint32_t r
 hipError_t unpack_pairs(const double2 *in, double *a, double *b, uint32_t rows, size_t D, hipStream_t s);
 // online VB (vbfm_online.hip): one level of the w / v sweep on a mini-batch (column layout)
 hipError_t ov_level(const LevelArgs &a, int is_w, hipStream_t s);
+// the same on the batch's level-ordered store (a.src / a.dst / a.lnext / a.lbase)
+hipError_t ov_lord_level(const LevelArgs &a, int is_w, hipStream_t s);
 // MCMC / ALS (vbfm_mcmc.hip); mode 0: fused, 1: statistics only (into a.stats),
 // 2: draw + correction from the (all-reduced) a.stats
 hipError_t mc_v_level(const McArgs &a, int mode, hipStream_t s);

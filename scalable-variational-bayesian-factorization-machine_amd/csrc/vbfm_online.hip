@@ -102,6 +102,16 @@ __global__ __launch_bounds__(256) void k_ov_gather(const uint32_t *rows, uint32_
 	if (lane == 0) t_b[i] = target[r];
 }
 
+// first entry of every level of every batch: lvl[b * (L+1) + l] = gptr[b * nf + level_ptr[l]]
+__global__ void k_ov_level_bases(const uint64_t *gptr, const uint32_t *level_ptr, uint32_t L, uint32_t nf, uint32_t nb,
+                                 uint64_t *lvl)
+{
+	const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+	if (i >= nb * (L + 1)) return;
+	const uint32_t b = i / (L + 1), l = i % (L + 1);
+	lvl[i] = gptr[(size_t)b * nf + level_ptr[l]];
+}
+
 // ---- update_w0 (fm_learn_vb_online.h:471-497): sum of the per-row natural-mean terms
 // (1 - new_w0) * mu_old + new_w0 * _size * alpha * (e + mu_0_dash)
 template <int BLOCK>
@@ -357,6 +367,184 @@ __global__ __launch_bounds__(256) void k_ov_w_level(LevelArgs a)
 	}
 }
 
+// ---- the per-batch level-ordered store --------------------------------------------------------
+// When every level holds each row of the batch exactly once (field-structured data) the
+// batch's records are kept in the current level's order: position p of level l is the p-th
+// entry of the level's batch columns, which are contiguous in ent_sorted (level order, rows
+// ascending in a column). A level then reads each column's records as one run and writes every
+// record, corrected, to its row's position in the next level (lnx): one random line per record
+// instead of a random read and a random write of the same line (tools/probe_ovlevel.hip: 7.7 vs
+// 12.6 us per level at C3's batch shape). Column statistics, posteriors and corrections are the
+// column kernels' (same entries, same lanes, same butterfly): bit-identical; only data-set sums
+// (w0, alpha, free energy) add the rows in another order.
+//
+// level of a batch entry (by its index g in ent_sorted) and its position in that level
+DEVI uint32_t ov_level_of(const uint64_t *base, uint32_t L, uint64_t g)
+{
+	uint32_t lo = 0, hi = L;   // base[lo] <= g < base[hi]
+	while (hi - lo > 1) {
+		const uint32_t mid = (lo + hi) >> 1;
+		if (base[mid] <= g) lo = mid;
+		else hi = mid;
+	}
+	return lo;
+}
+
+// pos[l * n + row] = position of the row in level l; base[L+1] = first entry of every level
+__global__ void k_ov_lord_pos(const uint2 *ent, const uint64_t *base, uint32_t L, uint32_t n, uint32_t *pos)
+{
+	const uint64_t g = base[0] + (uint64_t)blockIdx.x * 256u + threadIdx.x;
+	if (g >= base[L]) return;
+	const uint32_t l = ov_level_of(base, L, g);
+	pos[(size_t)l * n + (ent[g].x & ROW_MASK)] = (uint32_t)(g - base[l]);
+}
+
+// lnx[g - base[0]] = the entry's row position in the next level (the last level -> level 0)
+__global__ void k_ov_lord_next(const uint2 *ent, const uint64_t *base, uint32_t L, uint32_t n, const uint32_t *pos,
+                               uint32_t *lnx)
+{
+	const uint64_t g = base[0] + (uint64_t)blockIdx.x * 256u + threadIdx.x;
+	if (g >= base[L]) return;
+	const uint32_t l = ov_level_of(base, L, g), ln = l + 1 == L ? 0 : l + 1;
+	lnx[g - base[0]] = pos[(size_t)ln * n + (ent[g].x & ROW_MASK)];
+}
+
+// One level of the w (IS_W) or v sweep of a mini-batch on the level-ordered store. A workgroup
+// serves 256/G consecutive columns, i.e. one contiguous run of the level's records: the run
+// (up to CAP records) and its next-level positions are staged in LDS with coalesced loads, four
+// lanes per record; G lanes per column reduce the statistics as k_ov_{w,v}_level do (same
+// entries per lane, same butterfly), the corrected records go back to their LDS slots, and the
+// run is written out four lanes per record to a.dst[lnext] (every record: the write is the
+// move, also when the guards skip the correction). Records past CAP (a run longer than CAP)
+// are read and written directly.
+constexpr uint32_t OV_CAP = 512;
+
+DEVI uint32_t ov_slot(uint32_t i, uint32_t c) { return i * 4 + (c ^ ((i >> 2) & 3)); }
+
+template <int G, bool IS_W, int P, bool NEXT>
+__global__ __launch_bounds__(256) void k_ov_lord(LevelArgs a)
+{
+	static_assert(G <= 64, "lane groups inside one wave");
+	__shared__ double2 stage[OV_CAP * 4];
+	__shared__ uint32_t dsts[OV_CAP];
+	const uint32_t c0 = blockIdx.x * (256 / G);
+	const uint32_t c1 = min(c0 + 256 / G, a.nfeat);
+	const uint64_t wb = a.col_ptr[c0], we = a.col_ptr[c1];
+	const uint32_t m = (uint32_t)min<uint64_t>(we - wb, OV_CAP);
+	{
+		const double2 *s2 = reinterpret_cast<const double2 *>(a.src + (wb - a.lbase));
+		const uint32_t *nx2 = a.lnext + (wb - a.lbase);
+		for (uint32_t t = threadIdx.x; t < m * 4; t += 256) stage[ov_slot(t >> 2, t & 3)] = s2[t];
+		for (uint32_t t = threadIdx.x; t < m; t += 256) dsts[t] = nx2[t];
+	}
+	const uint32_t col_i = c0 + threadIdx.x / G;
+	const uint32_t lane = threadIdx.x % G;
+	const bool live = col_i < a.nfeat;
+	const uint32_t j = live ? a.feats[col_i] : 0u;
+	const uint64_t cb = live ? a.col_ptr[col_i] : 0u;
+	const uint32_t n = live ? (uint32_t)(a.col_ptr[col_i + 1] - cb) : 0u;
+	const uint32_t o0 = (uint32_t)(cb - wb);   // the column's first record in the run
+	const uint2 *col = a.csc + cb;
+	double2 msj = make_double2(0.0, 0.0), natj = make_double2(0.0, 0.0), nx = make_double2(0.0, 0.0);
+	double rho = 0.0, hg = a.hyp0;
+	uint32_t cc = 0, tc = 0;
+	const size_t pi = (size_t)j * a.ms_stride;
+	if (n) {   // every per-column load issued here, one dependent step after the feature id
+		msj = a.ms[pi];
+		natj = a.nat[pi];
+		rho = a.rho[j];
+		cc = a.ccount[j];
+		if (!a.hyp_uniform) hg = a.hyp[(size_t)a.attr_group[j] * a.hyp_stride];
+		if (a.tcount) tc = a.tcount[j];
+		if constexpr (NEXT) nx = a.ms_next[(size_t)j * a.ms_stride_next];
+	}
+	__syncthreads();
+	auto get = [&](uint32_t i, Rec &r) {
+		const uint32_t o = o0 + i;
+		if (o < m) {
+#pragma unroll
+			for (uint32_t c = 0; c < 4; ++c) r[c] = stage[ov_slot(o, c)];
+		} else {
+			load_rec(a.src, (uint32_t)(wb - a.lbase) + o, r);
+		}
+	};
+	const double mo = msj.x, so = msj.y;
+	const double keep_m = (1 - rho) * natj.x, keep_s = (1 - rho) * natj.y;
+	const double acc = a.alpha * cc;
+	const double rca = rho * cc * a.alpha;
+	double eta1 = 0.0, eta2 = 0.0;
+	for (uint32_t i = lane; i < n; i += G) {
+		Rec r;
+		get(i, r);
+		const float x = ent_x(col[i]);
+		if constexpr (IS_W) {
+			const double w_mean = x * (E(r) + x * mo);
+			const double w_sigma_sqr = x * x;   // fp32 product
+			eta2 += keep_s + rho * (hg + acc * w_sigma_sqr);
+			eta1 += keep_m + rca * w_mean;
+		} else {
+			double vm = 0.0, vs = 0.0;
+			v_stat(x, E(r), Q<P>(r), TQ<P>(r), mo, so, vm, vs);
+			eta2 += keep_s + rho * (hg + acc * vs);
+			eta1 += keep_m + rca * vm;
+		}
+	}
+	group_sum2<G>(eta1, eta2, nullptr);
+	double mu = mo, sig = so;
+	bool go = false;
+	if (n) {
+		const double nmu = eta1 / n, nsig = eta2 / n;
+		mu = nmu / nsig;
+		sig = 1 / nsig;
+		go = true;
+		const bool leader = lane == 0;
+		const int c_sig = IS_W ? CNT_NAN_SIGMA_W : CNT_NAN_SIGMA_V, c_nan = IS_W ? CNT_NAN_MU_W : CNT_NAN_MU_V,
+		          c_inf = IS_W ? CNT_INF_MU_W : CNT_INF_MU_V;
+		if (dnan(sig) || dinf(sig)) {
+			sig = so;
+			if (leader) atomicAdd(&a.counters[c_sig], 1u);
+		}
+		if (dnan(mu)) {
+			if (leader) atomicAdd(&a.counters[c_nan], 1u);
+			mu = mo;
+			go = false;
+		} else if (dinf(mu)) {
+			if (leader) atomicAdd(&a.counters[c_inf], 1u);
+			mu = mo;
+			go = false;
+		}
+		if (leader) {
+			a.nat[pi] = make_double2(nmu, nsig);
+			a.ms[pi] = make_double2(mu, sig);
+			if constexpr (IS_W) {
+				const uint32_t t = tc + n;
+				a.tcount[j] = t;
+				a.rho[j] = pow((double)(T0 + t), -LAMDA);
+			} else {
+				if (a.tcount) a.tcount[j] = tc + n;
+			}
+		}
+	}
+	for (uint32_t i = lane; i < n; i += G) {
+		Rec r;
+		get(i, r);
+		const uint2 e = col[i];
+		if constexpr (IS_W) w_apply<NEXT>(r, ent_x(e), (e.x & a.first_mask) != 0, go, mo, so, mu, sig, nx);
+		else v_apply<P, NEXT>(r, ent_x(e), (e.x & a.first_mask) != 0, go, mo, so, mu, sig, nx);
+		const uint32_t o = o0 + i;
+		if (o < m) {
+#pragma unroll
+			for (uint32_t c = 0; c < 4; ++c) stage[ov_slot(o, c)] = r[c];
+		} else {
+			store_rec(a.dst, a.lnext[(wb - a.lbase) + o], r);
+		}
+	}
+	__syncthreads();
+	double2 *d = reinterpret_cast<double2 *>(a.dst);
+	for (uint32_t t = threadIdx.x; t < m * 4; t += 256)
+		d[(size_t)dsts[t >> 2] * 4 + (t & 3)] = stage[ov_slot(t >> 2, t & 3)];
+}
+
 inline unsigned grid_of(uint64_t n, unsigned block = 256) { return (unsigned)((n + block - 1) / block); }
 
 }  // namespace
@@ -379,6 +567,36 @@ hipError_t launch_ov(const LevelArgs &a, int is_w, hipStream_t s)
 		else k_ov_v_level<G, 1, false><<<grid, 256, 0, s>>>(a);
 	}
 	return hipGetLastError();
+}
+
+template <int G>
+hipError_t launch_ov_lord(const LevelArgs &a, int is_w, hipStream_t s)
+{
+	const unsigned grid = (a.nfeat + 256 / G - 1) / (256 / G);
+	const bool nx = a.ms_next != nullptr;
+	if (is_w) {
+		if (nx) k_ov_lord<G, true, 0, true><<<grid, 256, 0, s>>>(a);
+		else k_ov_lord<G, true, 0, false><<<grid, 256, 0, s>>>(a);
+	} else if (a.slot == 0) {
+		if (nx) k_ov_lord<G, false, 0, true><<<grid, 256, 0, s>>>(a);
+		else k_ov_lord<G, false, 0, false><<<grid, 256, 0, s>>>(a);
+	} else {
+		if (nx) k_ov_lord<G, false, 1, true><<<grid, 256, 0, s>>>(a);
+		else k_ov_lord<G, false, 1, false><<<grid, 256, 0, s>>>(a);
+	}
+	return hipGetLastError();
+}
+
+// one level on the batch's level-ordered store (a.src / a.dst / a.lnext / a.lbase set)
+hipError_t ov_lord_level(const LevelArgs &a, int is_w, hipStream_t s)
+{
+	if (a.nfeat == 0) return hipSuccess;
+	const uint32_t m = a.avg_len;
+	if (m <= 6) return launch_ov_lord<4>(a, is_w, s);
+	if (m <= 12) return launch_ov_lord<8>(a, is_w, s);
+	if (m <= 24) return launch_ov_lord<16>(a, is_w, s);
+	if (m <= 48) return launch_ov_lord<32>(a, is_w, s);
+	return launch_ov_lord<64>(a, is_w, s);
 }
 
 // lanes per column from the batch's mean column length (LevelArgs::avg_len, set by
@@ -432,6 +650,18 @@ struct OvState {
 	hipEvent_t ev[4] = {};
 	std::vector<hipEvent_t> bev;   // [num_batch * 6] phase marks of every batch
 	uint32_t launches_v = 0;
+	// the per-batch level-ordered store (k_ov_lord)
+	uint32_t *level_ptr_d = nullptr;   // [L+1] level bounds in level positions
+	uint64_t *lvl_d = nullptr;         // [num_batch * (L+1)] first entry of every level of every batch
+	std::vector<uint64_t> lvl_h;
+	std::vector<uint8_t> batch_lord;   // [num_batch] the batch's levels are complete
+	uint32_t *lpos = nullptr, *lnx = nullptr;
+	RowRec *rows_b2 = nullptr;
+	uint32_t lord_cap_rows = 0;
+	uint64_t lord_cap_nnz = 0;
+	bool lord_on = false;              // the batch being processed uses the store
+	const uint64_t *lvl_cur = nullptr; // its level bases (host)
+	RowRec *rows_other = nullptr;      // the second record buffer of the ping-pong
 };
 
 namespace vbi {
@@ -445,6 +675,7 @@ void ov_free(vbfm_ctx *c)
 	dfree(o.loc_d); dfree(o.key_in); dfree(o.key_out); dfree(o.ent_sorted); dfree(o.ent_tmp); dfree(o.cnt);
 	dfree(o.gptr); dfree(o.lvcp); dfree(o.rstart_d); dfree(o.tmp); dfree(o.rp_b); dfree(o.len_b); dfree(o.csr_b); dfree(o.t_b);
 	dfree(o.rows_b);
+	dfree(o.level_ptr_d); dfree(o.lvl_d); dfree(o.lpos); dfree(o.lnx); dfree(o.rows_b2);
 	for (hipEvent_t e : o.ev)
 		if (e) (void)hipEventDestroy(e);
 	for (hipEvent_t e : o.bev) (void)hipEventDestroy(e);
@@ -461,7 +692,26 @@ void ov_level_args(vbfm_ctx *c, LevelArgs &a, bool is_w, int f)
 	a.tcount = is_w ? o.t_wj : (f == 0 ? o.t_vj : nullptr);
 	if (!is_w) o.launches_v++;
 	a.avg_len = a.avg_len / std::max(o.num_batch, 1u);   // the batch's share of the mean column
+	a.hyp_uniform = c->G == 1;
+	a.hyp0 = c->G == 1 ? (is_w ? c->hyp_w[0] : c->hyp_v[f]) : 0.0;
 	a.col_ptr += a.feats - c->level_feats;               // the batch's col_ptr by level position
+}
+
+// one level of the batch's sweep: on the batch's level-ordered store when it is in use (the
+// records move to the next level's order), else the column kernels
+void ov_launch_level(vbfm_ctx *c, LevelArgs &a, uint32_t l, bool is_w)
+{
+	OvState &o = *c->ov;
+	if (!o.lord_on) {
+		HIPCHK(vbk::ov_level(a, is_w, c->s));
+		return;
+	}
+	a.src = c->rows;
+	a.dst = o.rows_other;
+	a.lbase = o.lvl_cur[l];
+	a.lnext = o.lnx + (o.lvl_cur[l] - o.lvl_cur[0]);
+	HIPCHK(vbk::ov_lord_level(a, is_w, c->s));
+	std::swap(c->rows, o.rows_other);
 }
 
 }  // namespace vbi
@@ -524,7 +774,52 @@ void ov_regroup(vbfm_ctx *c)
 	HIPCHK(rocprim::exclusive_scan(ov_tmp(o, tb), tb, o.cnt, o.gptr, (uint64_t)0, ncnt, rocprim::plus<uint64_t>(),
 	                               c->s));
 	HIPCHK(hipMemcpyAsync(o.gptr + ncnt, &nnz, 8, hipMemcpyHostToDevice, c->s));
+	// the level bases of every batch, for the per-batch level-ordered store
+	const uint32_t L = nlevels(c);
+	if (o.level_ptr_d && L) {
+		k_ov_level_bases<<<grid_of((uint64_t)nb * (L + 1)), 256, 0, c->s>>>(o.gptr, o.level_ptr_d, L, nf, nb, o.lvl_d);
+		HIPCHK(hipGetLastError());
+		o.lvl_h.resize((size_t)nb * (L + 1));
+		HIPCHK(hipMemcpyAsync(o.lvl_h.data(), o.lvl_d, o.lvl_h.size() * 8, hipMemcpyDeviceToHost, c->s));
+	}
 	sync(c);   // nnz (host) must outlive the copy
+	o.batch_lord.assign(nb, 0);
+	if (o.level_ptr_d && L)
+		for (uint32_t b = 0; b < nb; b++) {
+			const uint64_t n = o.rstart[b + 1] - o.rstart[b];
+			bool ok = n > 0;
+			for (uint32_t l = 0; l < L && ok; l++) ok = o.lvl_h[(size_t)b * (L + 1) + l + 1] - o.lvl_h[(size_t)b * (L + 1) + l] == n;
+			o.batch_lord[b] = ok;
+		}
+}
+
+// the per-batch store: positions of the batch's rows in every level and every entry's
+// position in the next level; the records (predicted in row order) moved to level-0 order
+void ov_lord_begin(vbfm_ctx *c, uint32_t b, uint32_t n, uint64_t nnz)
+{
+	OvState &o = *c->ov;
+	const uint32_t L = nlevels(c);
+	if (n > o.lord_cap_rows) {
+		dfree(o.lpos); dfree(o.rows_b2);
+		o.lpos = dalloc<uint32_t>((size_t)L * n);
+		o.rows_b2 = dalloc<RowRec>(n);
+		o.lord_cap_rows = n;
+	}
+	if (nnz > o.lord_cap_nnz) {
+		dfree(o.lnx);
+		o.lnx = dalloc<uint32_t>(nnz);
+		o.lord_cap_nnz = nnz;
+	}
+	const uint64_t *base = o.lvl_d + (size_t)b * (L + 1);
+	k_ov_lord_pos<<<grid_of(nnz), 256, 0, c->s>>>(o.ent_sorted, base, L, n, o.lpos);
+	HIPCHK(hipGetLastError());
+	k_ov_lord_next<<<grid_of(nnz), 256, 0, c->s>>>(o.ent_sorted, base, L, n, o.lpos, o.lnx);
+	HIPCHK(hipGetLastError());
+	HIPCHK(vbk::rows_scatter(o.rows_b2, c->rows, o.lpos, n, c->s));   // row r -> its level-0 position
+	o.rows_other = c->rows;
+	c->rows = o.rows_b2;
+	o.lvl_cur = o.lvl_h.data() + (size_t)b * (L + 1);
+	o.lord_on = true;
 }
 
 void ov_batch_capacity(vbfm_ctx *c, uint32_t n, uint64_t nnz)
@@ -690,6 +985,25 @@ int vbfm_online_init(vbfm_ctx *c, const vbfm_online_config *cfg)
 			o.ent_tmp = dalloc<uint2>(nnz); o.ent_sorted = dalloc<uint2>(nnz);
 			o.cnt = dalloc<uint32_t>((size_t)nb * nf);
 			o.gptr = dalloc<uint64_t>((size_t)nb * nf + 1);
+			// the per-batch level-ordered store: field-structured data (no row lists a feature
+			// twice); factor 0's q-cache must come from the w sweep (k1), VBFM_LAYOUT=column or
+			// vbfm_set_layout(VBFM_LAYOUT_COLUMN) keep the column kernels
+			{
+				const char *lay = getenv("VBFM_LAYOUT");
+				bool want = c->layout_req != VBFM_LAYOUT_COLUMN && !(lay && !strcmp(lay, "column")) &&
+				            (c->k1 || c->k == 0) && nlevels(c) > 0;
+				if (want && nf) {
+					std::vector<uint8_t> dup(nf);
+					HIPCHK(hipMemcpy(dup.data(), c->dup, nf, hipMemcpyDeviceToHost));
+					for (uint8_t d : dup) want = want && !d;
+				}
+				if (want) {
+					const uint32_t L = nlevels(c);
+					o.level_ptr_d = dalloc<uint32_t>((size_t)L + 1);
+					HIPCHK(hipMemcpy(o.level_ptr_d, c->level_ptr.data(), ((size_t)L + 1) * 4, hipMemcpyHostToDevice));
+					o.lvl_d = dalloc<uint64_t>((size_t)nb * (L + 1));
+				}
+			}
 			{
 				std::vector<uint64_t> cp((size_t)nf + 1), lv((size_t)nf + 1, 0);
 				std::vector<uint32_t> feats(nf);
@@ -734,6 +1048,7 @@ int vbfm_online_epoch(vbfm_ctx *c, vbfm_online_stats *out)
 		RowRec *const rows_full = c->rows;
 		const uint64_t n_global_full = c->n_global;
 		auto restore = [&] {
+			o.lord_on = false;
 			c->tr = full;
 			c->rows = rows_full;
 			c->n_global = n_global_full;
@@ -774,6 +1089,11 @@ int vbfm_online_epoch(vbfm_ctx *c, vbfm_online_stats *out)
 				const int bl = blocked_predict(c, c->tr);
 				HIPCHK(vbk::predict_et(c->tr.row_ptr, c->tr.csr, c->ms_v, c->ms_w, c->k, c->k1, c->k0, c->mu0, c->s0d,
 				                       c->tr.target, c->scratch_n, c->rows, n, bl, c->s));
+				o.lord_on = false;
+				if (o.batch_lord[b]) {
+					ov_lord_begin(c, b, n, nnz);
+					st.n_lord_batches++;
+				}
 				// update_all(train1, train.num_cases) (fm_learn_vb_online.h:354-469)
 				HIPCHK(hipEventRecord(bev[1], c->s));
 				if (c->k0) ov_step_w0(c);

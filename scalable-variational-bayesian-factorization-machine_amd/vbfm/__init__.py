@@ -125,7 +125,7 @@ class OnlineStats(C.Structure):
                 + [("num_levels", C.c_int32), ("ms_regroup", C.c_double), ("ms_batches", C.c_double),
                    ("ms_test", C.c_double), ("ms_total", C.c_double), ("ms_predict", C.c_double),
                    ("ms_w0", C.c_double), ("ms_w", C.c_double), ("ms_v", C.c_double), ("ms_hyper", C.c_double),
-                   ("n_vlevel_launches", C.c_uint32), ("nnz_train", C.c_uint64)])
+                   ("n_vlevel_launches", C.c_uint32), ("nnz_train", C.c_uint64), ("n_lord_batches", C.c_uint32)])
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}
@@ -605,7 +605,7 @@ class FMLearnVBOnline(FMLearnVB):
     def __init__(self, k0=1, k1=1, num_factor=8, num_attribute=0, attr_group=None,
                  min_target=1.0, max_target=5.0, device=0):
         super().__init__(k0, k1, num_factor, num_attribute, attr_group, min_target, max_target, device,
-                         layout="column")
+                         layout="auto")
 
     def init(self, seed, init_stdev=0.1, num_batch=50, replay=False):
         """srand(seed); the VB learner's initial draws; fm_learn_vb_online::init (needs set_data first)."""
