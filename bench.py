@@ -230,7 +230,7 @@ def main():
     sweep_ms = sum(s.ms_v for s in stats) / len(stats)
     traffic = None
     if online:
-        kernel = "k_ov_v_level"
+        kernel = "k_ov_lord" if stats[-1].n_lord_batches else "k_ov_v_level"
     elif mc:
         kernel = "k_mc_level_lord" if layout == "level" else "k_mc_v_level"
     else:
@@ -255,7 +255,8 @@ def main():
                             "update_all; test RMSE)" % args.batch) if online else
                            "one full VB iteration (update_all + test RMSE)",
                    "parallelism": ("feature-sharded fs%d" if fshard else "row-sharded dp%d") % world,
-                   "row_layout": layout},
+                   "row_layout": ("level (per mini-batch)" if stats[-1].n_lord_batches else "column") if online
+                   else layout},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                      "kernel": kernel, "avg_launch_ms": avg_ms,
