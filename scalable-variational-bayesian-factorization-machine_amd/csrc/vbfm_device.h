@@ -127,6 +127,11 @@ struct McArgs {
 	const RowRec *src;
 	RowRec *dst;
 	int first_level;
+	// deferred correction (row-sharded split, as LevelArgs): the previous level's draws
+	const uint32_t *lpidx;
+	const float *lpx;
+	PostT *tab;                // {mo = old value, mu = drawn value or NaN (no correction)}
+	int pending;               // bit 0: apply the previous level's correction; bit 1: nt loads
 };
 
 // kernels launched from the C-ABI layer (vbfm_kernels.hip)
@@ -249,6 +254,11 @@ hipError_t mc_qcache(const uint64_t *row_ptr, const uint2 *csr, const double2 *p
                      uint32_t n, int slot, const uint32_t *pos, hipStream_t s);
 // MCMC / ALS level on the level-ordered store; mode as mc_v_level (2 = draw + move)
 hipError_t mc_lord_level(const McArgs &a, int mode, int is_w, hipStream_t s);
+// MCMC / ALS deferred split on the level-ordered store: level l-1's correction, level l's
+// statistics and the move in one pass; the draws after the all-reduce; the sweep's last correction
+hipError_t mc_lord_defer_level(const McArgs &a, int is_w, hipStream_t s);
+hipError_t mc_lord_defer_post(const McArgs &a, int is_w, hipStream_t s);
+hipError_t mc_lord_defer_flush(const McArgs &a, int is_w, uint32_t n, hipStream_t s);
 // per-block sums over rows; mode 0: e*e ; mode 1: e - w0
 hipError_t mc_row_sums(const RowRec *rows, uint32_t n, int mode, double w0, double *out, uint32_t nblocks,
                        hipStream_t s);

@@ -537,6 +537,137 @@ void launch_flush(const LevelArgs &a, uint32_t n, hipStream_t s)
 	k_lord_defer_flush<IS_W, P, NEXT><<<(n + 255) / 256, 256, 0, s>>>(a, n);
 }
 
+// ---- MCMC / ALS deferred split (row shards) ------------------------------------------------
+// As k_lord_defer for VB: level l's kernel applies level l-1's correction (fm_learn_mcmc.h
+// draw_v :826-834 / draw_w :712-717) from the table the previous post kernel wrote after its
+// all-reduce, adds level l's term of the next q-cache, reduces level l's statistics from the
+// corrected records and moves them; k_mc_lord_defer_post draws the level's parameters from the
+// all-reduced statistics (mc_draw, the same random input per attribute as the fused kernel).
+// The same arithmetic per row as the fused kernel: bit-identical results.
+template <bool IS_W, int P>
+DEVI void mc_apply_pending(Rec &r, const PostT &t, float x)
+{
+	if (__builtin_isnan(t.mu)) return;   // the draw was refused: no correction
+	McOp<IS_W, P, false> op;
+	op.vo = t.mo; op.v = t.mu; op.vn = 0.0; op.go = true;
+	op.apply(r, x, false);
+}
+
+template <bool IS_W, int P>
+DEVI void mc_add_next_q(Rec &r, float x, bool first, double vn)
+{
+	const double aq = vn * x;
+	double &q = IS_W ? Q<0>(r) : Q<1 - P>(r);
+	q = first ? 0.0 + aq : q + aq;
+}
+
+template <int BLOCK, int R, bool IS_W, int P, bool NEXT>
+__global__ __launch_bounds__(BLOCK) void k_mc_lord_defer(McArgs a)
+{
+	constexpr uint32_t CAP = BLOCK * R;
+	__shared__ double2 recs[CAP * 4];
+	__shared__ uint32_t dsts[CAP];
+	__shared__ double lds[2 * (BLOCK / 64)];
+	const uint32_t j = a.feats[blockIdx.x];
+	const uint64_t sb = a.lcp[blockIdx.x];
+	const uint32_t n = (uint32_t)(a.lcp[blockIdx.x + 1] - sb);
+	const double2 *s = reinterpret_cast<const double2 *>(a.src + (sb - a.lbase));
+	double2 *d = reinterpret_cast<double2 *>(a.dst);
+	const float *lx = a.lx + sb;
+	const uint32_t *nxt = a.lnext + sb;
+	const uint32_t *pidx = a.lpidx + sb;
+	const float *px = a.lpx + sb;
+	McOp<IS_W, P, false> op;
+	op.vo = a.par[(size_t)j * a.stride].x;
+	const double vn = NEXT ? a.par_next[(size_t)j * a.next_stride].x : 0.0;
+	const bool first = a.first_level != 0;
+	const bool pending = (a.pending & 1) != 0, nt = (a.pending & 2) != 0;
+	double sm = 0.0, ss = 0.0;
+	for (uint32_t base = 0; base < n; base += CAP) {
+		const uint32_t m = min(CAP, n - base);
+		if (base) __syncthreads();
+		PostT t[R];
+		float pxv[R];
+		if (pending) {
+#pragma unroll
+			for (int u = 0; u < R; ++u) {
+				const uint32_t i = threadIdx.x + u * BLOCK;
+				if (i < m) { t[u] = a.tab[pidx[base + i]]; pxv[u] = px[base + i]; }
+			}
+		}
+		if (nt) stage_in_nt<BLOCK>(recs, s + (size_t)base * 4, m);
+		else stage_in<BLOCK>(recs, s + (size_t)base * 4, m);
+		__syncthreads();
+#pragma unroll
+		for (int u = 0; u < R; ++u) {
+			const uint32_t i = threadIdx.x + u * BLOCK;
+			if (i >= m) continue;
+			Rec v;
+			lds_get(recs, i, v);
+			const float x = lx[base + i];
+			if (pending) mc_apply_pending<IS_W, P>(v, t[u], pxv[u]);
+			if constexpr (NEXT) mc_add_next_q<IS_W, P>(v, x, first, vn);
+			if (pending || NEXT) lds_put(recs, i, v);
+			op.stat(v, x, sm, ss);
+			dsts[i] = nxt[base + i];
+		}
+		__syncthreads();
+		for (uint32_t tt = threadIdx.x; tt < m * 4; tt += BLOCK) {
+			const uint32_t i = tt >> 2, c = tt & 3;
+			d[(size_t)dsts[i] * 4 + c] = recs[lslot(i, c)];
+		}
+	}
+	block_sum2<BLOCK>(sm, ss, lds);
+	if (threadIdx.x == 0) a.stats[blockIdx.x] = make_double2(sm, ss);
+}
+
+template <bool IS_W>
+__global__ __launch_bounds__(256) void k_mc_lord_defer_post(McArgs a)
+{
+	const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+	if (i >= a.nfeat) return;
+	const uint32_t j = a.feats[i];
+	const double vo = a.par[(size_t)j * a.stride].x;
+	const double2 st = a.stats[i];
+	const uint32_t g = a.attr_group[j];
+	double v = vo;
+	const bool go = mc_draw(st.x, st.y, vo, a.lambda[(size_t)g * a.hstride], a.mu[(size_t)g * a.hstride], a.alpha,
+	                        mc_z(a, j), a.z != nullptr, a.sample, !IS_W, v, a.counters, true);
+	a.par[(size_t)j * a.stride].x = v;
+	PostT t;
+	t.mo = vo; t.so = 0.0; t.sig = 0.0;
+	t.mu = go ? v : __builtin_nan("");
+	a.tab[i] = t;
+}
+
+template <bool IS_W, int P>
+__global__ __launch_bounds__(256) void k_mc_lord_defer_flush(McArgs a, uint32_t n)
+{
+	__shared__ double2 recs[256 * 4];
+	const uint32_t b = blockIdx.x * 256u;
+	const uint32_t m = min(256u, n - b);
+	double2 *r = reinterpret_cast<double2 *>(a.dst) + (size_t)b * 4;
+	stage_in_nt<256>(recs, r, m);
+	__syncthreads();
+	if (threadIdx.x < m) {
+		Rec v;
+		lds_get(recs, threadIdx.x, v);
+		mc_apply_pending<IS_W, P>(v, a.tab[a.lpidx[b + threadIdx.x]], a.lpx[b + threadIdx.x]);
+		lds_put(recs, threadIdx.x, v);
+	}
+	__syncthreads();
+	for (uint32_t t = threadIdx.x; t < m * 4; t += 256) r[t] = recs[lslot(t >> 2, t & 3)];
+}
+
+template <bool IS_W, int P, bool NEXT>
+void launch_mc_defer(const McArgs &a, hipStream_t s)
+{
+	if (a.avg_len <= 96) k_mc_lord_defer<64, 2, IS_W, P, NEXT><<<a.nfeat, 64, 0, s>>>(a);
+	else if (a.avg_len <= 320) k_mc_lord_defer<256, 1, IS_W, P, NEXT><<<a.nfeat, 256, 0, s>>>(a);
+	else if (a.avg_len <= 640) k_mc_lord_defer<256, 2, IS_W, P, NEXT><<<a.nfeat, 256, 0, s>>>(a);
+	else k_mc_lord_defer<512, 2, IS_W, P, NEXT><<<a.nfeat, 512, 0, s>>>(a);
+}
+
 template <int BLOCK, int R, int MODE>
 void launch_mc_lord(const McArgs &a, int is_w, hipStream_t s)
 {
@@ -574,6 +705,35 @@ hipError_t mc_lord_level(const McArgs &a, int mode, int is_w, hipStream_t s)
 	if (mode == 0) launch_mc_lord_shape<0>(a, is_w, s);
 	else if (mode == 1) launch_mc_lord_shape<1>(a, is_w, s);
 	else launch_mc_lord_shape<2>(a, is_w, s);
+	return hipGetLastError();
+}
+
+hipError_t mc_lord_defer_level(const McArgs &a, int is_w, hipStream_t s)
+{
+	if (a.nfeat == 0) return hipSuccess;
+	const bool nx = a.par_next != nullptr;
+	if (is_w) nx ? launch_mc_defer<true, 0, true>(a, s) : launch_mc_defer<true, 0, false>(a, s);
+	else if (a.slot == 0) nx ? launch_mc_defer<false, 0, true>(a, s) : launch_mc_defer<false, 0, false>(a, s);
+	else nx ? launch_mc_defer<false, 1, true>(a, s) : launch_mc_defer<false, 1, false>(a, s);
+	return hipGetLastError();
+}
+
+hipError_t mc_lord_defer_post(const McArgs &a, int is_w, hipStream_t s)
+{
+	if (a.nfeat == 0) return hipSuccess;
+	const unsigned g = (a.nfeat + 255) / 256;
+	if (is_w) k_mc_lord_defer_post<true><<<g, 256, 0, s>>>(a);
+	else k_mc_lord_defer_post<false><<<g, 256, 0, s>>>(a);
+	return hipGetLastError();
+}
+
+hipError_t mc_lord_defer_flush(const McArgs &a, int is_w, uint32_t n, hipStream_t s)
+{
+	if (n == 0) return hipSuccess;
+	const unsigned g = (n + 255) / 256;
+	if (is_w) k_mc_lord_defer_flush<true, 0><<<g, 256, 0, s>>>(a, n);
+	else if (a.slot == 0) k_mc_lord_defer_flush<false, 0><<<g, 256, 0, s>>>(a, n);
+	else k_mc_lord_defer_flush<false, 1><<<g, 256, 0, s>>>(a, n);
 	return hipGetLastError();
 }
 

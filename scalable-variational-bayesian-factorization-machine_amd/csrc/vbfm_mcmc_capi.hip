@@ -309,6 +309,21 @@ void mc_sweep(vbfm_ctx *c, bool is_w, int f)
 			a.first_level = l == 0;
 			if (!c->row_comm() && !c->force_split) {
 				HIPCHK(vbk::mc_lord_level(a, 0, is_w, c->s));
+			} else if (c->lpidx) {
+				// deferred: level l-1's correction, level l's statistics and the move in one pass;
+				// the draws after the all-reduce, applied by level l+1 (or the flush)
+				a.lpidx = c->lpidx;
+				a.lpx = c->lpx;
+				a.tab = c->post_tab;
+				a.pending = l > 0 ? 3 : 0;
+				HIPCHK(vbk::mc_lord_defer_level(a, is_w, c->s));
+				if (c->row_comm())
+					NCCLCHK(ncclAllReduce(c->stats, c->stats, 2 * (size_t)a.nfeat, ncclDouble, ncclSum, c->comm, c->s));
+				HIPCHK(vbk::mc_lord_defer_post(a, is_w, c->s));
+				if (l + 1 == nlevels(c)) {   // the sweep's last correction, on level-0-ordered records
+					a.dst = c->rows_alt;      // (swapped below)
+					HIPCHK(vbk::mc_lord_defer_flush(a, is_w, c->tr.n, c->s));
+				}
 			} else {
 				HIPCHK(vbk::mc_lord_level(a, 1, is_w, c->s));
 				if (c->row_comm())
