@@ -335,6 +335,40 @@ def test_wave_prediction_many_factors(k, monkeypatch):
     np.testing.assert_allclose(g.test_e(), oc.arr(o.s.e_test, o.s.n_test), rtol=1e-12, atol=1e-12)
 
 
+def test_million_rows_two_iterations_vs_oracle():
+    """Parity at scale: 1e6 rows x 40 one-hot fields of 25,000 ids (C3's field shape, real-valued
+    x), k = 4, on the level-ordered store with the wave-form predictions, two full iterations
+    against the oracle (the reference restated, bit-exact on every fixture): test RMSE, MAE,
+    free energy, alpha and the final parameters within REL."""
+    n, F, S, k, seed = 1_000_000, 40, 25_000, 4, 5
+    n_test = 20_000
+    D = F * S + 1
+    rp, f, v, y = synth.generate(n, F, S, seed, 1)
+    rpt, ft, vt, yt = synth.generate(n_test, F, S, seed + 1, 1)
+    fml = vbfm.FMLearnVB(1, 1, k, D, min_target=float(y.min()), max_target=float(y.max()))
+    fml.init(3, 0.1)
+    fml.synth(0, n, F, S, seed, 1)
+    fml.synth(1, n_test, F, S, seed + 1, 1)
+    fml.init_caches()
+    assert fml.layout() == "level"
+    o = oc.VB(1, 1, k, D)
+    o.init_params(3, 0.1)
+    o.attach(oc.Data(csr=(n, rp, f, v, y)), oc.Data(csr=(n_test, rpt, ft, vt, yt)))
+    o.init_caches()
+    for it in range(2):
+        st = fml.iterate()
+        rmse, mae, quirk = o.iterate()
+        assert st.num_levels == F
+        close(st.rmse, rmse)
+        close(st.mae, mae)
+        close(st.train_quirk, quirk)
+        close(st.free_energy, o.s.last_free_energy)
+        close(st.alpha, o.s.alpha)
+    p, op = fml.get_params(), o.params()
+    for key in ("mu_w", "sigma_w", "mu_v", "sigma_v"):
+        close(p[key], op[key])
+
+
 @pytest.mark.parametrize("k,dim", [(8, (1, 1)), (70, (1, 1)), (130, (0, 1)), (20, (1, 0))])
 def test_fused_train_prediction_equals_test_prediction(k, dim, monkeypatch):
     """init_caches predicts e and T of the train rows in one pass (k_predict_et_wave); the
