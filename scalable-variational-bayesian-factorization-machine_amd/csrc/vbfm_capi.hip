@@ -106,7 +106,7 @@ void lord_release(vbfm_ctx *c, bool keep_rows)
 	}
 	sync(c);
 	dfree(c->rows_alt); dfree(c->lcp); dfree(c->lx); dfree(c->lnext); dfree(c->lrow0); dfree(c->lpos0);
-	dfree(c->lpidx); dfree(c->lpx); dfree(c->post_tab);
+	dfree(c->lpidx); dfree(c->lpx); dfree(c->post_tab); dfree(c->lpay);
 	c->lord = false;
 	c->rows_lorder = false;
 }
@@ -195,6 +195,13 @@ void build_lorder(vbfm_ctx *c, const std::vector<uint64_t> &cp, const std::vecto
 		c->post_tab = dalloc<PostT>(maxlev);
 		sync(c);
 		dfree(tmpx);
+		// one 16-B record per entry for the deferred kernels; the separate arrays are not
+		// read in this mode any more
+		dfree(tmp);
+		c->lpay = dalloc<uint4>(d.nnz);
+		HIPCHK(vbk::lord_pack(c->lx, c->lnext, c->lpidx, c->lpx, c->lpay, d.nnz, c->s));
+		sync(c);
+		dfree(c->lx); dfree(c->lnext); dfree(c->lpidx); dfree(c->lpx);
 	}
 	sync(c);
 	dfree(tmp);
@@ -515,11 +522,10 @@ void sweep_level(vbfm_ctx *c, uint32_t l, bool is_w, int f)
 		a.first_level = l == 0;
 		if (!c->row_comm() && !c->force_split) {
 			HIPCHK(vbk::lord_level(a, is_w, c->s));
-		} else if (c->lpidx) {
+		} else if (c->lpay) {
 			// deferred: level l-1's correction, level l's statistics and the move in one pass;
 			// level l's correction after the all-reduce, by level l+1 (or the flush)
-			a.lpidx = c->lpidx;
-			a.lpx = c->lpx;
+			a.lpay = c->lpay;
 			a.tab = c->post_tab;
 			{
 				// non-temporal record loads (default; VBFM_DEFER_NT=0: plain loads, 1.5 % slower at C4)

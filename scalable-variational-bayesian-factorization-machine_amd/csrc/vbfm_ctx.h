@@ -141,6 +141,8 @@ struct vbfm_ctx {
 	uint32_t *lpos0 = nullptr;     // [n] level-0 position of each row
 	uint32_t *lpidx = nullptr;     // [nnz] split form: the row's previous-level feature (index in its level)
 	float *lpx = nullptr;          // [nnz] ... and its x (deferred correction)
+	uint4 *lpay = nullptr;         // [nnz] deferred split: {x, lnext, lpidx, lpx} of every entry in one
+	                               // 16-B load (lx / lnext / lpidx / lpx are freed once packed)
 	PostT *post_tab = nullptr;     // [max level width] posteriors of the last level swept
 	// feature-sharded mode (vbfm_set_shard_mode): shards own column chunks of every level
 	int shard_mode = VBFM_SHARD_ROWS;

@@ -81,6 +81,7 @@ struct LevelArgs {
 	const uint32_t *lpidx;     // the entry's row: index of its previous-level feature in that level
 	const float *lpx;          // ... and that entry's x
 	PostT *tab;                // posteriors of the previous level (read) / of this level (written)
+	const uint4 *lpay;         // {x bits, lnext, lpidx, lpx bits} per level-ordered entry (deferred split)
 	int pending;               // bit 0: apply the previous level's correction first; bit 1: non-temporal record loads
 	int first_prev;            // the previous level is level 0 (q-cache restart of its entries)
 	// online VB (vbfm_online.hip): natural-gradient steps on a mini-batch; nat == nullptr: VB
@@ -131,6 +132,7 @@ struct McArgs {
 	const uint32_t *lpidx;
 	const float *lpx;
 	PostT *tab;                // {mo = old value, mu = drawn value or NaN (no correction)}
+	const uint4 *lpay;         // as LevelArgs::lpay
 	int pending;               // bit 0: apply the previous level's correction; bit 1: nt loads
 };
 
@@ -166,6 +168,9 @@ hipError_t lord_fill(const uint32_t *feats, uint32_t nfeat, const uint64_t *lcp,
                      hipStream_t s);
 // dst[p] = src[idx[p]] / dst[idx[p]] = src[p]
 hipError_t rows_gather(RowRec *dst, const RowRec *src, const uint32_t *idx, uint32_t n, hipStream_t s);
+// lpay[p] = {lx[p], lnext[p], lpidx[p], lpx[p]}
+hipError_t lord_pack(const float *lx, const uint32_t *lnext, const uint32_t *lpidx, const float *lpx, uint4 *lpay,
+                     uint64_t nnz, hipStream_t s);
 hipError_t rows_scatter(RowRec *dst, const RowRec *src, const uint32_t *idx, uint32_t n, hipStream_t s);
 hipError_t mark_first(const uint64_t *row_ptr, const uint2 *csr, const uint64_t *col_ptr, uint2 *csc,
                       uint32_t n, hipStream_t s);

@@ -296,6 +296,13 @@ __global__ __launch_bounds__(BLOCK) void k_mc_level_lord(McArgs a)
 }
 
 // ---- build -------------------------------------------------------------------------------
+__global__ void k_lord_pack(const float *lx, const uint32_t *lnext, const uint32_t *lpidx, const float *lpx, uint4 *lpay,
+                            uint64_t nnz)
+{
+	const uint64_t p = (uint64_t)blockIdx.x * 256u + threadIdx.x;
+	if (p < nnz) lpay[p] = make_uint4(__float_as_uint(lx[p]), lnext[p], lpidx[p], __float_as_uint(lpx[p]));
+}
+
 // pos[row] = level-relative position of the row's entry in this level
 __global__ __launch_bounds__(256) void k_lord_pos(const uint32_t *feats, const uint64_t *lcp, uint64_t lbase,
                                                   const uint64_t *col_ptr, const uint2 *csc, uint32_t *pos)
@@ -404,10 +411,7 @@ __global__ __launch_bounds__(BLOCK) void k_lord_defer(LevelArgs a)
 	const RowRec *src = a.src + (sb - a.lbase);
 	const double2 *s = reinterpret_cast<const double2 *>(src);
 	double2 *d = reinterpret_cast<double2 *>(a.dst);
-	const float *lx = a.lx + sb;
-	const uint32_t *nxt = a.lnext + sb;
-	const uint32_t *pidx = a.lpidx + sb;
-	const float *px = a.lpx + sb;
+	const uint4 *pay = a.lpay + sb;
 	const double2 msj = a.ms[(size_t)j * a.ms_stride];
 	VbOp<IS_W, P, NEXT> op;
 	op.mo = msj.x; op.so = msj.y;
@@ -418,15 +422,17 @@ __global__ __launch_bounds__(BLOCK) void k_lord_defer(LevelArgs a)
 	for (uint32_t base = 0; base < n; base += CAP) {
 		const uint32_t m = min(CAP, n - base);
 		if (base) __syncthreads();
-		// the posteriors of the records' previous-level features are gathered (L2 / MALL:
-		// one line each) while the run streams into LDS
+		// each entry's {x, next position, previous-level feature, its x} in one 16-B load; the
+		// posteriors of the records' previous-level features are gathered (L2 / MALL: one line
+		// each) while the run streams into LDS
 		PostT t[R];
-		float pxv[R];
-		if (pending) {
+		uint4 q[R];
 #pragma unroll
-			for (int u = 0; u < R; ++u) {
-				const uint32_t i = threadIdx.x + u * BLOCK;
-				if (i < m) { t[u] = a.tab[pidx[base + i]]; pxv[u] = px[base + i]; }
+		for (int u = 0; u < R; ++u) {
+			const uint32_t i = threadIdx.x + u * BLOCK;
+			if (i < m) {
+				q[u] = pay[base + i];
+				if (pending) t[u] = a.tab[q[u].z];
 			}
 		}
 		if (nt) stage_in_nt<BLOCK>(recs, s + (size_t)base * 4, m);
@@ -438,12 +444,12 @@ __global__ __launch_bounds__(BLOCK) void k_lord_defer(LevelArgs a)
 			if (i >= m) continue;
 			Rec v;
 			lds_get(recs, i, v);
-			const float x = lx[base + i];
-			if (pending) apply_pending<IS_W, P>(v, t[u], pxv[u]);
+			const float x = __uint_as_float(q[u].x);
+			if (pending) apply_pending<IS_W, P>(v, t[u], __uint_as_float(q[u].w));
 			if constexpr (NEXT) add_next_q<IS_W, P>(v, x, first, nx);
 			if (pending || NEXT) lds_put(recs, i, v);
 			op.stat(v, x, s1, s2);
-			dsts[i] = nxt[base + i];
+			dsts[i] = q[u].y;
 		}
 		__syncthreads();
 		for (uint32_t t = threadIdx.x; t < m * 4; t += BLOCK) {
@@ -488,7 +494,8 @@ __global__ __launch_bounds__(256) void k_lord_defer_flush(LevelArgs a, uint32_t 
 	if (threadIdx.x < m) {
 		Rec v;
 		lds_get(recs, threadIdx.x, v);
-		apply_pending<IS_W, P>(v, a.tab[a.lpidx[b + threadIdx.x]], a.lpx[b + threadIdx.x]);
+		const uint4 q = a.lpay[b + threadIdx.x];
+		apply_pending<IS_W, P>(v, a.tab[q.z], __uint_as_float(q.w));
 		lds_put(recs, threadIdx.x, v);
 	}
 	__syncthreads();
@@ -573,10 +580,7 @@ __global__ __launch_bounds__(BLOCK) void k_mc_lord_defer(McArgs a)
 	const uint32_t n = (uint32_t)(a.lcp[blockIdx.x + 1] - sb);
 	const double2 *s = reinterpret_cast<const double2 *>(a.src + (sb - a.lbase));
 	double2 *d = reinterpret_cast<double2 *>(a.dst);
-	const float *lx = a.lx + sb;
-	const uint32_t *nxt = a.lnext + sb;
-	const uint32_t *pidx = a.lpidx + sb;
-	const float *px = a.lpx + sb;
+	const uint4 *pay = a.lpay + sb;
 	McOp<IS_W, P, false> op;
 	op.vo = a.par[(size_t)j * a.stride].x;
 	const double vn = NEXT ? a.par_next[(size_t)j * a.next_stride].x : 0.0;
@@ -587,12 +591,13 @@ __global__ __launch_bounds__(BLOCK) void k_mc_lord_defer(McArgs a)
 		const uint32_t m = min(CAP, n - base);
 		if (base) __syncthreads();
 		PostT t[R];
-		float pxv[R];
-		if (pending) {
+		uint4 q[R];
 #pragma unroll
-			for (int u = 0; u < R; ++u) {
-				const uint32_t i = threadIdx.x + u * BLOCK;
-				if (i < m) { t[u] = a.tab[pidx[base + i]]; pxv[u] = px[base + i]; }
+		for (int u = 0; u < R; ++u) {
+			const uint32_t i = threadIdx.x + u * BLOCK;
+			if (i < m) {
+				q[u] = pay[base + i];
+				if (pending) t[u] = a.tab[q[u].z];
 			}
 		}
 		if (nt) stage_in_nt<BLOCK>(recs, s + (size_t)base * 4, m);
@@ -604,12 +609,12 @@ __global__ __launch_bounds__(BLOCK) void k_mc_lord_defer(McArgs a)
 			if (i >= m) continue;
 			Rec v;
 			lds_get(recs, i, v);
-			const float x = lx[base + i];
-			if (pending) mc_apply_pending<IS_W, P>(v, t[u], pxv[u]);
+			const float x = __uint_as_float(q[u].x);
+			if (pending) mc_apply_pending<IS_W, P>(v, t[u], __uint_as_float(q[u].w));
 			if constexpr (NEXT) mc_add_next_q<IS_W, P>(v, x, first, vn);
 			if (pending || NEXT) lds_put(recs, i, v);
 			op.stat(v, x, sm, ss);
-			dsts[i] = nxt[base + i];
+			dsts[i] = q[u].y;
 		}
 		__syncthreads();
 		for (uint32_t tt = threadIdx.x; tt < m * 4; tt += BLOCK) {
@@ -652,7 +657,8 @@ __global__ __launch_bounds__(256) void k_mc_lord_defer_flush(McArgs a, uint32_t 
 	if (threadIdx.x < m) {
 		Rec v;
 		lds_get(recs, threadIdx.x, v);
-		mc_apply_pending<IS_W, P>(v, a.tab[a.lpidx[b + threadIdx.x]], a.lpx[b + threadIdx.x]);
+		const uint4 q = a.lpay[b + threadIdx.x];
+		mc_apply_pending<IS_W, P>(v, a.tab[q.z], __uint_as_float(q.w));
 		lds_put(recs, threadIdx.x, v);
 	}
 	__syncthreads();
@@ -825,6 +831,14 @@ hipError_t lord_fill(const uint32_t *feats, uint32_t nfeat, const uint64_t *lcp,
 {
 	if (nfeat == 0) return hipSuccess;
 	k_lord_fill<<<nfeat, 256, 0, s>>>(feats, lcp, lbase, col_ptr, csc, pos_next, lx, lnext, row0);
+	return hipGetLastError();
+}
+
+hipError_t lord_pack(const float *lx, const uint32_t *lnext, const uint32_t *lpidx, const float *lpx, uint4 *lpay,
+                     uint64_t nnz, hipStream_t s)
+{
+	if (nnz == 0) return hipSuccess;
+	k_lord_pack<<<(unsigned)((nnz + 255) / 256), 256, 0, s>>>(lx, lnext, lpidx, lpx, lpay, nnz);
 	return hipGetLastError();
 }
 

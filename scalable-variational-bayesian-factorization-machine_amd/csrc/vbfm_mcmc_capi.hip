@@ -309,11 +309,10 @@ void mc_sweep(vbfm_ctx *c, bool is_w, int f)
 			a.first_level = l == 0;
 			if (!c->row_comm() && !c->force_split) {
 				HIPCHK(vbk::mc_lord_level(a, 0, is_w, c->s));
-			} else if (c->lpidx) {
+			} else if (c->lpay) {
 				// deferred: level l-1's correction, level l's statistics and the move in one pass;
 				// the draws after the all-reduce, applied by level l+1 (or the flush)
-				a.lpidx = c->lpidx;
-				a.lpx = c->lpx;
+				a.lpay = c->lpay;
 				a.tab = c->post_tab;
 				a.pending = l > 0 ? 3 : 0;
 				HIPCHK(vbk::mc_lord_defer_level(a, is_w, c->s));
