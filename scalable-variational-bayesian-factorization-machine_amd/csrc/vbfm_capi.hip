@@ -527,20 +527,33 @@ void sweep_level(vbfm_ctx *c, uint32_t l, bool is_w, int f)
 			// level l's correction after the all-reduce, by level l+1 (or the flush)
 			a.lpay = c->lpay;
 			a.tab = c->post_tab;
+			// level 0 of a v sweep may carry the previous sweep's last correction (vbfm_iterate)
+			const bool carried = l == 0 && c->carry != 0 && !is_w;
+			a.pend_kind = carried ? (c->carry == 3 ? 2 : 1) : 0;
+			c->carry = 0;
 			{
 				// non-temporal record loads (default; VBFM_DEFER_NT=0: plain loads, 1.5 % slower at C4)
 				static const int defer_nt = [] { const char *e = getenv("VBFM_DEFER_NT"); return !(e && e[0] == '0'); }();
-				a.pending = (l > 0 ? 1 : 0) | (l > 0 && defer_nt ? 2 : 0);
+				const bool pend = l > 0 || carried;
+				a.pending = (pend ? 1 : 0) | (pend && defer_nt ? 2 : 0);
 			}
 			a.first_prev = l == 1;
 			HIPCHK(vbk::lord_defer_level(a, is_w, c->s));
 			if (c->row_comm())
 				NCCLCHK(ncclAllReduce(c->stats, c->stats, 2 * (size_t)a.nfeat, ncclDouble, ncclSum, c->comm, c->s));
 			HIPCHK(vbk::lord_defer_post(a, is_w, c->s));
-			if (l + 1 == nlevels(c)) {   // the sweep's last correction, on level-0-ordered records
-				a.dst = c->rows_alt;      // (swapped below)
-				a.first_prev = l == 0;
-				HIPCHK(vbk::lord_defer_flush(a, is_w, c->tr.n, c->s));
+			if (l + 1 == nlevels(c)) {
+				// the sweep's last correction: left to level 0 of the next sweep when one follows
+				// inside update_all (the w sweep -> factor 0, factor f -> f+1), else applied in
+				// place on the level-0-ordered records
+				const bool carry_out = c->carry_ok && (is_w ? c->k > 0 : f + 1 < c->k);
+				if (carry_out) {
+					c->carry = is_w ? 3 : 1 + (f & 1);
+				} else {
+					a.dst = c->rows_alt;      // (swapped below)
+					a.first_prev = l == 0;
+					HIPCHK(vbk::lord_defer_flush(a, is_w, c->tr.n, c->s));
+				}
 			}
 		} else {
 			HIPCHK(vbk::lord_level_stats(a, is_w, c->s));
@@ -1154,16 +1167,27 @@ int vbfm_iterate(vbfm_ctx *c, vbfm_iter_stats *o)
 		// update_all (fm_learn_vb.h:383-501)
 		if (c->k0) { Range r("update_w0"); step_w0(c); }
 		HIPCHK(hipEventRecord(c->ev[EV_W0], c->s));
-		if (c->k1) { Range r("update_w sweep"); step_w(c); }
-		HIPCHK(hipEventRecord(c->ev[EV_W], c->s));
-		if (c->D > 0)
-			for (int f = 0; f < c->k; f++) {
-				char nm[32];
-				snprintf(nm, sizeof(nm), "factor %d", f);
-				Range r(nm);
-				step_qcache(c, f);
-				step_v(c, f);
-			}
+		// the sweeps follow each other directly: a deferred split may carry a sweep's last
+		// correction into the next sweep's first level (sweep_level); the last sweep flushes
+		c->carry = 0;
+		c->carry_ok = c->lpay && c->D > 0 && c->k > 0;
+		try {
+			if (c->k1) { Range r("update_w sweep"); step_w(c); }
+			HIPCHK(hipEventRecord(c->ev[EV_W], c->s));
+			if (c->D > 0)
+				for (int f = 0; f < c->k; f++) {
+					char nm[32];
+					snprintf(nm, sizeof(nm), "factor %d", f);
+					Range r(nm);
+					step_qcache(c, f);
+					step_v(c, f);
+				}
+		} catch (...) {
+			c->carry_ok = c->carry = 0;
+			throw;
+		}
+		c->carry_ok = 0;
+		if (c->carry) throw std::string("internal: a deferred correction was left pending");
 		HIPCHK(hipEventRecord(c->ev[EV_V], c->s));
 		double energy = 0.0;
 		bool early;

@@ -144,6 +144,10 @@ struct vbfm_ctx {
 	uint4 *lpay = nullptr;         // [nnz] deferred split: {x, lnext, lpidx, lpx} of every entry in one
 	                               // 16-B load (lx / lnext / lpidx / lpx are freed once packed)
 	PostT *post_tab = nullptr;     // [max level width] posteriors of the last level swept
+	// deferred split across sweeps (vbfm_iterate only): the last level's correction of a sweep is
+	// left to level 0 of the next one instead of a flush pass. carry: 0 none, 1 / 2 = v sweep of
+	// q-cache slot 0 / 1, 3 = w sweep
+	int carry_ok = 0, carry = 0;
 	// feature-sharded mode (vbfm_set_shard_mode): shards own column chunks of every level
 	int shard_mode = VBFM_SHARD_ROWS;
 	int fs_req = 1;                // shards requested (no communicator: run one after another here)

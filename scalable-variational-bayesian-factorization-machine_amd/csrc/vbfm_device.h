@@ -84,6 +84,8 @@ struct LevelArgs {
 	const uint4 *lpay;         // {x bits, lnext, lpidx, lpx bits} per level-ordered entry (deferred split)
 	int pending;               // bit 0: apply the previous level's correction first; bit 1: non-temporal record loads
 	int first_prev;            // the previous level is level 0 (q-cache restart of its entries)
+	int pend_kind;             // level 0 of a v sweep: the pending correction is the previous sweep's last
+	                           // level (1: v of the other q-cache slot, 2: w); 0: this sweep's own
 	// online VB (vbfm_online.hip): natural-gradient steps on a mini-batch; nat == nullptr: VB
 	double2 *nat;              // natural parameters {mu, sigma} of each feature, laid out like ms
 	double *rho;               // step size of each feature (new_wj / new_vj)

@@ -398,7 +398,10 @@ DEVI void add_next_q(Rec &v, float x, bool first, double2 nx)
 	else qacc<1 - P>(v, x, first, nx);
 }
 
-template <int BLOCK, int R, bool IS_W, int P, bool NEXT>
+// PK: which level's correction is pending -- 0: the previous level of this sweep; at level 0 of
+// a v sweep the previous sweep's last level, left unflushed: 1 = v with the other q-cache slot
+// (the previous factor), 2 = w (the w sweep before factor 0)
+template <int BLOCK, int R, bool IS_W, int P, bool NEXT, int PK = 0>
 __global__ __launch_bounds__(BLOCK) void k_lord_defer(LevelArgs a)
 {
 	constexpr uint32_t CAP = BLOCK * R;
@@ -445,7 +448,11 @@ __global__ __launch_bounds__(BLOCK) void k_lord_defer(LevelArgs a)
 			Rec v;
 			lds_get(recs, i, v);
 			const float x = __uint_as_float(q[u].x);
-			if (pending) apply_pending<IS_W, P>(v, t[u], __uint_as_float(q[u].w));
+			if (pending) {
+				if constexpr (PK == 0) apply_pending<IS_W, P>(v, t[u], __uint_as_float(q[u].w));
+				else if constexpr (PK == 1) apply_pending<false, 1 - P>(v, t[u], __uint_as_float(q[u].w));
+				else apply_pending<true, 0>(v, t[u], __uint_as_float(q[u].w));
+			}
 			if constexpr (NEXT) add_next_q<IS_W, P>(v, x, first, nx);
 			if (pending || NEXT) lds_put(recs, i, v);
 			op.stat(v, x, s1, s2);
@@ -529,13 +536,23 @@ __global__ __launch_bounds__(256) void k_lord_prev_fill(const uint32_t *feats, c
 	}
 }
 
+template <bool IS_W, int P, bool NEXT, int PK>
+void launch_defer_pk(const LevelArgs &a, hipStream_t s)
+{
+	if (a.avg_len <= 96) k_lord_defer<64, 2, IS_W, P, NEXT, PK><<<a.nfeat, 64, 0, s>>>(a);
+	else if (a.avg_len <= 320) k_lord_defer<256, 1, IS_W, P, NEXT, PK><<<a.nfeat, 256, 0, s>>>(a);
+	else if (a.avg_len <= 640) k_lord_defer<256, 2, IS_W, P, NEXT, PK><<<a.nfeat, 256, 0, s>>>(a);
+	else k_lord_defer<512, 2, IS_W, P, NEXT, PK><<<a.nfeat, 512, 0, s>>>(a);
+}
+
 template <bool IS_W, int P, bool NEXT>
 void launch_defer(const LevelArgs &a, hipStream_t s)
 {
-	if (a.avg_len <= 96) k_lord_defer<64, 2, IS_W, P, NEXT><<<a.nfeat, 64, 0, s>>>(a);
-	else if (a.avg_len <= 320) k_lord_defer<256, 1, IS_W, P, NEXT><<<a.nfeat, 256, 0, s>>>(a);
-	else if (a.avg_len <= 640) k_lord_defer<256, 2, IS_W, P, NEXT><<<a.nfeat, 256, 0, s>>>(a);
-	else k_lord_defer<512, 2, IS_W, P, NEXT><<<a.nfeat, 512, 0, s>>>(a);
+	if constexpr (!IS_W) {
+		if (a.pend_kind == 1) return launch_defer_pk<IS_W, P, NEXT, 1>(a, s);
+		if (a.pend_kind == 2) return launch_defer_pk<IS_W, P, NEXT, 2>(a, s);
+	}
+	launch_defer_pk<IS_W, P, NEXT, 0>(a, s);
 }
 
 template <bool IS_W, int P, bool NEXT>
