@@ -235,9 +235,18 @@ def main():
         kernel = "k_mc_level_lord" if layout == "level" else "k_mc_v_level"
     else:
         kernel = "k_level_lord" if layout == "level" else "k_v_level_fused"
+    # row shards (N > 1, or the multi-rank kernels forced on one GPU): a level is the split
+    # form -- statistics kernel, RCCL all-reduce, posterior / correction -- and its time (the
+    # per-level events bracket all of it) is what avg_launch_ms reports
+    split = (world > 1 and not fshard and not online) or os.environ.get("VBFM_FORCE_SPLIT") == "1"
+    if split:
+        kernel = {"k_level_lord": "k_lord_defer + all-reduce + post (per level)",
+                  "k_mc_level_lord": "k_mc_lord_defer + all-reduce + post (per level)",
+                  "k_v_level_fused": "k_v_level_stats + all-reduce + k_v_level_correct (per level)",
+                  "k_mc_v_level": "k_mc_v_level stats + all-reduce + draw (per level)"}.get(kernel, kernel)
     tf = os.path.join(ROOT, "profiles", "traffic_%s_%s%s.json" % (args.config, layout,
                                                                    "_" + args.method if mc or online else ""))
-    if os.path.exists(tf):
+    if os.path.exists(tf) and not split:
         with open(tf) as fh:
             traffic = json.load(fh).get("bytes_per_launch")
     result = {
