@@ -132,7 +132,9 @@ def main():
 
     if world > 1:
         dist.init_process_group("gloo", rank=rank, world_size=world)
-    torch.cuda.set_device(local_rank)
+    ndev = torch.cuda.device_count()
+    device = local_rank % max(1, ndev)      # one rank per GPU; a rehearsal with more ranks than GPUs shares them
+    torch.cuda.set_device(device)
 
     t0 = time.time()
     online = args.method == "vb_online"
@@ -140,12 +142,12 @@ def main():
     if online:
         if world > 1:
             raise SystemExit("vb_online runs on one GPU")
-        fml = vbfm.FMLearnVBOnline(1, 1, k, D, min_target=1.0, max_target=5.0, device=local_rank)
+        fml = vbfm.FMLearnVBOnline(1, 1, k, D, min_target=1.0, max_target=5.0, device=device)
     elif mc:
-        fml = vbfm.FMLearnMCMC(1, 1, k, D, min_target=1.0, max_target=5.0, device=local_rank, method=args.method,
+        fml = vbfm.FMLearnMCMC(1, 1, k, D, min_target=1.0, max_target=5.0, device=device, method=args.method,
                                layout=args.layout)
     else:
-        fml = vbfm.FMLearnVB(1, 1, k, D, min_target=1.0, max_target=5.0, device=local_rank, layout=args.layout)
+        fml = vbfm.FMLearnVB(1, 1, k, D, min_target=1.0, max_target=5.0, device=device, layout=args.layout)
     fshard = args.shard == "features"
     if fshard:
         if mc:

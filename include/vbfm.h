@@ -180,6 +180,21 @@ int vbfm_factor_sweep(vbfm_ctx *ctx, double *ms_device);
 int vbfm_comm_unique_id(uint8_t out[128]);
 int vbfm_comm_init(vbfm_ctx *ctx, int32_t nranks, int32_t rank, const uint8_t uid[128]);
 
+/* The same row- / feature-sharded modes with a caller-supplied exchange instead of RCCL:
+ * every all-reduce of the path stages its buffer in host memory and calls
+ * fn(user, buf, count, dtype, op), which must all-reduce buf in place across the ranks and
+ * return 0 (non-zero: the call fails with "host exchange failed"). dtype: VBFM_X_F64 /
+ * VBFM_X_U32 / VBFM_X_U8; op: VBFM_X_SUM / VBFM_X_MAX. Test transport (e.g. a gloo
+ * all-reduce from Python): it lets several ranks share one GPU, which RCCL refuses, so the
+ * multi-rank kernels run on a one-GPU box exactly as over RCCL, minus the collective itself. */
+#define VBFM_X_F64 0
+#define VBFM_X_U32 1
+#define VBFM_X_U8 2
+#define VBFM_X_SUM 0
+#define VBFM_X_MAX 1
+typedef int (*vbfm_exchange_fn)(void *user, void *buf, uint64_t count, int32_t dtype, int32_t op);
+int vbfm_comm_init_host(vbfm_ctx *ctx, int32_t nranks, int32_t rank, vbfm_exchange_fn fn, void *user);
+
 /* Partition of the VB sweep over ranks (set before vbfm_set_train).
  *   VBFM_SHARD_ROWS (default): the exact row-sharded mode above.
  *   VBFM_SHARD_FEATURES: the north star's feature-column partition. Every rank holds ALL train

@@ -28,12 +28,33 @@ int fail(vbfm_ctx *c, const std::string &m)
 
 void sync(vbfm_ctx *c) { HIPCHK(hipStreamSynchronize(c->s)); }
 
+// in-place all-reduce of a device buffer across the ranks: RCCL on the context's stream, or
+// (vbfm_comm_init_host) staged through host memory and handed to the caller's exchange
+void allreduce_dev(vbfm_ctx *c, void *buf, size_t n, ncclDataType_t t, ncclRedOp_t op)
+{
+	if (c->comm) {
+		NCCLCHK(ncclAllReduce(buf, buf, n, t, op, c->comm, c->s));
+		return;
+	}
+	if (!c->xfn) throw std::string("all-reduce without a communicator");
+	const size_t es = t == ncclDouble ? 8 : t == ncclUint32 ? 4 : 1;
+	const int32_t xt = t == ncclDouble ? VBFM_X_F64 : t == ncclUint32 ? VBFM_X_U32 : VBFM_X_U8;
+	if (t != ncclDouble && t != ncclUint32 && t != ncclUint8) throw std::string("host exchange: unsupported type");
+	if (c->xbuf.size() < n * es) c->xbuf.resize(n * es);
+	if (n) HIPCHK(hipMemcpyAsync(c->xbuf.data(), buf, n * es, hipMemcpyDeviceToHost, c->s));
+	sync(c);
+	if (c->xfn(c->xuser, c->xbuf.data(), n, xt, op == ncclMax ? VBFM_X_MAX : VBFM_X_SUM) != 0)
+		throw std::string("host exchange failed");
+	if (n) HIPCHK(hipMemcpyAsync(buf, c->xbuf.data(), n * es, hipMemcpyHostToDevice, c->s));
+	sync(c);
+}
+
 // all-reduce a few host doubles across the row shards (identity with one rank)
 void allreduce_host(vbfm_ctx *c, double *v, int n)
 {
 	if (!c->row_comm()) return;   // feature shards hold every row: their sums are already global
 	HIPCHK(hipMemcpyAsync(c->red_d, v, n * sizeof(double), hipMemcpyHostToDevice, c->s));
-	NCCLCHK(ncclAllReduce(c->red_d, c->red_d, n, ncclDouble, ncclSum, c->comm, c->s));
+	allreduce_dev(c, c->red_d, n, ncclDouble, ncclSum);
 	HIPCHK(hipMemcpyAsync(v, c->red_d, n * sizeof(double), hipMemcpyDeviceToHost, c->s));
 	sync(c);
 }
@@ -106,7 +127,7 @@ void lord_release(vbfm_ctx *c, bool keep_rows)
 	}
 	sync(c);
 	dfree(c->rows_alt); dfree(c->lcp); dfree(c->lx); dfree(c->lnext); dfree(c->lrow0); dfree(c->lpos0);
-	dfree(c->lpidx); dfree(c->lpx); dfree(c->post_tab); dfree(c->lpay);
+	dfree(c->lpidx); dfree(c->lpx); dfree(c->post_tab); dfree(c->lpay); dfree(c->lpay2);
 	c->lord = false;
 	c->rows_lorder = false;
 }
@@ -152,7 +173,17 @@ void build_lorder(vbfm_ctx *c, const std::vector<uint64_t> &cp, const std::vecto
 	}
 	c->lcp = dalloc<uint64_t>(lcp.size());
 	HIPCHK(hipMemcpyAsync(c->lcp, lcp.data(), lcp.size() * 8, hipMemcpyHostToDevice, c->s));
-	c->lx = dalloc<float>(d.nnz);
+	// x of every entry, unless all are 1.0f (one-hot libfm data): the level kernels then
+	// read no x at all (VBFM_LX=1 keeps the array)
+	{
+		uint32_t *cnt = dalloc<uint32_t>(1), h = 1;
+		HIPCHK(vbk::count_x_ne1(d.csc, d.nnz, cnt, c->s));
+		HIPCHK(hipMemcpyAsync(&h, cnt, 4, hipMemcpyDeviceToHost, c->s));
+		sync(c);
+		dfree(cnt);
+		const char *kx = getenv("VBFM_LX");
+		if (h != 0 || (kx && kx[0] == '1')) c->lx = dalloc<float>(d.nnz);
+	}
 	c->lnext = dalloc<uint32_t>(d.nnz);
 	c->lrow0 = dalloc<uint32_t>(n);
 	c->lpos0 = dalloc<uint32_t>(n);
@@ -198,8 +229,13 @@ void build_lorder(vbfm_ctx *c, const std::vector<uint64_t> &cp, const std::vecto
 		// one 16-B record per entry for the deferred kernels; the separate arrays are not
 		// read in this mode any more
 		dfree(tmp);
-		c->lpay = dalloc<uint4>(d.nnz);
-		HIPCHK(vbk::lord_pack(c->lx, c->lnext, c->lpidx, c->lpx, c->lpay, d.nnz, c->s));
+		if (c->lx) {
+			c->lpay = dalloc<uint4>(d.nnz);
+			HIPCHK(vbk::lord_pack(c->lx, c->lnext, c->lpidx, c->lpx, c->lpay, d.nnz, c->s));
+		} else {   // every x (and so every previous x) is 1: 8 B per entry
+			c->lpay2 = dalloc<uint2>(d.nnz);
+			HIPCHK(vbk::lord_pack2(c->lnext, c->lpidx, c->lpay2, d.nnz, c->s));
+		}
 		sync(c);
 		dfree(c->lx); dfree(c->lnext); dfree(c->lpidx); dfree(c->lpx);
 	}
@@ -238,9 +274,9 @@ void build_fshards(vbfm_ctx *c)
 {
 	fs_free(c);
 	if (c->shard_mode != VBFM_SHARD_FEATURES) return;
-	if (c->comm && c->fs_req > 1 && c->fs_req != c->nranks)
+	if (c->multi() && c->fs_req > 1 && c->fs_req != c->nranks)
 		throw std::string("feature shards: num_shards must equal the number of ranks (or 0)");
-	const int P = c->comm ? c->nranks : std::max(1, c->fs_req);
+	const int P = c->multi() ? c->nranks : std::max(1, c->fs_req);
 	c->fs_n = P;
 	const uint32_t L = nlevels(c), n = c->tr.n;
 	c->fs_lo.assign((size_t)L * (P + 1), 0);
@@ -248,7 +284,7 @@ void build_fshards(vbfm_ctx *c)
 		const uint32_t b = c->level_ptr[l], nl = c->level_ptr[l + 1] - b;
 		for (int s = 0; s <= P; s++) c->fs_lo[(size_t)l * (P + 1) + s] = b + (uint32_t)((uint64_t)nl * s / P);
 	}
-	if (c->comm) {
+	if (c->multi()) {
 		std::vector<uint32_t> feats(c->tr.nf), own;
 		if (c->tr.nf) HIPCHK(hipMemcpy(feats.data(), c->level_feats, (size_t)c->tr.nf * 4, hipMemcpyDeviceToHost));
 		for (uint32_t l = 0; l < L; l++)
@@ -261,7 +297,7 @@ void build_fshards(vbfm_ctx *c)
 	}
 	c->fs_base = dalloc<double>(2 * (size_t)n);
 	c->fs_buf = dalloc<double>(5 * (size_t)n);
-	if (!c->comm && P > 1) c->fs_rows0 = dalloc<RowRec>(n);
+	if (!c->multi() && P > 1) c->fs_rows0 = dalloc<RowRec>(n);
 }
 
 // one level of one shard: the shard's chunk of the level's columns (fused kernels; the fused
@@ -288,7 +324,7 @@ void fs_pass(vbfm_ctx *c, bool is_w, int f)
 {
 	const uint32_t n = c->tr.n;
 	const int next = is_w ? (c->k > 0 ? 0 : -1) : (f + 1 < c->k ? ((f + 1) & 1) : -1);
-	const bool local = !c->comm;   // shards run here one after another
+	const bool local = !c->multi();   // shards run here one after another
 	const int s0 = local ? 0 : c->rank, s1 = local ? c->fs_n : c->rank + 1;
 	HIPCHK(vbk::fs_begin(c->rows, n, c->fs_base, next, c->s));
 	if (local && c->fs_n > 1)
@@ -299,14 +335,14 @@ void fs_pass(vbfm_ctx *c, bool is_w, int f)
 		for (uint32_t l = 0; l < nlevels(c); l++) sweep_level_shard(c, l, is_w, f, s);
 		HIPCHK(vbk::fs_pack(c->rows, n, c->fs_base, c->fs_buf, next, s > s0, c->s));
 	}
-	if (c->comm) {
-		NCCLCHK(ncclAllReduce(c->fs_buf, c->fs_buf, (next < 0 ? 2 : 5) * (size_t)n, ncclDouble, ncclSum, c->comm, c->s));
+	if (c->multi()) {
+		allreduce_dev(c, c->fs_buf, (next < 0 ? 2 : 5) * (size_t)n, ncclDouble, ncclSum);
 		// parameters: each rank contributes its own features, zero elsewhere
 		double2 *ms = is_w ? c->ms_w : c->ms_v + f;
 		const uint32_t stride = is_w ? 1 : (uint32_t)c->k;
 		HIPCHK(hipMemsetAsync(c->fs_pbuf, 0, (size_t)c->tr.nf * 16, c->s));
 		HIPCHK(vbk::fs_params(ms, stride, c->fs_own, c->fs_own_n, c->fs_pbuf, 1, c->s));
-		NCCLCHK(ncclAllReduce(c->fs_pbuf, c->fs_pbuf, 2 * (size_t)c->tr.nf, ncclDouble, ncclSum, c->comm, c->s));
+		allreduce_dev(c, c->fs_pbuf, 2 * (size_t)c->tr.nf, ncclDouble, ncclSum);
 		HIPCHK(vbk::fs_params(ms, stride, c->level_feats, c->tr.nf, c->fs_pbuf, 0, c->s));
 	}
 	HIPCHK(vbk::fs_unpack(c->rows, n, c->fs_base, c->fs_buf, next, c->s));
@@ -346,14 +382,14 @@ void build_schedule(vbfm_ctx *c)
 	HIPCHK(hipMemsetAsync(c->dup, 0, nf, c->s));
 	HIPCHK(vbk::level_init(level, nf, c->s));
 	HIPCHK(vbk::mark_dups(d.row_ptr, d.csr, d.n, c->dup, c->s));
-	if (c->comm && nf) NCCLCHK(ncclAllReduce(c->dup, c->dup, nf, ncclUint8, ncclMax, c->comm, c->s));
+	if (c->multi() && nf) allreduce_dev(c, c->dup, nf, ncclUint8, ncclMax);
 	for (int round = 0;; round++) {
 		uint32_t ch = 0;
 		HIPCHK(hipMemsetAsync(changed, 0, 4, c->s));
 		HIPCHK(vbk::level_relax(d.row_ptr, d.csr, d.n, nf, level, changed, c->s));
-		if (c->comm) {
-			if (nf) NCCLCHK(ncclAllReduce(level, level, nf, ncclUint32, ncclMax, c->comm, c->s));
-			NCCLCHK(ncclAllReduce(changed, changed, 1, ncclUint32, ncclMax, c->comm, c->s));
+		if (c->multi()) {
+			if (nf) allreduce_dev(c, level, nf, ncclUint32, ncclMax);
+			allreduce_dev(c, changed, 1, ncclUint32, ncclMax);
 		}
 		HIPCHK(hipMemcpyAsync(&ch, changed, 4, hipMemcpyDeviceToHost, c->s));
 		sync(c);
@@ -522,10 +558,11 @@ void sweep_level(vbfm_ctx *c, uint32_t l, bool is_w, int f)
 		a.first_level = l == 0;
 		if (!c->row_comm() && !c->force_split) {
 			HIPCHK(vbk::lord_level(a, is_w, c->s));
-		} else if (c->lpay) {
+		} else if (c->deferred()) {
 			// deferred: level l-1's correction, level l's statistics and the move in one pass;
 			// level l's correction after the all-reduce, by level l+1 (or the flush)
 			a.lpay = c->lpay;
+			a.lpay2 = c->lpay2;
 			a.tab = c->post_tab;
 			// level 0 of a v sweep may carry the previous sweep's last correction (vbfm_iterate)
 			const bool carried = l == 0 && c->carry != 0 && !is_w;
@@ -540,7 +577,7 @@ void sweep_level(vbfm_ctx *c, uint32_t l, bool is_w, int f)
 			a.first_prev = l == 1;
 			HIPCHK(vbk::lord_defer_level(a, is_w, c->s));
 			if (c->row_comm())
-				NCCLCHK(ncclAllReduce(c->stats, c->stats, 2 * (size_t)a.nfeat, ncclDouble, ncclSum, c->comm, c->s));
+				allreduce_dev(c, c->stats, 2 * (size_t)a.nfeat, ncclDouble, ncclSum);
 			HIPCHK(vbk::lord_defer_post(a, is_w, c->s));
 			if (l + 1 == nlevels(c)) {
 				// the sweep's last correction: left to level 0 of the next sweep when one follows
@@ -558,7 +595,7 @@ void sweep_level(vbfm_ctx *c, uint32_t l, bool is_w, int f)
 		} else {
 			HIPCHK(vbk::lord_level_stats(a, is_w, c->s));
 			if (c->row_comm())
-				NCCLCHK(ncclAllReduce(c->stats, c->stats, 2 * (size_t)a.nfeat, ncclDouble, ncclSum, c->comm, c->s));
+				allreduce_dev(c, c->stats, 2 * (size_t)a.nfeat, ncclDouble, ncclSum);
 			HIPCHK(vbk::lord_level_move(a, is_w, c->s));
 		}
 		std::swap(c->rows, c->rows_alt);
@@ -574,7 +611,7 @@ void sweep_level(vbfm_ctx *c, uint32_t l, bool is_w, int f)
 	// the shards, then every shard applies the identical posterior to its own rows
 	HIPCHK(is_w ? vbk::w_level_stats(a, c->s) : vbk::v_level_stats(a, c->s));
 	if (c->row_comm())
-		NCCLCHK(ncclAllReduce(c->stats, c->stats, 2 * (size_t)a.nfeat, ncclDouble, ncclSum, c->comm, c->s));
+		allreduce_dev(c, c->stats, 2 * (size_t)a.nfeat, ncclDouble, ncclSum);
 	HIPCHK(is_w ? vbk::w_level_correct(a, c->s) : vbk::v_level_correct(a, c->s));
 	prof_end(c, p);
 }
@@ -812,7 +849,7 @@ static void alloc_rows(vbfm_ctx *c)
 	uint64_t n = c->tr.n;
 	c->n_global = n;
 	c->q_ready[0] = c->q_ready[1] = -1;
-	if (c->comm) {
+	if (c->multi()) {
 		double v = (double)n;
 		allreduce_host(c, &v, 1);
 		c->n_global = (uint64_t)v;
@@ -823,10 +860,10 @@ static void alloc_rows(vbfm_ctx *c)
 // the train feature count every shard pads to (the max over shards)
 static uint32_t global_nf(vbfm_ctx *c, uint32_t nf)
 {
-	if (!c->comm) return nf;
+	if (!c->multi()) return nf;
 	uint32_t *w = dalloc<uint32_t>(1);
 	HIPCHK(hipMemcpyAsync(w, &nf, 4, hipMemcpyHostToDevice, c->s));
-	NCCLCHK(ncclAllReduce(w, w, 1, ncclUint32, ncclMax, c->comm, c->s));
+	allreduce_dev(c, w, 1, ncclUint32, ncclMax);
 	uint32_t out = 0;
 	HIPCHK(hipMemcpyAsync(&out, w, 4, hipMemcpyDeviceToHost, c->s));
 	sync(c);
@@ -1170,7 +1207,7 @@ int vbfm_iterate(vbfm_ctx *c, vbfm_iter_stats *o)
 		// the sweeps follow each other directly: a deferred split may carry a sweep's last
 		// correction into the next sweep's first level (sweep_level); the last sweep flushes
 		c->carry = 0;
-		c->carry_ok = c->lpay && c->D > 0 && c->k > 0;
+		c->carry_ok = c->deferred() && c->D > 0 && c->k > 0;
 		try {
 			if (c->k1) { Range r("update_w sweep"); step_w(c); }
 			HIPCHK(hipEventRecord(c->ev[EV_W], c->s));
@@ -1297,6 +1334,21 @@ int vbfm_comm_init(vbfm_ctx *c, int32_t nranks, int32_t rank, const uint8_t uid[
 		ncclUniqueId id;
 		memcpy(&id, uid, 128);
 		NCCLCHK(ncclCommInitRank(&c->comm, nranks, id, rank));
+		c->nranks = nranks;
+		c->rank = rank;
+	});
+}
+
+int vbfm_comm_init_host(vbfm_ctx *c, int32_t nranks, int32_t rank, vbfm_exchange_fn fn, void *user)
+{
+	if (!c) return fail(nullptr, "null context");
+	return guarded(c, [&] {
+		if (c->rows) throw std::string("vbfm_comm_init_host must precede vbfm_set_train");
+		if (c->multi()) throw std::string("the context already has a communicator");
+		if (nranks < 1 || rank < 0 || rank >= nranks) throw std::string("bad rank / nranks");
+		if (!fn) throw std::string("null exchange function");
+		c->xfn = fn;
+		c->xuser = user;
 		c->nranks = nranks;
 		c->rank = rank;
 	});

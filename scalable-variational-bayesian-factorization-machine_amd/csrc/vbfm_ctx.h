@@ -141,6 +141,7 @@ struct vbfm_ctx {
 	uint32_t *lpos0 = nullptr;     // [n] level-0 position of each row
 	uint32_t *lpidx = nullptr;     // [nnz] split form: the row's previous-level feature (index in its level)
 	float *lpx = nullptr;          // [nnz] ... and its x (deferred correction)
+	uint2 *lpay2 = nullptr;        // [nnz] ... {lnext, lpidx} instead when every x is 1 (no lx)
 	uint4 *lpay = nullptr;         // [nnz] deferred split: {x, lnext, lpidx, lpx} of every entry in one
 	                               // 16-B load (lx / lnext / lpidx / lpx are freed once packed)
 	PostT *post_tab = nullptr;     // [max level width] posteriors of the last level swept
@@ -159,7 +160,12 @@ struct vbfm_ctx {
 	double *fs_buf = nullptr;      // [5n] summed changes / partial q-caches
 	double2 *fs_pbuf = nullptr;    // [nf] parameter exchange
 	RowRec *fs_rows0 = nullptr;    // in-process shards: the rows at the start of a pass
-	bool row_comm() const { return comm && shard_mode == VBFM_SHARD_ROWS; }
+	vbfm_exchange_fn xfn = nullptr; // vbfm_comm_init_host: all-reduces through the caller
+	void *xuser = nullptr;
+	std::vector<uint8_t> xbuf;      // host staging of a host-exchange all-reduce
+	bool deferred() const { return lpay || lpay2; }
+	bool multi() const { return comm || xfn; }
+	bool row_comm() const { return multi() && shard_mode == VBFM_SHARD_ROWS; }
 	McState *mc = nullptr;         // set by vbfm_mcmc_init: the context runs the MCMC / ALS learner
 	OvState *ov = nullptr;         // set by vbfm_online_init: the context runs the online VB learner
 	// vbfm_init_params_replay: the draws' seed and the glibc outputs they consumed (after the
@@ -192,6 +198,8 @@ template <class F> int guarded(vbfm_ctx *c, F &&fn)
 
 void sync(vbfm_ctx *c);
 void allreduce_host(vbfm_ctx *c, double *v, int n);
+// in-place all-reduce of a device buffer over the ranks (RCCL on c->s, or the host exchange)
+void allreduce_dev(vbfm_ctx *c, void *buf, size_t n, ncclDataType_t t, ncclRedOp_t op);
 double finish_sum(vbfm_ctx *c, uint32_t nblocks);
 void require_train(vbfm_ctx *c);
 uint32_t nlevels(vbfm_ctx *c);

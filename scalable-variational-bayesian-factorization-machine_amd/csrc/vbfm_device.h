@@ -82,6 +82,7 @@ struct LevelArgs {
 	const float *lpx;          // ... and that entry's x
 	PostT *tab;                // posteriors of the previous level (read) / of this level (written)
 	const uint4 *lpay;         // {x bits, lnext, lpidx, lpx bits} per level-ordered entry (deferred split)
+	const uint2 *lpay2;        // ... {lnext, lpidx} instead when every x is 1 (lpay null)
 	int pending;               // bit 0: apply the previous level's correction first; bit 1: non-temporal record loads
 	int first_prev;            // the previous level is level 0 (q-cache restart of its entries)
 	int pend_kind;             // level 0 of a v sweep: the pending correction is the previous sweep's last
@@ -135,6 +136,7 @@ struct McArgs {
 	const float *lpx;
 	PostT *tab;                // {mo = old value, mu = drawn value or NaN (no correction)}
 	const uint4 *lpay;         // as LevelArgs::lpay
+	const uint2 *lpay2;        // as LevelArgs::lpay2
 	int pending;               // bit 0: apply the previous level's correction; bit 1: nt loads
 };
 
@@ -171,6 +173,10 @@ hipError_t lord_fill(const uint32_t *feats, uint32_t nfeat, const uint64_t *lcp,
 // dst[p] = src[idx[p]] / dst[idx[p]] = src[p]
 hipError_t rows_gather(RowRec *dst, const RowRec *src, const uint32_t *idx, uint32_t n, hipStream_t s);
 // lpay[p] = {lx[p], lnext[p], lpidx[p], lpx[p]}
+// entries of a CSC whose x is not 1.0f: *cnt = 0 iff every x is 1 (count of waves that saw one)
+hipError_t count_x_ne1(const uint2 *csc, uint64_t nnz, uint32_t *cnt, hipStream_t s);
+// lpay2[p] = {lnext[p], lpidx[p]} (every x 1)
+hipError_t lord_pack2(const uint32_t *lnext, const uint32_t *lpidx, uint2 *lpay2, uint64_t nnz, hipStream_t s);
 hipError_t lord_pack(const float *lx, const uint32_t *lnext, const uint32_t *lpidx, const float *lpx, uint4 *lpay,
                      uint64_t nnz, hipStream_t s);
 hipError_t rows_scatter(RowRec *dst, const RowRec *src, const uint32_t *idx, uint32_t n, hipStream_t s);

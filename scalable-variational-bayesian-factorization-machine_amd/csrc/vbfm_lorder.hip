@@ -146,7 +146,7 @@ DEVI void lord_stats(double2 *recs, const RowRec *src, const float *lx, uint32_t
 		for (uint32_t i = threadIdx.x; i < m; i += BLOCK) {
 			Rec v;
 			lds_get(recs, i, v);
-			op.stat(v, lx[base + i], s1, s2);
+			op.stat(v, lx ? lx[base + i] : 1.0f, s1, s2);
 		}
 	}
 }
@@ -170,7 +170,7 @@ DEVI void lord_move(double2 *recs, uint32_t *dsts, const RowRec *src, const floa
 		for (uint32_t i = threadIdx.x; i < m; i += BLOCK) {
 			Rec v;
 			lds_get(recs, i, v);
-			op.apply(v, lx[base + i], first);
+			op.apply(v, lx ? lx[base + i] : 1.0f, first);
 			lds_put(recs, i, v);
 			dsts[i] = nxt[base + i];
 		}
@@ -179,6 +179,63 @@ DEVI void lord_move(double2 *recs, uint32_t *dsts, const RowRec *src, const floa
 			const uint32_t i = t >> 2, c = t & 3;
 			d[(size_t)dsts[i] * 4 + c] = recs[lslot(i, c)];
 		}
+	}
+}
+
+// A run that fits LDS (n <= CAP = BLOCK*R), thread-owned entries i = threadIdx.x + u*BLOCK
+// (the order lord_stats / lord_move visit them): each entry's x and next position are loaded
+// into registers BEFORE the records stream in, so their latency hides under the run's load
+// instead of following it (the stats loop then touches no global memory; 15 % per launch at C4
+// measured with the x array present, gpurun_out/r24).
+template <int BLOCK, int R>
+DEVI void res_prefetch(const float *lx, const uint32_t *nxt, uint32_t n, float (&xr)[R], uint32_t (&nr)[R])
+{
+#pragma unroll
+	for (int u = 0; u < R; ++u) {
+		const uint32_t i = threadIdx.x + u * BLOCK;
+		xr[u] = 1.0f;
+		nr[u] = 0;
+		if (i < n) {
+			nr[u] = nxt[i];
+			if (lx) xr[u] = lx[i];
+		}
+	}
+}
+
+template <int BLOCK, int R, class Op>
+DEVI void res_stats(const double2 *recs, uint32_t n, const float (&xr)[R], const Op &op, double &s1, double &s2)
+{
+#pragma unroll
+	for (int u = 0; u < R; ++u) {
+		const uint32_t i = threadIdx.x + u * BLOCK;
+		if (i < n) {
+			Rec v;
+			lds_get(recs, i, v);
+			op.stat(v, xr[u], s1, s2);
+		}
+	}
+}
+
+template <int BLOCK, int R, class Op>
+DEVI void res_move(double2 *recs, uint32_t *dsts, uint32_t n, const float (&xr)[R], const uint32_t (&nr)[R],
+                   RowRec *dst, bool first, const Op &op)
+{
+#pragma unroll
+	for (int u = 0; u < R; ++u) {
+		const uint32_t i = threadIdx.x + u * BLOCK;
+		if (i < n) {
+			Rec v;
+			lds_get(recs, i, v);
+			op.apply(v, xr[u], first);
+			lds_put(recs, i, v);
+			dsts[i] = nr[u];
+		}
+	}
+	__syncthreads();
+	double2 *d = reinterpret_cast<double2 *>(dst);
+	for (uint32_t t = threadIdx.x; t < n * 4; t += BLOCK) {
+		const uint32_t i = t >> 2, c = t & 3;
+		d[(size_t)dsts[i] * 4 + c] = recs[lslot(i, c)];
 	}
 }
 
@@ -197,20 +254,32 @@ __global__ __launch_bounds__(BLOCK) void k_level_lord(LevelArgs a)
 	const uint64_t sb = a.lcp[blockIdx.x];
 	const uint32_t n = (uint32_t)(a.lcp[blockIdx.x + 1] - sb);
 	const RowRec *src = a.src + (sb - a.lbase);
-	const float *lx = a.lx + sb;
+	const float *lx = a.lx ? a.lx + sb : nullptr;   // null: every x is 1 (lx not stored)
 	const double2 msj = a.ms[(size_t)j * a.ms_stride];
 	VbOp<IS_W, P, NEXT> op;
 	op.mo = msj.x; op.so = msj.y;
 	op.nx = NEXT ? a.ms_next[(size_t)j * a.ms_stride_next] : make_double2(0.0, 0.0);
 
 	double s1 = 0.0, s2 = 0.0;
+	const double hyp = a.hyp[(size_t)a.attr_group[j] * a.hyp_stride];
+	if (n <= CAP) {   // the run stays in LDS from the statistics to the move
+		float xr[R];
+		uint32_t nr[R];
+		res_prefetch<BLOCK, R>(lx, a.lnext + sb, n, xr, nr);
+		stage_in<BLOCK>(recs, reinterpret_cast<const double2 *>(src), n);
+		__syncthreads();
+		res_stats<BLOCK, R>(recs, n, xr, op, s1, s2);
+		block_sum2<BLOCK>(s1, s2, lds);
+		op.go = vb_post<IS_W>(s1, s2, hyp, a.alpha, op.mo, op.so, op.mu, op.sig, a.counters, threadIdx.x == 0);
+		if (threadIdx.x == 0) a.ms[(size_t)j * a.ms_stride] = make_double2(op.mu, op.sig);
+		res_move<BLOCK, R>(recs, dsts, n, xr, nr, a.dst, a.first_level != 0, op);
+		return;
+	}
 	lord_stats<BLOCK, CAP>(recs, src, lx, n, op, s1, s2);
 	block_sum2<BLOCK>(s1, s2, lds);
-
-	const double hyp = a.hyp[(size_t)a.attr_group[j] * a.hyp_stride];
 	op.go = vb_post<IS_W>(s1, s2, hyp, a.alpha, op.mo, op.so, op.mu, op.sig, a.counters, threadIdx.x == 0);
 	if (threadIdx.x == 0) a.ms[(size_t)j * a.ms_stride] = make_double2(op.mu, op.sig);
-	lord_move<BLOCK, CAP>(recs, dsts, src, lx, a.lnext + sb, n, n <= CAP, a.dst, a.first_level != 0, op);
+	lord_move<BLOCK, CAP>(recs, dsts, src, lx, a.lnext + sb, n, false, a.dst, a.first_level != 0, op);
 }
 
 // split form (row-sharded multi-GPU): statistics of the local rows -> all-reduce -> move
@@ -227,7 +296,7 @@ __global__ __launch_bounds__(BLOCK) void k_level_lord_stats(LevelArgs a)
 	VbOp<IS_W, P, false> op;
 	op.mo = msj.x; op.so = msj.y;
 	double s1 = 0.0, s2 = 0.0;
-	lord_stats<BLOCK, CAP>(recs, a.src + (sb - a.lbase), a.lx + sb, n, op, s1, s2);
+	lord_stats<BLOCK, CAP>(recs, a.src + (sb - a.lbase), a.lx ? a.lx + sb : nullptr, n, op, s1, s2);
 	block_sum2<BLOCK>(s1, s2, lds);
 	if (threadIdx.x == 0) a.stats[blockIdx.x] = make_double2(s1, s2);
 }
@@ -249,7 +318,7 @@ __global__ __launch_bounds__(BLOCK) void k_level_lord_move(LevelArgs a)
 	const double hyp = a.hyp[(size_t)a.attr_group[j] * a.hyp_stride];
 	op.go = vb_post<IS_W>(st.x, st.y, hyp, a.alpha, op.mo, op.so, op.mu, op.sig, a.counters, threadIdx.x == 0);
 	if (threadIdx.x == 0) a.ms[(size_t)j * a.ms_stride] = make_double2(op.mu, op.sig);
-	lord_move<BLOCK, CAP>(recs, dsts, a.src + (sb - a.lbase), a.lx + sb, a.lnext + sb, n, false, a.dst,
+	lord_move<BLOCK, CAP>(recs, dsts, a.src + (sb - a.lbase), a.lx ? a.lx + sb : nullptr, a.lnext + sb, n, false, a.dst,
 	                      a.first_level != 0, op);
 }
 
@@ -268,11 +337,28 @@ __global__ __launch_bounds__(BLOCK) void k_mc_level_lord(McArgs a)
 	const uint64_t sb = a.lcp[blockIdx.x];
 	const uint32_t n = (uint32_t)(a.lcp[blockIdx.x + 1] - sb);
 	const RowRec *src = a.src + (sb - a.lbase);
-	const float *lx = a.lx + sb;
+	const float *lx = a.lx ? a.lx + sb : nullptr;
 	McOp<IS_W, P, NEXT> op;
 	op.vo = a.par[(size_t)j * a.stride].x;
 	op.vn = NEXT ? a.par_next[(size_t)j * a.next_stride].x : 0.0;
 	double sm = 0.0, ss = 0.0;
+	if constexpr (MODE == 0) {
+		if (n <= CAP) {   // resident run, x / next positions prefetched (as k_level_lord)
+			float xr[R];
+			uint32_t nr[R];
+			res_prefetch<BLOCK, R>(lx, a.lnext + sb, n, xr, nr);
+			stage_in<BLOCK>(recs, reinterpret_cast<const double2 *>(src), n);
+			__syncthreads();
+			res_stats<BLOCK, R>(recs, n, xr, op, sm, ss);
+			block_sum2<BLOCK>(sm, ss, lds);
+			const uint32_t g = a.attr_group[j];
+			op.go = mc_draw(sm, ss, op.vo, a.lambda[(size_t)g * a.hstride], a.mu[(size_t)g * a.hstride], a.alpha,
+			                mc_z(a, j), a.z != nullptr, a.sample, !IS_W, op.v, a.counters, threadIdx.x == 0);
+			if (threadIdx.x == 0) a.par[(size_t)j * a.stride].x = op.v;
+			res_move<BLOCK, R>(recs, dsts, n, xr, nr, a.dst, a.first_level != 0, op);
+			return;
+		}
+	}
 	if constexpr (MODE != 2) {
 		lord_stats<BLOCK, CAP>(recs, src, lx, n, op, sm, ss);
 		block_sum2<BLOCK>(sm, ss, lds);
@@ -290,8 +376,7 @@ __global__ __launch_bounds__(BLOCK) void k_mc_level_lord(McArgs a)
 		op.go = mc_draw(sm, ss, op.vo, a.lambda[(size_t)g * a.hstride], a.mu[(size_t)g * a.hstride], a.alpha,
 		                mc_z(a, j), a.z != nullptr, a.sample, !IS_W, op.v, a.counters, threadIdx.x == 0);
 		if (threadIdx.x == 0) a.par[(size_t)j * a.stride].x = op.v;
-		lord_move<BLOCK, CAP>(recs, dsts, src, lx, a.lnext + sb, n, MODE == 0 && n <= CAP, a.dst, a.first_level != 0,
-		                      op);
+		lord_move<BLOCK, CAP>(recs, dsts, src, lx, a.lnext + sb, n, false, a.dst, a.first_level != 0, op);
 	}
 }
 
@@ -300,7 +385,14 @@ __global__ void k_lord_pack(const float *lx, const uint32_t *lnext, const uint32
                             uint64_t nnz)
 {
 	const uint64_t p = (uint64_t)blockIdx.x * 256u + threadIdx.x;
-	if (p < nnz) lpay[p] = make_uint4(__float_as_uint(lx[p]), lnext[p], lpidx[p], __float_as_uint(lpx[p]));
+	if (p < nnz)
+		lpay[p] = make_uint4(__float_as_uint(lx ? lx[p] : 1.0f), lnext[p], lpidx[p], __float_as_uint(lpx[p]));
+}
+
+__global__ void k_lord_pack2(const uint32_t *lnext, const uint32_t *lpidx, uint2 *lpay2, uint64_t nnz)
+{
+	const uint64_t p = (uint64_t)blockIdx.x * 256u + threadIdx.x;
+	if (p < nnz) lpay2[p] = make_uint2(lnext[p], lpidx[p]);
 }
 
 // pos[row] = level-relative position of the row's entry in this level
@@ -327,10 +419,20 @@ __global__ __launch_bounds__(256) void k_lord_fill(const uint32_t *feats, const 
 	for (uint32_t i = threadIdx.x; i < n; i += 256) {
 		const uint2 ent = csc[cb + i];
 		const uint32_t r = ent.x & ROW_MASK;
-		lx[g0 + i] = ent_x(ent);
+		if (lx) lx[g0 + i] = ent_x(ent);
 		lnext[g0 + i] = pos_next[r];
 		if (row0) row0[g0 + i - lbase] = r;
 	}
+}
+
+// number of entries whose x is not 1.0f (the level store then keeps x per entry)
+__global__ __launch_bounds__(256) void k_count_x_ne1(const uint2 *csc, uint64_t nnz, uint32_t *cnt)
+{
+	uint32_t m = 0;
+	for (uint64_t p = (uint64_t)blockIdx.x * 256u + threadIdx.x; p < nnz; p += (uint64_t)gridDim.x * 256u)
+		m |= ent_x(csc[p]) != 1.0f;
+	m = __any(m);
+	if (m && (threadIdx.x & 63) == 0) atomicAdd(cnt, 1u);
 }
 
 // record permutations between row order and level-0 order; 4 lanes per 64-B record
@@ -380,6 +482,17 @@ void launch_lord_move(const LevelArgs &a, hipStream_t s)
 // last level of a sweep. Same arithmetic per row as the fused kernel: bit-identical results.
 // the previous level's correction (without its q-cache term: each level adds its own term
 // of the next factor's q-cache in its kernel, in the same per-row order as the fused kernel)
+// an entry's deferred payload {x, next position, previous-level feature, its x}: the 16-B
+// record, or the 8-B {next, previous} one when every x is 1
+template <class A> DEVI uint4 pay_at(const A &a, uint64_t p)
+{
+	if (a.lpay2) {
+		const uint2 w = a.lpay2[p];
+		return make_uint4(0x3f800000u, w.x, w.y, 0x3f800000u);
+	}
+	return a.lpay[p];
+}
+
 template <bool IS_W, int P>
 DEVI void apply_pending(Rec &v, const PostT &t, float x)
 {
@@ -414,7 +527,6 @@ __global__ __launch_bounds__(BLOCK) void k_lord_defer(LevelArgs a)
 	const RowRec *src = a.src + (sb - a.lbase);
 	const double2 *s = reinterpret_cast<const double2 *>(src);
 	double2 *d = reinterpret_cast<double2 *>(a.dst);
-	const uint4 *pay = a.lpay + sb;
 	const double2 msj = a.ms[(size_t)j * a.ms_stride];
 	VbOp<IS_W, P, NEXT> op;
 	op.mo = msj.x; op.so = msj.y;
@@ -434,7 +546,7 @@ __global__ __launch_bounds__(BLOCK) void k_lord_defer(LevelArgs a)
 		for (int u = 0; u < R; ++u) {
 			const uint32_t i = threadIdx.x + u * BLOCK;
 			if (i < m) {
-				q[u] = pay[base + i];
+				q[u] = pay_at(a, sb + base + i);
 				if (pending) t[u] = a.tab[q[u].z];
 			}
 		}
@@ -501,7 +613,7 @@ __global__ __launch_bounds__(256) void k_lord_defer_flush(LevelArgs a, uint32_t 
 	if (threadIdx.x < m) {
 		Rec v;
 		lds_get(recs, threadIdx.x, v);
-		const uint4 q = a.lpay[b + threadIdx.x];
+		const uint4 q = pay_at(a, b + threadIdx.x);
 		apply_pending<IS_W, P>(v, a.tab[q.z], __uint_as_float(q.w));
 		lds_put(recs, threadIdx.x, v);
 	}
@@ -597,7 +709,6 @@ __global__ __launch_bounds__(BLOCK) void k_mc_lord_defer(McArgs a)
 	const uint32_t n = (uint32_t)(a.lcp[blockIdx.x + 1] - sb);
 	const double2 *s = reinterpret_cast<const double2 *>(a.src + (sb - a.lbase));
 	double2 *d = reinterpret_cast<double2 *>(a.dst);
-	const uint4 *pay = a.lpay + sb;
 	McOp<IS_W, P, false> op;
 	op.vo = a.par[(size_t)j * a.stride].x;
 	const double vn = NEXT ? a.par_next[(size_t)j * a.next_stride].x : 0.0;
@@ -613,7 +724,7 @@ __global__ __launch_bounds__(BLOCK) void k_mc_lord_defer(McArgs a)
 		for (int u = 0; u < R; ++u) {
 			const uint32_t i = threadIdx.x + u * BLOCK;
 			if (i < m) {
-				q[u] = pay[base + i];
+				q[u] = pay_at(a, sb + base + i);
 				if (pending) t[u] = a.tab[q[u].z];
 			}
 		}
@@ -674,7 +785,7 @@ __global__ __launch_bounds__(256) void k_mc_lord_defer_flush(McArgs a, uint32_t 
 	if (threadIdx.x < m) {
 		Rec v;
 		lds_get(recs, threadIdx.x, v);
-		const uint4 q = a.lpay[b + threadIdx.x];
+		const uint4 q = pay_at(a, b + threadIdx.x);
 		mc_apply_pending<IS_W, P>(v, a.tab[q.z], __uint_as_float(q.w));
 		lds_put(recs, threadIdx.x, v);
 	}
@@ -848,6 +959,22 @@ hipError_t lord_fill(const uint32_t *feats, uint32_t nfeat, const uint64_t *lcp,
 {
 	if (nfeat == 0) return hipSuccess;
 	k_lord_fill<<<nfeat, 256, 0, s>>>(feats, lcp, lbase, col_ptr, csc, pos_next, lx, lnext, row0);
+	return hipGetLastError();
+}
+
+hipError_t count_x_ne1(const uint2 *csc, uint64_t nnz, uint32_t *cnt, hipStream_t s)
+{
+	const hipError_t e = hipMemsetAsync(cnt, 0, 4, s);
+	if (e != hipSuccess || nnz == 0) return e;
+	const uint64_t g = std::min<uint64_t>((nnz + 255) / 256, 8192);
+	k_count_x_ne1<<<(unsigned)g, 256, 0, s>>>(csc, nnz, cnt);
+	return hipGetLastError();
+}
+
+hipError_t lord_pack2(const uint32_t *lnext, const uint32_t *lpidx, uint2 *lpay2, uint64_t nnz, hipStream_t s)
+{
+	if (nnz == 0) return hipSuccess;
+	k_lord_pack2<<<(unsigned)((nnz + 255) / 256), 256, 0, s>>>(lnext, lpidx, lpay2, nnz);
 	return hipGetLastError();
 }
 

@@ -309,15 +309,16 @@ void mc_sweep(vbfm_ctx *c, bool is_w, int f)
 			a.first_level = l == 0;
 			if (!c->row_comm() && !c->force_split) {
 				HIPCHK(vbk::mc_lord_level(a, 0, is_w, c->s));
-			} else if (c->lpay) {
+			} else if (c->deferred()) {
 				// deferred: level l-1's correction, level l's statistics and the move in one pass;
 				// the draws after the all-reduce, applied by level l+1 (or the flush)
 				a.lpay = c->lpay;
+				a.lpay2 = c->lpay2;
 				a.tab = c->post_tab;
 				a.pending = l > 0 ? 3 : 0;
 				HIPCHK(vbk::mc_lord_defer_level(a, is_w, c->s));
 				if (c->row_comm())
-					NCCLCHK(ncclAllReduce(c->stats, c->stats, 2 * (size_t)a.nfeat, ncclDouble, ncclSum, c->comm, c->s));
+					allreduce_dev(c, c->stats, 2 * (size_t)a.nfeat, ncclDouble, ncclSum);
 				HIPCHK(vbk::mc_lord_defer_post(a, is_w, c->s));
 				if (l + 1 == nlevels(c)) {   // the sweep's last correction, on level-0-ordered records
 					a.dst = c->rows_alt;      // (swapped below)
@@ -326,7 +327,7 @@ void mc_sweep(vbfm_ctx *c, bool is_w, int f)
 			} else {
 				HIPCHK(vbk::mc_lord_level(a, 1, is_w, c->s));
 				if (c->row_comm())
-					NCCLCHK(ncclAllReduce(c->stats, c->stats, 2 * (size_t)a.nfeat, ncclDouble, ncclSum, c->comm, c->s));
+					allreduce_dev(c, c->stats, 2 * (size_t)a.nfeat, ncclDouble, ncclSum);
 				HIPCHK(vbk::mc_lord_level(a, 2, is_w, c->s));
 			}
 			std::swap(c->rows, c->rows_alt);
@@ -338,7 +339,7 @@ void mc_sweep(vbfm_ctx *c, bool is_w, int f)
 		} else {   // row-sharded: statistics of this shard, summed over shards, identical draws
 			HIPCHK(is_w ? vbk::mc_w_level(a, 1, c->s) : vbk::mc_v_level(a, 1, c->s));
 			if (c->row_comm())
-				NCCLCHK(ncclAllReduce(c->stats, c->stats, 2 * (size_t)a.nfeat, ncclDouble, ncclSum, c->comm, c->s));
+				allreduce_dev(c, c->stats, 2 * (size_t)a.nfeat, ncclDouble, ncclSum);
 			HIPCHK(is_w ? vbk::mc_w_level(a, 2, c->s) : vbk::mc_v_level(a, 2, c->s));
 		}
 		prof_end(c, p);
@@ -412,10 +413,10 @@ void scan_columns(vbfm_ctx *c)
 	HIPCHK(hipMemcpy(cp.data(), c->tr.col_ptr, ((size_t)nf + 1) * 8, hipMemcpyDeviceToHost));
 	m.col_nonempty.assign(nf, 0);
 	for (uint32_t j = 0; j < nf; j++) m.col_nonempty[j] = cp[j + 1] > cp[j];
-	if (c->comm && nf) {
+	if (c->multi() && nf) {
 		uint8_t *d = dalloc<uint8_t>(nf);
 		HIPCHK(hipMemcpyAsync(d, m.col_nonempty.data(), nf, hipMemcpyHostToDevice, c->s));
-		NCCLCHK(ncclAllReduce(d, d, nf, ncclUint8, ncclMax, c->comm, c->s));
+		allreduce_dev(c, d, nf, ncclUint8, ncclMax);
 		HIPCHK(hipMemcpyAsync(m.col_nonempty.data(), d, nf, hipMemcpyDeviceToHost, c->s));
 		sync(c);
 		dfree(d);

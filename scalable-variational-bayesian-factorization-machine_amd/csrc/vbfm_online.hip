@@ -897,7 +897,7 @@ int vbfm_online_init(vbfm_ctx *c, const vbfm_online_config *cfg)
 	if (!c || !cfg) return fail(c, "vbfm_online_init: null argument");
 	return guarded(c, [&] {
 		if (c->mc) throw std::string("an MCMC / ALS context cannot run the online VB learner");
-		if (c->comm || c->shard_mode == VBFM_SHARD_FEATURES)
+		if (c->multi() || c->shard_mode == VBFM_SHARD_FEATURES)
 			throw std::string("the online VB learner runs on one GPU (no communicator, no feature shards)");
 		if (!c->rows) throw std::string("no train data set (vbfm_set_train)");
 		if (!c->e_test) throw std::string("no test data set (vbfm_set_test)");

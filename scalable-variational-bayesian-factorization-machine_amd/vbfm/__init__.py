@@ -144,10 +144,14 @@ EXPORTS = ["vbfm_abi_version", "vbfm_last_error", "vbfm_create", "vbfm_destroy",
            "vbfm_step_w0", "vbfm_step_w", "vbfm_step_qcache", "vbfm_step_v", "vbfm_step_hyper",
            "vbfm_free_energy", "vbfm_get_rows", "vbfm_get_test_e", "vbfm_factor_sweep", "vbfm_set_profiling",
            "vbfm_set_layout", "vbfm_get_layout", "vbfm_set_shard_mode",
-           "vbfm_comm_unique_id", "vbfm_comm_init", "vbfm_load_data", "vbfm_free_host_data", "vbfm_save_data",
+           "vbfm_comm_unique_id", "vbfm_comm_init", "vbfm_comm_init_host", "vbfm_load_data", "vbfm_free_host_data", "vbfm_save_data",
            "vbfm_init_params_host", "vbfm_mcmc_init", "vbfm_mcmc_set_params", "vbfm_mcmc_get_params",
            "vbfm_mcmc_init_caches", "vbfm_mcmc_iterate", "vbfm_mcmc_get_test_pred", "vbfm_mcmc_factor_sweep",
            "vbfm_online_init", "vbfm_online_epoch", "vbfm_online_get_state"]
+
+# vbfm_exchange_fn: int fn(void *user, void *buf, uint64_t count, int32_t dtype, int32_t op)
+EXCHANGE_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_void_p, C.c_uint64, C.c_int32, C.c_int32)
+_X_DTYPES = {0: np.float64, 1: np.uint32, 2: np.uint8}
 
 _lib = None
 
@@ -193,6 +197,7 @@ def lib():
         L.vbfm_get_layout.argtypes = [V, C.POINTER(C.c_int32)]
         L.vbfm_comm_unique_id.argtypes = [C.POINTER(C.c_uint8)]
         L.vbfm_comm_init.argtypes = [V, C.c_int32, C.c_int32, C.POINTER(C.c_uint8)]
+        L.vbfm_comm_init_host.argtypes = [V, C.c_int32, C.c_int32, EXCHANGE_FN, V]
         L.vbfm_load_data.argtypes = [C.c_char_p, C.POINTER(HostData)]
         L.vbfm_free_host_data.argtypes = [C.POINTER(HostData)]
         L.vbfm_save_data.argtypes = [C.c_char_p, C.POINTER(HostData)]
@@ -513,6 +518,27 @@ class FMLearnVB:
     def comm_init(self, nranks, rank, uid):
         buf = (C.c_uint8 * 128).from_buffer_copy(uid)
         _check(lib().vbfm_comm_init(self._ctx, nranks, rank, buf), self._ctx)
+
+    def comm_init_host(self, nranks, rank, allreduce):
+        """Ranks exchange through the caller instead of RCCL (vbfm_comm_init_host): every
+        all-reduce of the path calls allreduce(array, op) with a numpy view of the staged host
+        buffer (float64 / uint32 / uint8), op "sum" or "max", to be reduced in place across the
+        ranks -- e.g. a torch.distributed gloo all_reduce, so that several ranks can share one
+        GPU in tests."""
+        def _fn(user, buf, count, dtype, op):
+            try:
+                dt = _X_DTYPES[dtype]
+                n = int(count)
+                arr = np.ctypeslib.as_array(C.cast(buf, C.POINTER(np.ctypeslib.as_ctypes_type(dt))), shape=(n,)) \
+                    if n else np.zeros(0, dt)
+                allreduce(arr, "max" if op == 1 else "sum")
+                return 0
+            except Exception:  # reported to the library as a failed exchange
+                import traceback
+                traceback.print_exc()
+                return 1
+        self._xfn = EXCHANGE_FN(_fn)          # kept alive as long as the context
+        _check(lib().vbfm_comm_init_host(self._ctx, nranks, rank, self._xfn, None), self._ctx)
 
     def close(self):
         if self._ctx:

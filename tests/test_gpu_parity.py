@@ -306,6 +306,49 @@ def test_layouts_agree():
     close(res["level"][3], res["column"][3], 1e-12)
 
 
+@pytest.mark.parametrize("split", ["0", "1"])
+@pytest.mark.parametrize("method", ["vb", "als"])
+def test_unit_x_store_bit_identical(method, split, monkeypatch):
+    """One-hot data (every x 1.0f, libfm's categorical case and the bench shape): the level
+    store keeps no x per entry and the deferred split an 8-B payload {next, previous}.
+    VBFM_LX=1 keeps the x array / 16-B payload: the results are bit for bit the same (x = 1
+    enters every product exactly), fused and split. VB also against the oracle."""
+    monkeypatch.setenv("VBFM_FORCE_SPLIT", split)
+    n, F, S, k = 20000, 6, 200, 4
+    rp, f, v, y = synth.generate(n, F, S, 13, 0)
+    rpt, ft, vt, yt = synth.generate(500, F, S, 14, 0)
+    assert np.all(v == 1.0)
+    D = F * S + 1
+    res = {}
+    for lx in ("0", "1"):
+        monkeypatch.setenv("VBFM_LX", lx)
+        if method == "vb":
+            g = vbfm.FMLearnVB(1, 1, k, D, min_target=float(y.min()), max_target=float(y.max()), layout="level")
+            g.init(5, 0.1)
+        else:
+            g = vbfm.FMLearnMCMC(1, 1, k, D, min_target=float(y.min()), max_target=float(y.max()), method="als",
+                                 layout="level")
+            g.init_device(5, 0.1)
+        g.set_data(vbfm.DataSubset.from_csr(rp, f, v, y, F * S), vbfm.DataSubset.from_csr(rpt, ft, vt, yt, F * S))
+        g.init_caches()
+        st = [g.iterate() for _ in range(3)]
+        assert g.layout() == "level"
+        p = g.get_params()
+        res[lx] = ([s.rmse if method == "vb" else s.rmse_all for s in st],
+                   np.asarray(p["mu_v"] if method == "vb" else p["v"]), g.rows()["e"])
+        g.close()
+    for a, b in zip(res["0"], res["1"]):
+        np.testing.assert_array_equal(np.asarray(a), np.asarray(b))
+    if method == "vb":
+        o = oc.VB(1, 1, k, D)
+        o.init_params(5, 0.1)
+        o.attach(oc.Data(csr=(n, rp, f, v, y)), oc.Data(csr=(500, rpt, ft, vt, yt)))
+        o.init_caches()
+        for it in range(3):
+            ro, _, _ = o.iterate()
+            assert abs(res["0"][0][it] - ro) <= REL * ro
+
+
 def test_level_layout_refused_when_levels_incomplete():
     """tiny has rows of different lengths: a level misses rows, the level layout cannot
     apply -- auto falls back to the column layout, an explicit request fails loudly."""
