@@ -102,22 +102,43 @@ struct McOp {
 // lanes then touch 16 distinct 16-B bank groups.
 DEVI uint32_t lslot(uint32_t i, uint32_t c) { return i * 4 + (c ^ ((i >> 2) & 3)); }
 
-template <int BLOCK>
+typedef double ntv2 __attribute__((ext_vector_type(2)));
+
+// m <= BLOCK*R records = at most 4R pieces per thread; recs holds BLOCK*R records. Every piece is loaded into registers
+// (straight-line, index clamped to the run) before the first LDS write, so a thread keeps 4R
+// reads in flight; a load/write loop waits on each read before issuing the next
+// (s_waitcnt vmcnt(0) per piece). NT: non-temporal loads (records read once: keep L2 for
+// gathered tables).
+template <int BLOCK, int R, bool NT = false>
 DEVI void stage_in(double2 *recs, const double2 *src, uint32_t m)
 {
-	for (uint32_t t = threadIdx.x; t < m * 4; t += BLOCK) recs[lslot(t >> 2, t & 3)] = src[t];
+	constexpr int K = 4 * R;
+	const uint32_t np = m * 4;
+	if (np == 0) return;
+	double2 v[K];
+#pragma unroll
+	for (int k = 0; k < K; ++k) {
+		const uint32_t t = min(threadIdx.x + k * BLOCK, np - 1);
+		if constexpr (NT) {
+			const ntv2 w = __builtin_nontemporal_load(reinterpret_cast<const ntv2 *>(src) + t);
+			v[k] = make_double2(w.x, w.y);
+		} else {
+			v[k] = src[t];
+		}
+	}
+	// unconditional: slots past the run (copies of its last piece) are never read, and a
+	// conditional write lets the compiler sink each load next to it
+#pragma unroll
+	for (int k = 0; k < K; ++k) {
+		const uint32_t t = threadIdx.x + k * BLOCK;
+		recs[lslot(t >> 2, t & 3)] = v[k];
+	}
 }
 
-// the same with non-temporal loads (records read once: keep L2 for gathered tables)
-typedef double ntv2 __attribute__((ext_vector_type(2)));
-template <int BLOCK>
+template <int BLOCK, int R>
 DEVI void stage_in_nt(double2 *recs, const double2 *src, uint32_t m)
 {
-	const ntv2 *p = reinterpret_cast<const ntv2 *>(src);
-	for (uint32_t t = threadIdx.x; t < m * 4; t += BLOCK) {
-		const ntv2 v = __builtin_nontemporal_load(p + t);
-		recs[lslot(t >> 2, t & 3)] = make_double2(v.x, v.y);
-	}
+	stage_in<BLOCK, R, true>(recs, src, m);
 }
 
 DEVI void lds_get(const double2 *recs, uint32_t i, Rec &v)
@@ -141,7 +162,7 @@ DEVI void lord_stats(double2 *recs, const RowRec *src, const float *lx, uint32_t
 	for (uint32_t base = 0; base < n; base += CAP) {
 		const uint32_t m = min(CAP, n - base);
 		if (base) __syncthreads();
-		stage_in<BLOCK>(recs, s + (size_t)base * 4, m);
+		stage_in<BLOCK, CAP / BLOCK>(recs, s + (size_t)base * 4, m);
 		__syncthreads();
 		for (uint32_t i = threadIdx.x; i < m; i += BLOCK) {
 			Rec v;
@@ -164,7 +185,7 @@ DEVI void lord_move(double2 *recs, uint32_t *dsts, const RowRec *src, const floa
 		const uint32_t m = min(CAP, n - base);
 		if (!resident) {
 			__syncthreads();
-			stage_in<BLOCK>(recs, s + (size_t)base * 4, m);
+			stage_in<BLOCK, CAP / BLOCK>(recs, s + (size_t)base * 4, m);
 			__syncthreads();
 		}
 		for (uint32_t i = threadIdx.x; i < m; i += BLOCK) {
@@ -266,7 +287,7 @@ __global__ __launch_bounds__(BLOCK) void k_level_lord(LevelArgs a)
 		float xr[R];
 		uint32_t nr[R];
 		res_prefetch<BLOCK, R>(lx, a.lnext + sb, n, xr, nr);
-		stage_in<BLOCK>(recs, reinterpret_cast<const double2 *>(src), n);
+		stage_in<BLOCK, R>(recs, reinterpret_cast<const double2 *>(src), n);
 		__syncthreads();
 		res_stats<BLOCK, R>(recs, n, xr, op, s1, s2);
 		block_sum2<BLOCK>(s1, s2, lds);
@@ -347,7 +368,7 @@ __global__ __launch_bounds__(BLOCK) void k_mc_level_lord(McArgs a)
 			float xr[R];
 			uint32_t nr[R];
 			res_prefetch<BLOCK, R>(lx, a.lnext + sb, n, xr, nr);
-			stage_in<BLOCK>(recs, reinterpret_cast<const double2 *>(src), n);
+			stage_in<BLOCK, R>(recs, reinterpret_cast<const double2 *>(src), n);
 			__syncthreads();
 			res_stats<BLOCK, R>(recs, n, xr, op, sm, ss);
 			block_sum2<BLOCK>(sm, ss, lds);
@@ -550,8 +571,8 @@ __global__ __launch_bounds__(BLOCK) void k_lord_defer(LevelArgs a)
 				if (pending) t[u] = a.tab[q[u].z];
 			}
 		}
-		if (nt) stage_in_nt<BLOCK>(recs, s + (size_t)base * 4, m);
-		else stage_in<BLOCK>(recs, s + (size_t)base * 4, m);
+		if (nt) stage_in_nt<BLOCK, R>(recs, s + (size_t)base * 4, m);
+		else stage_in<BLOCK, R>(recs, s + (size_t)base * 4, m);
 		__syncthreads();
 #pragma unroll
 		for (int u = 0; u < R; ++u) {
@@ -608,7 +629,7 @@ __global__ __launch_bounds__(256) void k_lord_defer_flush(LevelArgs a, uint32_t 
 	const uint32_t b = blockIdx.x * 256u;
 	const uint32_t m = min(256u, n - b);
 	double2 *r = reinterpret_cast<double2 *>(a.dst) + (size_t)b * 4;
-	stage_in_nt<256>(recs, r, m);
+	stage_in_nt<256, 1>(recs, r, m);
 	__syncthreads();
 	if (threadIdx.x < m) {
 		Rec v;
@@ -728,8 +749,8 @@ __global__ __launch_bounds__(BLOCK) void k_mc_lord_defer(McArgs a)
 				if (pending) t[u] = a.tab[q[u].z];
 			}
 		}
-		if (nt) stage_in_nt<BLOCK>(recs, s + (size_t)base * 4, m);
-		else stage_in<BLOCK>(recs, s + (size_t)base * 4, m);
+		if (nt) stage_in_nt<BLOCK, R>(recs, s + (size_t)base * 4, m);
+		else stage_in<BLOCK, R>(recs, s + (size_t)base * 4, m);
 		__syncthreads();
 #pragma unroll
 		for (int u = 0; u < R; ++u) {
@@ -780,7 +801,7 @@ __global__ __launch_bounds__(256) void k_mc_lord_defer_flush(McArgs a, uint32_t 
 	const uint32_t b = blockIdx.x * 256u;
 	const uint32_t m = min(256u, n - b);
 	double2 *r = reinterpret_cast<double2 *>(a.dst) + (size_t)b * 4;
-	stage_in_nt<256>(recs, r, m);
+	stage_in_nt<256, 1>(recs, r, m);
 	__syncthreads();
 	if (threadIdx.x < m) {
 		Rec v;
