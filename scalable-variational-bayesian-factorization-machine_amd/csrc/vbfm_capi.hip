@@ -568,12 +568,7 @@ void sweep_level(vbfm_ctx *c, uint32_t l, bool is_w, int f)
 			const bool carried = l == 0 && c->carry != 0 && !is_w;
 			a.pend_kind = carried ? (c->carry == 3 ? 2 : 1) : 0;
 			c->carry = 0;
-			{
-				// non-temporal record loads (default; VBFM_DEFER_NT=0: plain loads, 1.5 % slower at C4)
-				static const int defer_nt = [] { const char *e = getenv("VBFM_DEFER_NT"); return !(e && e[0] == '0'); }();
-				const bool pend = l > 0 || carried;
-				a.pending = (pend ? 1 : 0) | (pend && defer_nt ? 2 : 0);
-			}
+			a.pending = (l > 0 || carried) ? 1 : 0;   // the kernels stream the records non-temporally
 			a.first_prev = l == 1;
 			HIPCHK(vbk::lord_defer_level(a, is_w, c->s));
 			if (c->row_comm())

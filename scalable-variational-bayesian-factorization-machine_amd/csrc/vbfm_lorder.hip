@@ -104,20 +104,18 @@ DEVI uint32_t lslot(uint32_t i, uint32_t c) { return i * 4 + (c ^ ((i >> 2) & 3)
 
 typedef double ntv2 __attribute__((ext_vector_type(2)));
 
-// m <= BLOCK*R records = at most 4R pieces per thread; recs holds BLOCK*R records. Every piece is loaded into registers
-// (straight-line, index clamped to the run) before the first LDS write, so a thread keeps 4R
-// reads in flight; a load/write loop waits on each read before issuing the next
-// (s_waitcnt vmcnt(0) per piece). NT: non-temporal loads (records read once: keep L2 for
-// gathered tables).
-template <int BLOCK, int R, bool NT = false>
-DEVI void stage_in(double2 *recs, const double2 *src, uint32_t m)
+// m <= BLOCK*R records = at most 4R pieces per thread; recs holds BLOCK*R records. Every
+// piece is loaded into registers (straight-line, index clamped to the run) before the first
+// LDS write, so a thread keeps 4R reads in flight; a load/write loop waits on each read before
+// issuing the next (s_waitcnt vmcnt(0) per piece). stage_load / stage_store split the two
+// halves so that a kernel can issue dependent loads (the deferred posterior gathers) between
+// them. NT: non-temporal loads (records read once: keep L2 for gathered tables).
+template <int BLOCK, int R, bool NT>
+DEVI void stage_load(double2 (&v)[4 * R], const double2 *src, uint32_t m)
 {
-	constexpr int K = 4 * R;
-	const uint32_t np = m * 4;
-	if (np == 0) return;
-	double2 v[K];
+	const uint32_t np = max(m * 4, 1u);
 #pragma unroll
-	for (int k = 0; k < K; ++k) {
+	for (int k = 0; k < 4 * R; ++k) {
 		const uint32_t t = min(threadIdx.x + k * BLOCK, np - 1);
 		if constexpr (NT) {
 			const ntv2 w = __builtin_nontemporal_load(reinterpret_cast<const ntv2 *>(src) + t);
@@ -126,13 +124,27 @@ DEVI void stage_in(double2 *recs, const double2 *src, uint32_t m)
 			v[k] = src[t];
 		}
 	}
-	// unconditional: slots past the run (copies of its last piece) are never read, and a
-	// conditional write lets the compiler sink each load next to it
+}
+
+// unconditional: slots past the run (copies of its last piece) are never read, and a
+// conditional write lets the compiler sink each load next to it
+template <int BLOCK, int R>
+DEVI void stage_store(double2 *recs, const double2 (&v)[4 * R])
+{
 #pragma unroll
-	for (int k = 0; k < K; ++k) {
+	for (int k = 0; k < 4 * R; ++k) {
 		const uint32_t t = threadIdx.x + k * BLOCK;
 		recs[lslot(t >> 2, t & 3)] = v[k];
 	}
+}
+
+template <int BLOCK, int R, bool NT = false>
+DEVI void stage_in(double2 *recs, const double2 *src, uint32_t m)
+{
+	if (m == 0) return;
+	double2 v[4 * R];
+	stage_load<BLOCK, R, NT>(v, src, m);
+	stage_store<BLOCK, R>(recs, v);
 }
 
 template <int BLOCK, int R>
@@ -505,6 +517,16 @@ void launch_lord_move(const LevelArgs &a, hipStream_t s)
 // of the next factor's q-cache in its kernel, in the same per-row order as the fused kernel)
 // an entry's deferred payload {x, next position, previous-level feature, its x}: the 16-B
 // record, or the 8-B {next, previous} one when every x is 1
+template <bool PAY8, class A> DEVI uint4 pay_load(const A &a, uint64_t p)
+{
+	if constexpr (PAY8) {
+		const uint2 w = a.lpay2[p];
+		return make_uint4(0x3f800000u, w.x, w.y, 0x3f800000u);
+	} else {
+		return a.lpay[p];
+	}
+}
+
 template <class A> DEVI uint4 pay_at(const A &a, uint64_t p)
 {
 	if (a.lpay2) {
@@ -535,7 +557,7 @@ DEVI void add_next_q(Rec &v, float x, bool first, double2 nx)
 // PK: which level's correction is pending -- 0: the previous level of this sweep; at level 0 of
 // a v sweep the previous sweep's last level, left unflushed: 1 = v with the other q-cache slot
 // (the previous factor), 2 = w (the w sweep before factor 0)
-template <int BLOCK, int R, bool IS_W, int P, bool NEXT, int PK = 0>
+template <int BLOCK, int R, bool IS_W, int P, bool NEXT, int PK, bool PAY8>
 __global__ __launch_bounds__(BLOCK) void k_lord_defer(LevelArgs a)
 {
 	constexpr uint32_t CAP = BLOCK * R;
@@ -553,7 +575,7 @@ __global__ __launch_bounds__(BLOCK) void k_lord_defer(LevelArgs a)
 	op.mo = msj.x; op.so = msj.y;
 	const double2 nx = NEXT ? a.ms_next[(size_t)j * a.ms_stride_next] : make_double2(0.0, 0.0);
 	const bool first = a.first_level != 0;
-	const bool pending = (a.pending & 1) != 0, nt = (a.pending & 2) != 0;
+	const bool pending = (a.pending & 1) != 0;
 	double s1 = 0.0, s2 = 0.0;
 	for (uint32_t base = 0; base < n; base += CAP) {
 		const uint32_t m = min(CAP, n - base);
@@ -561,18 +583,22 @@ __global__ __launch_bounds__(BLOCK) void k_lord_defer(LevelArgs a)
 		// each entry's {x, next position, previous-level feature, its x} in one 16-B load; the
 		// posteriors of the records' previous-level features are gathered (L2 / MALL: one line
 		// each) while the run streams into LDS
+		// payloads, then the run's records, then the posteriors the payloads point at (the
+		// gathers wait for the payloads only), then the LDS writes: three round trips overlap
 		PostT t[R];
 		uint4 q[R];
 #pragma unroll
 		for (int u = 0; u < R; ++u) {
 			const uint32_t i = threadIdx.x + u * BLOCK;
-			if (i < m) {
-				q[u] = pay_at(a, sb + base + i);
-				if (pending) t[u] = a.tab[q[u].z];
-			}
+			q[u] = pay_load<PAY8>(a, sb + base + min(i, m - 1));
 		}
-		if (nt) stage_in_nt<BLOCK, R>(recs, s + (size_t)base * 4, m);
-		else stage_in<BLOCK, R>(recs, s + (size_t)base * 4, m);
+		double2 sv[4 * R];
+		stage_load<BLOCK, R, true>(sv, s + (size_t)base * 4, m);   // records read once: non-temporal
+		// unconditional (a.tab always holds a previous level's width; unused unless pending):
+		// a branch here lets the compiler sink half of each payload load after the records'
+#pragma unroll
+		for (int u = 0; u < R; ++u) t[u] = a.tab[q[u].z];
+		stage_store<BLOCK, R>(recs, sv);
 		__syncthreads();
 #pragma unroll
 		for (int u = 0; u < R; ++u) {
@@ -672,10 +698,17 @@ __global__ __launch_bounds__(256) void k_lord_prev_fill(const uint32_t *feats, c
 template <bool IS_W, int P, bool NEXT, int PK>
 void launch_defer_pk(const LevelArgs &a, hipStream_t s)
 {
-	if (a.avg_len <= 96) k_lord_defer<64, 2, IS_W, P, NEXT, PK><<<a.nfeat, 64, 0, s>>>(a);
-	else if (a.avg_len <= 320) k_lord_defer<256, 1, IS_W, P, NEXT, PK><<<a.nfeat, 256, 0, s>>>(a);
-	else if (a.avg_len <= 640) k_lord_defer<256, 2, IS_W, P, NEXT, PK><<<a.nfeat, 256, 0, s>>>(a);
-	else k_lord_defer<512, 2, IS_W, P, NEXT, PK><<<a.nfeat, 512, 0, s>>>(a);
+	if (a.lpay2) {   // every x 1: 8-B payloads
+		if (a.avg_len <= 96) k_lord_defer<64, 2, IS_W, P, NEXT, PK, true><<<a.nfeat, 64, 0, s>>>(a);
+		else if (a.avg_len <= 320) k_lord_defer<256, 1, IS_W, P, NEXT, PK, true><<<a.nfeat, 256, 0, s>>>(a);
+		else if (a.avg_len <= 640) k_lord_defer<256, 2, IS_W, P, NEXT, PK, true><<<a.nfeat, 256, 0, s>>>(a);
+		else k_lord_defer<512, 2, IS_W, P, NEXT, PK, true><<<a.nfeat, 512, 0, s>>>(a);
+		return;
+	}
+	if (a.avg_len <= 96) k_lord_defer<64, 2, IS_W, P, NEXT, PK, false><<<a.nfeat, 64, 0, s>>>(a);
+	else if (a.avg_len <= 320) k_lord_defer<256, 1, IS_W, P, NEXT, PK, false><<<a.nfeat, 256, 0, s>>>(a);
+	else if (a.avg_len <= 640) k_lord_defer<256, 2, IS_W, P, NEXT, PK, false><<<a.nfeat, 256, 0, s>>>(a);
+	else k_lord_defer<512, 2, IS_W, P, NEXT, PK, false><<<a.nfeat, 512, 0, s>>>(a);
 }
 
 template <bool IS_W, int P, bool NEXT>
@@ -718,7 +751,7 @@ DEVI void mc_add_next_q(Rec &r, float x, bool first, double vn)
 	q = first ? 0.0 + aq : q + aq;
 }
 
-template <int BLOCK, int R, bool IS_W, int P, bool NEXT>
+template <int BLOCK, int R, bool IS_W, int P, bool NEXT, bool PAY8>
 __global__ __launch_bounds__(BLOCK) void k_mc_lord_defer(McArgs a)
 {
 	constexpr uint32_t CAP = BLOCK * R;
@@ -734,23 +767,27 @@ __global__ __launch_bounds__(BLOCK) void k_mc_lord_defer(McArgs a)
 	op.vo = a.par[(size_t)j * a.stride].x;
 	const double vn = NEXT ? a.par_next[(size_t)j * a.next_stride].x : 0.0;
 	const bool first = a.first_level != 0;
-	const bool pending = (a.pending & 1) != 0, nt = (a.pending & 2) != 0;
+	const bool pending = (a.pending & 1) != 0;
 	double sm = 0.0, ss = 0.0;
 	for (uint32_t base = 0; base < n; base += CAP) {
 		const uint32_t m = min(CAP, n - base);
 		if (base) __syncthreads();
+		// payloads, then the run's records, then the posteriors the payloads point at (the
+		// gathers wait for the payloads only), then the LDS writes: three round trips overlap
 		PostT t[R];
 		uint4 q[R];
 #pragma unroll
 		for (int u = 0; u < R; ++u) {
 			const uint32_t i = threadIdx.x + u * BLOCK;
-			if (i < m) {
-				q[u] = pay_at(a, sb + base + i);
-				if (pending) t[u] = a.tab[q[u].z];
-			}
+			q[u] = pay_load<PAY8>(a, sb + base + min(i, m - 1));
 		}
-		if (nt) stage_in_nt<BLOCK, R>(recs, s + (size_t)base * 4, m);
-		else stage_in<BLOCK, R>(recs, s + (size_t)base * 4, m);
+		double2 sv[4 * R];
+		stage_load<BLOCK, R, true>(sv, s + (size_t)base * 4, m);   // records read once: non-temporal
+		// unconditional (a.tab always holds a previous level's width; unused unless pending):
+		// a branch here lets the compiler sink half of each payload load after the records'
+#pragma unroll
+		for (int u = 0; u < R; ++u) t[u] = a.tab[q[u].z];
+		stage_store<BLOCK, R>(recs, sv);
 		__syncthreads();
 #pragma unroll
 		for (int u = 0; u < R; ++u) {
@@ -817,10 +854,17 @@ __global__ __launch_bounds__(256) void k_mc_lord_defer_flush(McArgs a, uint32_t 
 template <bool IS_W, int P, bool NEXT>
 void launch_mc_defer(const McArgs &a, hipStream_t s)
 {
-	if (a.avg_len <= 96) k_mc_lord_defer<64, 2, IS_W, P, NEXT><<<a.nfeat, 64, 0, s>>>(a);
-	else if (a.avg_len <= 320) k_mc_lord_defer<256, 1, IS_W, P, NEXT><<<a.nfeat, 256, 0, s>>>(a);
-	else if (a.avg_len <= 640) k_mc_lord_defer<256, 2, IS_W, P, NEXT><<<a.nfeat, 256, 0, s>>>(a);
-	else k_mc_lord_defer<512, 2, IS_W, P, NEXT><<<a.nfeat, 512, 0, s>>>(a);
+	if (a.lpay2) {   // every x 1: 8-B payloads
+		if (a.avg_len <= 96) k_mc_lord_defer<64, 2, IS_W, P, NEXT, true><<<a.nfeat, 64, 0, s>>>(a);
+		else if (a.avg_len <= 320) k_mc_lord_defer<256, 1, IS_W, P, NEXT, true><<<a.nfeat, 256, 0, s>>>(a);
+		else if (a.avg_len <= 640) k_mc_lord_defer<256, 2, IS_W, P, NEXT, true><<<a.nfeat, 256, 0, s>>>(a);
+		else k_mc_lord_defer<512, 2, IS_W, P, NEXT, true><<<a.nfeat, 512, 0, s>>>(a);
+		return;
+	}
+	if (a.avg_len <= 96) k_mc_lord_defer<64, 2, IS_W, P, NEXT, false><<<a.nfeat, 64, 0, s>>>(a);
+	else if (a.avg_len <= 320) k_mc_lord_defer<256, 1, IS_W, P, NEXT, false><<<a.nfeat, 256, 0, s>>>(a);
+	else if (a.avg_len <= 640) k_mc_lord_defer<256, 2, IS_W, P, NEXT, false><<<a.nfeat, 256, 0, s>>>(a);
+	else k_mc_lord_defer<512, 2, IS_W, P, NEXT, false><<<a.nfeat, 512, 0, s>>>(a);
 }
 
 template <int BLOCK, int R, int MODE>
