@@ -4,7 +4,7 @@
 # --pmc passes over a k=4 run (per-launch bytes of the level kernel do not depend on k).
 cd "$GRAFT_REPO_ROOT" || exit 1
 export TMPDIR=/tmp
-out=gpurun_out/prof_final2
+out=gpurun_out/prof_final3
 mkdir -p $out
 echo "kt start $(date +%T)" >> $out/progress.txt
 timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $out/kt -o kt --output-format csv -- \
