@@ -59,12 +59,15 @@ __global__ __launch_bounds__(BLOCK) void k_v_level_fused(LevelArgs a)
 #pragma unroll
 	for (int u = 0; u < R; ++u) {
 		const uint32_t i = threadIdx.x + u * BLOCK;
-		row[u] = 0; xv[u] = 0.f;
-		if (i < n) { const uint2 ent = col[i]; row[u] = ent.x; xv[u] = ent_x(ent); }
+		// unconditional, index clamped (entries and records past the column are never used;
+		// an empty column reads row 0): a guarded load is sunk into its branch and waited on
+		// there, so the entries and then the records would arrive one after the other
+		const uint2 ent = n ? col[min(i, n - 1)] : make_uint2(0u, 0u);
+		row[u] = ent.x;
+		xv[u] = ent_x(ent);
 	}
 #pragma unroll
-	for (int u = 0; u < R; ++u)
-		if (threadIdx.x + u * BLOCK < n) load_rec(a.rows, row[u] & ROW_MASK, rec[u]);
+	for (int u = 0; u < R; ++u) load_rec(a.rows, row[u] & ROW_MASK, rec[u]);
 	double vm = 0.0, vs = 0.0;
 #pragma unroll
 	for (int u = 0; u < R; ++u)
@@ -186,12 +189,15 @@ __global__ __launch_bounds__(BLOCK) void k_w_level_fused(LevelArgs a)
 #pragma unroll
 	for (int u = 0; u < R; ++u) {
 		const uint32_t i = threadIdx.x + u * BLOCK;
-		row[u] = 0; xv[u] = 0.f;
-		if (i < n) { const uint2 ent = col[i]; row[u] = ent.x; xv[u] = ent_x(ent); }
+		// unconditional, index clamped (entries and records past the column are never used;
+		// an empty column reads row 0): a guarded load is sunk into its branch and waited on
+		// there, so the entries and then the records would arrive one after the other
+		const uint2 ent = n ? col[min(i, n - 1)] : make_uint2(0u, 0u);
+		row[u] = ent.x;
+		xv[u] = ent_x(ent);
 	}
 #pragma unroll
-	for (int u = 0; u < R; ++u)
-		if (threadIdx.x + u * BLOCK < n) load_rec(a.rows, row[u] & ROW_MASK, rec[u]);
+	for (int u = 0; u < R; ++u) load_rec(a.rows, row[u] & ROW_MASK, rec[u]);
 	double wm = 0.0, ws = 0.0;
 #pragma unroll
 	for (int u = 0; u < R; ++u)
