@@ -431,18 +431,34 @@ __global__ __launch_bounds__(256) void k_ov_lord(LevelArgs a)
 	const uint32_t c1 = min(c0 + 256 / G, a.nfeat);
 	const uint64_t wb = a.col_ptr[c0], we = a.col_ptr[c1];
 	const uint32_t m = (uint32_t)min<uint64_t>(we - wb, OV_CAP);
-	{
-		const double2 *s2 = reinterpret_cast<const double2 *>(a.src + (wb - a.lbase));
-		const uint32_t *nx2 = a.lnext + (wb - a.lbase);
-		for (uint32_t t = threadIdx.x; t < m * 4; t += 256) stage[ov_slot(t >> 2, t & 3)] = s2[t];
-		for (uint32_t t = threadIdx.x; t < m; t += 256) dsts[t] = nx2[t];
-	}
+	// the column's id and bounds first: the per-column loads that depend on them then wait
+	// for these only, not for the run's pieces issued in between
 	const uint32_t col_i = c0 + threadIdx.x / G;
 	const uint32_t lane = threadIdx.x % G;
 	const bool live = col_i < a.nfeat;
 	const uint32_t j = live ? a.feats[col_i] : 0u;
 	const uint64_t cb = live ? a.col_ptr[col_i] : 0u;
 	const uint32_t n = live ? (uint32_t)(a.col_ptr[col_i + 1] - cb) : 0u;
+	// the run's pieces into registers first, only as many rounds as the run needs (uniform
+	// bound), the per-column loads below overlap them, the LDS writes come last (a load/write
+	// loop waits on every read before issuing the next)
+	constexpr int KS = OV_CAP * 4 / 256, KD = OV_CAP / 256;
+	const uint32_t np = m * 4;
+	const uint32_t ks = (np + 255) / 256, kd = (m + 255) / 256;
+	double2 sv[KS];
+	uint32_t dv[KD];
+	const double2 *s2 = reinterpret_cast<const double2 *>(a.src + (wb - a.lbase));
+	const uint32_t *nx2 = a.lnext + (wb - a.lbase);
+#pragma unroll
+	for (int k = 0; k < KS; ++k) {
+		sv[k] = make_double2(0.0, 0.0);
+		if (k < (int)ks) sv[k] = s2[min(threadIdx.x + k * 256, np - 1)];
+	}
+#pragma unroll
+	for (int k = 0; k < KD; ++k) {
+		dv[k] = 0;
+		if (k < (int)kd) dv[k] = nx2[min(threadIdx.x + k * 256, m - 1)];
+	}
 	const uint32_t o0 = (uint32_t)(cb - wb);   // the column's first record in the run
 	const uint2 *col = a.csc + cb;
 	double2 msj = make_double2(0.0, 0.0), natj = make_double2(0.0, 0.0), nx = make_double2(0.0, 0.0);
@@ -458,6 +474,15 @@ __global__ __launch_bounds__(256) void k_ov_lord(LevelArgs a)
 		if (a.tcount) tc = a.tcount[j];
 		if constexpr (NEXT) nx = a.ms_next[(size_t)j * a.ms_stride_next];
 	}
+	// unconditional: slots past the run are never read, and a guarded write lets the compiler
+	// merge it with its load and wait there
+#pragma unroll
+	for (int k = 0; k < KS; ++k) {
+		const uint32_t t = threadIdx.x + k * 256;
+		stage[ov_slot(t >> 2, t & 3)] = sv[k];
+	}
+#pragma unroll
+	for (int k = 0; k < KD; ++k) dsts[threadIdx.x + k * 256] = dv[k];
 	__syncthreads();
 	auto get = [&](uint32_t i, Rec &r) {
 		const uint32_t o = o0 + i;
