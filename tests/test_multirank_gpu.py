@@ -57,8 +57,9 @@ def _data(kind):
         rpt, ft, vt, yt = synth.generate(1500, F, S, 22, 1)
         return (rp, f, v, y), (rpt, ft, vt, yt), F * S
     N, F, S = 16000, 6, 250
-    tr = synth.generate(N, F, S, 5, 1)
-    te = synth.generate(1500, F, S, 6, 1)
+    xmode = 0 if kind == "onehot" else 1   # onehot: every x 1 (no x array, 8-B deferred payloads)
+    tr = synth.generate(N, F, S, 5, xmode)
+    te = synth.generate(1500, F, S, 6, xmode)
     return tr, te, F * S
 
 
@@ -168,8 +169,8 @@ def _rel(a, b):
     return float(np.max(np.abs(a - b)) / max(np.max(np.abs(b)), 1e-300))
 
 
-@pytest.mark.parametrize("world,kind,layout", [(2, "field", "level"), (3, "field", "level"), (2, "field", "column"),
-                                               (2, "ragged", "auto")])
+@pytest.mark.parametrize("world,kind,layout", [(2, "field", "level"), (3, "field", "level"), (2, "onehot", "level"),
+                                               (2, "field", "column"), (2, "ragged", "auto")])
 def test_vb_row_shards_match_one_rank(world, kind, layout):
     """VB row shards (deferred split kernels on the level-ordered store, stats / correct on the
     column layout) vs the un-sharded data set: RMSE, free energy, alpha per iteration and the
@@ -186,12 +187,13 @@ def test_vb_row_shards_match_one_rank(world, kind, layout):
     assert _rel(s["mu_w"], r["mu_w"]) <= REL
 
 
-@pytest.mark.parametrize("method,layout", [("als", "level"), ("als", "column"), ("mcmc", "level")])
-def test_mcmc_row_shards_match_one_rank(method, layout):
+@pytest.mark.parametrize("method,layout,kind", [("als", "level", "field"), ("als", "level", "onehot"),
+                                              ("als", "column", "field"), ("mcmc", "level", "field")])
+def test_mcmc_row_shards_match_one_rank(method, layout, kind):
     """MCMC / ALS row shards with the device RNG streams (keyed by seed, iteration, factor and
     attribute, so every rank draws the same numbers) vs one rank: ALS is deterministic
     (1e-9); the Gibbs chain only sees the summation order of the statistics change (1e-7)."""
-    s, r = _launch(2, "field", method, layout)
+    s, r = _launch(2, kind, method, layout)
     assert s["layout"] == r["layout"] == layout
     tol = REL if method == "als" else 1e-7
     for a, b in zip(s["rmse"], r["rmse"]):
