@@ -174,12 +174,22 @@ DEVI void lord_stats(double2 *recs, const RowRec *src, const float *lx, uint32_t
 	for (uint32_t base = 0; base < n; base += CAP) {
 		const uint32_t m = min(CAP, n - base);
 		if (base) __syncthreads();
-		stage_in<BLOCK, CAP / BLOCK>(recs, s + (size_t)base * 4, m);
+		// this chunk's x in registers before its records stream in (a per-record load after
+		// the barrier would wait once per record)
+		constexpr int R = CAP / BLOCK;
+		float xr[R];
+#pragma unroll
+		for (int u = 0; u < R; ++u) xr[u] = lx ? lx[base + min(threadIdx.x + u * BLOCK, m - 1)] : 1.0f;
+		stage_in<BLOCK, R>(recs, s + (size_t)base * 4, m);
 		__syncthreads();
-		for (uint32_t i = threadIdx.x; i < m; i += BLOCK) {
-			Rec v;
-			lds_get(recs, i, v);
-			op.stat(v, lx ? lx[base + i] : 1.0f, s1, s2);
+#pragma unroll
+		for (int u = 0; u < R; ++u) {
+			const uint32_t i = threadIdx.x + u * BLOCK;
+			if (i < m) {
+				Rec v;
+				lds_get(recs, i, v);
+				op.stat(v, xr[u], s1, s2);
+			}
 		}
 	}
 }
@@ -195,17 +205,31 @@ DEVI void lord_move(double2 *recs, uint32_t *dsts, const RowRec *src, const floa
 	double2 *d = reinterpret_cast<double2 *>(dst);
 	for (uint32_t base = 0; base < n; base += CAP) {
 		const uint32_t m = min(CAP, n - base);
+		// x and next positions of the chunk in registers before its records stream in
+		constexpr int R = CAP / BLOCK;
+		float xr[R];
+		uint32_t nr[R];
+#pragma unroll
+		for (int u = 0; u < R; ++u) {
+			const uint32_t ic = base + min(threadIdx.x + u * BLOCK, m - 1);
+			nr[u] = nxt[ic];
+			xr[u] = lx ? lx[ic] : 1.0f;
+		}
 		if (!resident) {
 			__syncthreads();
-			stage_in<BLOCK, CAP / BLOCK>(recs, s + (size_t)base * 4, m);
+			stage_in<BLOCK, R>(recs, s + (size_t)base * 4, m);
 			__syncthreads();
 		}
-		for (uint32_t i = threadIdx.x; i < m; i += BLOCK) {
-			Rec v;
-			lds_get(recs, i, v);
-			op.apply(v, lx ? lx[base + i] : 1.0f, first);
-			lds_put(recs, i, v);
-			dsts[i] = nxt[base + i];
+#pragma unroll
+		for (int u = 0; u < R; ++u) {
+			const uint32_t i = threadIdx.x + u * BLOCK;
+			if (i < m) {
+				Rec v;
+				lds_get(recs, i, v);
+				op.apply(v, xr[u], first);
+				lds_put(recs, i, v);
+				dsts[i] = nr[u];
+			}
 		}
 		__syncthreads();
 		for (uint32_t t = threadIdx.x; t < m * 4; t += BLOCK) {
