@@ -128,6 +128,9 @@ void lord_release(vbfm_ctx *c, bool keep_rows)
 	sync(c);
 	dfree(c->rows_alt); dfree(c->lcp); dfree(c->lx); dfree(c->lnext); dfree(c->lrow0); dfree(c->lpos0);
 	dfree(c->lpidx); dfree(c->lpx); dfree(c->post_tab); dfree(c->lpay); dfree(c->lpay2);
+	dfree(c->long_segs); dfree(c->seg_part);
+	c->seg_ptr.clear();
+	c->long_min = 0;
 	c->lord = false;
 	c->rows_lorder = false;
 }
@@ -173,6 +176,39 @@ void build_lorder(vbfm_ctx *c, const std::vector<uint64_t> &cp, const std::vecto
 	}
 	c->lcp = dalloc<uint64_t>(lcp.size());
 	HIPCHK(hipMemcpyAsync(c->lcp, lcp.data(), lcp.size() * 8, hipMemcpyHostToDevice, c->s));
+	// long columns (skewed data): runs longer than SEG_MIN entries are cut into segments of
+	// SEG_LEN, one workgroup each, in the fused single-rank sweep (VBFM_LONG=0: one workgroup
+	// per column as for the rest)
+	{
+		constexpr uint32_t SEG_MIN = 8192, SEG_LEN = 4096;
+		const char *lg = getenv("VBFM_LONG");
+		const bool on = !(lg && lg[0] == '0');
+		std::vector<LongSeg> segs;
+		c->seg_ptr.assign((size_t)L + 1, 0);
+		uint32_t maxs = 0;
+		for (uint32_t l = 0; l < L; l++) {
+			c->seg_ptr[l] = (uint32_t)segs.size();
+			for (uint32_t i = c->level_ptr[l]; on && i < c->level_ptr[l + 1]; i++) {
+				const uint64_t len = lcp[i + 1] - lcp[i];
+				if (len <= SEG_MIN) continue;
+				// seg0: the column's first segment, counted from the level's first (blockIdx in lord_long)
+				const uint32_t ns = (uint32_t)((len + SEG_LEN - 1) / SEG_LEN), s0 = (uint32_t)segs.size() - c->seg_ptr[l];
+				for (uint32_t q = 0; q < ns; q++)
+					segs.push_back({i - c->level_ptr[l], q * SEG_LEN,
+					                (uint32_t)std::min<uint64_t>(SEG_LEN, len - (uint64_t)q * SEG_LEN), s0, ns});
+			}
+			maxs = std::max(maxs, (uint32_t)segs.size() - c->seg_ptr[l]);
+		}
+		c->seg_ptr[L] = (uint32_t)segs.size();
+		if (!segs.empty()) {
+			c->long_min = SEG_MIN;
+			c->long_segs = dalloc<LongSeg>(segs.size());
+			HIPCHK(hipMemcpyAsync(c->long_segs, segs.data(), segs.size() * sizeof(LongSeg), hipMemcpyHostToDevice,
+			                      c->s));
+			c->seg_part = dalloc<double2>(2 * (size_t)maxs);
+			sync(c);
+		}
+	}
 	// x of every entry, unless all are 1.0f (one-hot libfm data): the level kernels then
 	// read no x at all (VBFM_LX=1 keeps the array)
 	{
@@ -557,7 +593,14 @@ void sweep_level(vbfm_ctx *c, uint32_t l, bool is_w, int f)
 		a.dst = c->rows_alt;
 		a.first_level = l == 0;
 		if (!c->row_comm() && !c->force_split) {
+			if (c->long_min) {
+				a.long_min = c->long_min;
+				a.segs = c->long_segs + c->seg_ptr[l];
+				a.nsegs = c->seg_ptr[l + 1] - c->seg_ptr[l];
+				a.seg_part = c->seg_part;
+			}
 			HIPCHK(vbk::lord_level(a, is_w, c->s));
+			HIPCHK(vbk::lord_long(a, is_w, c->s));
 		} else if (c->deferred()) {
 			// deferred: level l-1's correction, level l's statistics and the move in one pass;
 			// level l's correction after the all-reduce, by level l+1 (or the flush)

@@ -145,6 +145,11 @@ struct vbfm_ctx {
 	uint4 *lpay = nullptr;         // [nnz] deferred split: {x, lnext, lpidx, lpx} of every entry in one
 	                               // 16-B load (lx / lnext / lpidx / lpx are freed once packed)
 	PostT *post_tab = nullptr;     // [max level width] posteriors of the last level swept
+	// long columns of the level store (fused single-rank sweep): segments of every level
+	uint32_t long_min = 0;         // columns longer than this are split (0: none)
+	std::vector<uint32_t> seg_ptr; // [L+1] each level's segments in long_segs
+	LongSeg *long_segs = nullptr;
+	double2 *seg_part = nullptr;   // [2 * max segments of a level]
 	// deferred split across sweeps (vbfm_iterate only): the last level's correction of a sweep is
 	// left to level 0 of the next one instead of a flush pass. carry: 0 none, 1 / 2 = v sweep of
 	// q-cache slot 0 / 1, 3 = w sweep

@@ -48,6 +48,12 @@ struct __attribute__((aligned(32))) PostT {   // 32 B: two entries per 64-B line
 };
 
 // per-level launch description for the v / w sweeps
+// a segment of a long column of one level (index of the column in the level's feature list,
+// first entry and length within the column's run, the column's first segment and count)
+struct LongSeg {
+	uint32_t col, start, len, seg0, nseg;
+};
+
 struct LevelArgs {
 	const uint64_t *col_ptr;
 	const uint2 *csc;
@@ -94,6 +100,13 @@ struct LevelArgs {
 	uint32_t *tcount;          // w: t_wj (+= batch entries, rho refreshed); v of factor 0: t_vj; else nullptr
 	int hyp_uniform;           // one attribute group: the prior is hyp0 (no per-column lookup)
 	double hyp0;
+	// long columns of the level-ordered store (fused single-rank VB sweep): columns longer than
+	// long_min are left by k_level_lord to segment workgroups (statistics partials, then a
+	// posterior from the partials and the move); 0: none
+	uint32_t long_min;
+	const LongSeg *segs;       // the level's segments
+	uint32_t nsegs;
+	double2 *seg_part;         // per segment: (sum1, sum2), then the column's old {mu, sigma}
 };
 
 // per-level launch description for the MCMC / ALS draws (vbfm_mcmc.hip); parameters are
@@ -153,6 +166,8 @@ hipError_t qcache(const uint64_t *row_ptr, const uint2 *csr, const double2 *ms_f
                   uint32_t n, int slot, const uint32_t *pos, hipStream_t s);
 // level-ordered row store (vbfm_lorder.hip): fused level, or split stats -> (all-reduce) -> move
 hipError_t lord_level(const LevelArgs &a, int is_w, hipStream_t s);
+// the long columns of a fused level (a.nsegs segments): statistics partials, then posterior + move
+hipError_t lord_long(const LevelArgs &a, int is_w, hipStream_t s);
 hipError_t lord_level_stats(const LevelArgs &a, int is_w, hipStream_t s);
 hipError_t lord_level_move(const LevelArgs &a, int is_w, hipStream_t s);
 // deferred form of the split (one pass over the records per level): previous level's

@@ -310,6 +310,7 @@ __global__ __launch_bounds__(BLOCK) void k_level_lord(LevelArgs a)
 	const uint32_t j = a.feats[blockIdx.x];
 	const uint64_t sb = a.lcp[blockIdx.x];
 	const uint32_t n = (uint32_t)(a.lcp[blockIdx.x + 1] - sb);
+	if (a.long_min && n > a.long_min) return;      // a long column: the segment kernels' (lord_long)
 	const RowRec *src = a.src + (sb - a.lbase);
 	const float *lx = a.lx ? a.lx + sb : nullptr;   // null: every x is 1 (lx not stored)
 	const double2 msj = a.ms[(size_t)j * a.ms_stride];
@@ -337,6 +338,61 @@ __global__ __launch_bounds__(BLOCK) void k_level_lord(LevelArgs a)
 	op.go = vb_post<IS_W>(s1, s2, hyp, a.alpha, op.mo, op.so, op.mu, op.sig, a.counters, threadIdx.x == 0);
 	if (threadIdx.x == 0) a.ms[(size_t)j * a.ms_stride] = make_double2(op.mu, op.sig);
 	lord_move<BLOCK, CAP>(recs, dsts, src, lx, a.lnext + sb, n, false, a.dst, a.first_level != 0, op);
+}
+
+// Long columns (skewed data: a popular item): one workgroup would stream the whole run while
+// the rest of the level is long done. Their runs are cut into segments, one workgroup each:
+// k_lord_long_stats writes each segment's statistics (and the column's parameters before the
+// level), k_lord_long_move sums the column's segment partials in segment order (every
+// workgroup of the column the same sum, so the same posterior), the column's first segment
+// writes the new parameters, and every segment corrects and moves its records. The column's
+// sum is taken in another order than one workgroup's (segments, then the tree): ~1e-16.
+constexpr uint32_t LONG_BLOCK = 512, LONG_CAP = 1024;
+
+template <bool IS_W, int P>
+__global__ __launch_bounds__(LONG_BLOCK) void k_lord_long_stats(LevelArgs a)
+{
+	__shared__ double2 recs[LONG_CAP * 4];
+	__shared__ double lds[2 * (LONG_BLOCK / 64)];
+	const LongSeg g = a.segs[blockIdx.x];
+	const uint32_t j = a.feats[g.col];
+	const uint64_t sb = a.lcp[g.col] + g.start;
+	const double2 msj = a.ms[(size_t)j * a.ms_stride];
+	VbOp<IS_W, P, false> op;
+	op.mo = msj.x; op.so = msj.y;
+	double s1 = 0.0, s2 = 0.0;
+	lord_stats<LONG_BLOCK, LONG_CAP>(recs, a.src + (sb - a.lbase), a.lx ? a.lx + sb : nullptr, g.len, op, s1, s2);
+	block_sum2<LONG_BLOCK>(s1, s2, lds);
+	if (threadIdx.x == 0) {
+		a.seg_part[2 * blockIdx.x] = make_double2(s1, s2);
+		a.seg_part[2 * blockIdx.x + 1] = msj;
+	}
+}
+
+template <bool IS_W, int P, bool NEXT>
+__global__ __launch_bounds__(LONG_BLOCK) void k_lord_long_move(LevelArgs a)
+{
+	__shared__ double2 recs[LONG_CAP * 4];
+	__shared__ uint32_t dsts[LONG_CAP];
+	const LongSeg g = a.segs[blockIdx.x];
+	const uint32_t j = a.feats[g.col];
+	const uint64_t sb = a.lcp[g.col] + g.start;
+	double s1 = 0.0, s2 = 0.0;
+	for (uint32_t q = 0; q < g.nseg; ++q) {
+		const double2 p = a.seg_part[2 * (g.seg0 + q)];
+		s1 += p.x;
+		s2 += p.y;
+	}
+	const double2 msj = a.seg_part[2 * g.seg0 + 1];   // before this level (the first segment rewrites ms)
+	VbOp<IS_W, P, NEXT> op;
+	op.mo = msj.x; op.so = msj.y;
+	op.nx = NEXT ? a.ms_next[(size_t)j * a.ms_stride_next] : make_double2(0.0, 0.0);
+	const double hyp = a.hyp[(size_t)a.attr_group[j] * a.hyp_stride];
+	const bool lead = threadIdx.x == 0 && blockIdx.x == g.seg0;
+	op.go = vb_post<IS_W>(s1, s2, hyp, a.alpha, op.mo, op.so, op.mu, op.sig, a.counters, lead);
+	if (lead) a.ms[(size_t)j * a.ms_stride] = make_double2(op.mu, op.sig);
+	lord_move<LONG_BLOCK, LONG_CAP>(recs, dsts, a.src + (sb - a.lbase), a.lx ? a.lx + sb : nullptr, a.lnext + sb, g.len,
+	                                false, a.dst, a.first_level != 0, op);
 }
 
 // split form (row-sharded multi-GPU): statistics of the local rows -> all-reduce -> move
@@ -967,6 +1023,26 @@ hipError_t lord_level(const LevelArgs &a, int is_w, hipStream_t s)
 	if (is_w) nx ? launch_lord<true, 0, true>(a, s) : launch_lord<true, 0, false>(a, s);
 	else if (a.slot == 0) nx ? launch_lord<false, 0, true>(a, s) : launch_lord<false, 0, false>(a, s);
 	else nx ? launch_lord<false, 1, true>(a, s) : launch_lord<false, 1, false>(a, s);
+	return hipGetLastError();
+}
+
+hipError_t lord_long(const LevelArgs &a, int is_w, hipStream_t s)
+{
+	if (a.nsegs == 0) return hipSuccess;
+	const bool nx = a.ms_next != nullptr;
+	if (is_w) k_lord_long_stats<true, 0><<<a.nsegs, LONG_BLOCK, 0, s>>>(a);
+	else if (a.slot == 0) k_lord_long_stats<false, 0><<<a.nsegs, LONG_BLOCK, 0, s>>>(a);
+	else k_lord_long_stats<false, 1><<<a.nsegs, LONG_BLOCK, 0, s>>>(a);
+	if (is_w) {
+		if (nx) k_lord_long_move<true, 0, true><<<a.nsegs, LONG_BLOCK, 0, s>>>(a);
+		else k_lord_long_move<true, 0, false><<<a.nsegs, LONG_BLOCK, 0, s>>>(a);
+	} else if (a.slot == 0) {
+		if (nx) k_lord_long_move<false, 0, true><<<a.nsegs, LONG_BLOCK, 0, s>>>(a);
+		else k_lord_long_move<false, 0, false><<<a.nsegs, LONG_BLOCK, 0, s>>>(a);
+	} else {
+		if (nx) k_lord_long_move<false, 1, true><<<a.nsegs, LONG_BLOCK, 0, s>>>(a);
+		else k_lord_long_move<false, 1, false><<<a.nsegs, LONG_BLOCK, 0, s>>>(a);
+	}
 	return hipGetLastError();
 }
 

@@ -349,6 +349,52 @@ def test_unit_x_store_bit_identical(method, split, monkeypatch):
             assert abs(res["0"][0][it] - ro) <= REL * ro
 
 
+@pytest.mark.parametrize("k1", [1, 0])
+def test_long_columns_split_into_segments(k1, monkeypatch):
+    """Skewed two-field data (a Zipf item field: the top items hold 10k-20k rows): on the level
+    store the columns longer than 8192 entries are swept by segment workgroups (statistics
+    partials, then posterior + move). Against the oracle (1e-9), against one workgroup per
+    column (VBFM_LONG=0) and against the column layout (summation order only, 1e-12)."""
+    n, U, I, k = 60000, 5000, 400, 4
+    rng = np.random.default_rng(11)
+    u = rng.integers(0, U, n).astype(np.uint32)
+    it = ((rng.zipf(1.4, n) - 1) % I).astype(np.uint32)
+    assert np.bincount(it).max() > 2 * 8192
+    f = np.empty(2 * n, np.uint32); f[0::2] = u; f[1::2] = U + it
+    v = (0.5 + rng.random(2 * n)).astype(np.float32)
+    y = rng.integers(1, 6, n).astype(np.float32)
+    rp = np.arange(0, 2 * n + 1, 2, dtype=np.uint64)
+    nt = 2000
+    D = U + I + 1
+    res = {}
+    for name, env in (("seg", {}), ("noseg", {"VBFM_LONG": "0"}), ("column", {"VBFM_LAYOUT": "column"})):
+        for kk in ("VBFM_LONG", "VBFM_LAYOUT"):
+            monkeypatch.delenv(kk, raising=False)
+        for kk, vv in env.items():
+            monkeypatch.setenv(kk, vv)
+        g = vbfm.FMLearnVB(1, k1, k, D, min_target=1.0, max_target=5.0)
+        g.init(5, 0.1)
+        g.set_data(vbfm.DataSubset.from_csr(rp, f, v, y, U + I),
+                   vbfm.DataSubset.from_csr(rp[:nt + 1], f[:2 * nt], v[:2 * nt], y[:nt], U + I))
+        g.init_caches()
+        st = [g.iterate() for _ in range(2)]
+        res[name] = ([s.rmse for s in st], [s.free_energy for s in st], g.get_params()["mu_v"], g.layout())
+        g.close()
+    assert res["seg"][3] == "level" and res["column"][3] == "column"
+    for other in ("noseg", "column"):
+        close(res["seg"][0], res[other][0], 1e-12)
+        close(res["seg"][1], res[other][1], 1e-12)
+        close(res["seg"][2], res[other][2], 1e-12)
+    o = oc.VB(1, k1, k, D)
+    o.init_params(5, 0.1)
+    o.attach(oc.Data(csr=(n, rp, f, v, y)), oc.Data(csr=(nt, rp[:nt + 1], f[:2 * nt], v[:2 * nt], y[:nt])))
+    o.init_caches()
+    for it_ in range(2):
+        ro, _, _ = o.iterate()
+        assert abs(res["seg"][0][it_] - ro) <= REL * ro
+    close(res["seg"][2], o.params()["mu_v"])
+
+
 def test_level_layout_refused_when_levels_incomplete():
     """tiny has rows of different lengths: a level misses rows, the level layout cannot
     apply -- auto falls back to the column layout, an explicit request fails loudly."""

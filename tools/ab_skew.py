@@ -33,11 +33,17 @@ print(json.dumps({"ms_launch": ms, "ms_iter": sum(s.ms_total for s in st) / 2, "
 
 def main():
     rounds = int(sys.argv[1])
-    variants = [a.split("=", 1) for a in sys.argv[2:]]
-    res = {l: [] for l, _ in variants}
+    variants = []
+    for a in sys.argv[2:]:
+        label, rest = a.split("=", 1)
+        parts = rest.split(":")
+        env = dict(kv.split("=") for kv in parts[1].split(",")) if len(parts) > 1 else {}
+        variants.append((label, parts[0], env))
+    res = {v[0]: [] for v in variants}
     for r in range(rounds):
-        for label, lib in variants:
+        for label, lib, env in variants:
             e = dict(os.environ)
+            e.update(env)
             e["VBFM_LIB"] = os.path.join(ROOT, lib)
             e["AB_PKG"] = os.path.join(ROOT, "tools", "ab_head") if "head" in lib else \
                 os.path.join(ROOT, "scalable-variational-bayesian-factorization-machine_amd")
