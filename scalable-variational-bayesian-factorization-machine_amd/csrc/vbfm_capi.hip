@@ -144,6 +144,42 @@ static int layout_request(const vbfm_ctx *c)
 	return c->layout_req;
 }
 
+// Long columns (skewed data): columns longer than SEG_MIN entries are cut into segments of
+// SEG_LEN, one workgroup each, in the fused single-rank sweep of either layout (lord_long /
+// col_long); columns listing a row twice stay sequential. VBFM_LONG=0: one workgroup per column.
+// lcp: prefix sums of the level features' column lengths (level_feats order).
+static void build_long_segs(vbfm_ctx *c, const std::vector<uint64_t> &lcp, const std::vector<uint8_t> &dup,
+                            const std::vector<uint32_t> &feats)
+{
+	constexpr uint32_t SEG_MIN = 8192, SEG_LEN = 4096;
+	const uint32_t L = nlevels(c);
+	const char *lg = getenv("VBFM_LONG");
+	const bool on = !(lg && lg[0] == '0');
+	std::vector<LongSeg> segs;
+	c->seg_ptr.assign((size_t)L + 1, 0);
+	uint32_t maxs = 0;
+	for (uint32_t l = 0; l < L; l++) {
+		c->seg_ptr[l] = (uint32_t)segs.size();
+		for (uint32_t i = c->level_ptr[l]; on && i < c->level_ptr[l + 1]; i++) {
+			const uint64_t len = lcp[i + 1] - lcp[i];
+			if (len <= SEG_MIN || dup[feats[i]]) continue;
+			// seg0: the column's first segment, counted from the level's first (blockIdx)
+			const uint32_t ns = (uint32_t)((len + SEG_LEN - 1) / SEG_LEN), s0 = (uint32_t)segs.size() - c->seg_ptr[l];
+			for (uint32_t q = 0; q < ns; q++)
+				segs.push_back({i - c->level_ptr[l], q * SEG_LEN,
+				                (uint32_t)std::min<uint64_t>(SEG_LEN, len - (uint64_t)q * SEG_LEN), s0, ns});
+		}
+		maxs = std::max(maxs, (uint32_t)segs.size() - c->seg_ptr[l]);
+	}
+	c->seg_ptr[L] = (uint32_t)segs.size();
+	if (segs.empty()) return;
+	c->long_min = SEG_MIN;
+	c->long_segs = dalloc<LongSeg>(segs.size());
+	HIPCHK(hipMemcpyAsync(c->long_segs, segs.data(), segs.size() * sizeof(LongSeg), hipMemcpyHostToDevice, c->s));
+	c->seg_part = dalloc<double2>(2 * (size_t)maxs);
+	sync(c);
+}
+
 // Level-ordered store of the train set when every level holds each row exactly once (no
 // repeated feature in a row): per level l, positions [l*n, (l+1)*n) list the level's
 // columns in ascending feature order, rows ascending within a column.
@@ -151,7 +187,7 @@ void build_lorder(vbfm_ctx *c, const std::vector<uint64_t> &cp, const std::vecto
 {
 	lord_release(c, true);
 	const int req = layout_request(c);
-	if (req == VBFM_LAYOUT_COLUMN || c->ov) return;   // the online learner sweeps mini-batch columns
+	if (c->ov) return;   // the online learner sweeps mini-batch columns
 	if (c->shard_mode == VBFM_SHARD_FEATURES) {
 		if (req == VBFM_LAYOUT_LEVEL) throw std::string("the level-ordered row layout does not combine with feature shards");
 		return;
@@ -163,6 +199,10 @@ void build_lorder(vbfm_ctx *c, const std::vector<uint64_t> &cp, const std::vecto
 	if (nf) HIPCHK(hipMemcpy(dup.data(), c->dup, nf, hipMemcpyDeviceToHost));
 	std::vector<uint64_t> lcp((size_t)nf + 1, 0);
 	for (uint32_t i = 0; i < nf; i++) lcp[i + 1] = lcp[i] + (cp[feats[i] + 1] - cp[feats[i]]);
+	if (req == VBFM_LAYOUT_COLUMN) {
+		build_long_segs(c, lcp, dup, feats);
+		return;
+	}
 	if (n == 0 || L == 0) why = "no train rows";
 	for (uint32_t l = 0; l < L && why.empty(); l++) {
 		if (lcp[c->level_ptr[l + 1]] - lcp[c->level_ptr[l]] != n)
@@ -172,43 +212,12 @@ void build_lorder(vbfm_ctx *c, const std::vector<uint64_t> &cp, const std::vecto
 	}
 	if (!why.empty()) {
 		if (req == VBFM_LAYOUT_LEVEL) throw std::string("level-ordered row layout not possible: ") + why;
+		build_long_segs(c, lcp, dup, feats);   // the column-gather layout
 		return;
 	}
 	c->lcp = dalloc<uint64_t>(lcp.size());
 	HIPCHK(hipMemcpyAsync(c->lcp, lcp.data(), lcp.size() * 8, hipMemcpyHostToDevice, c->s));
-	// long columns (skewed data): runs longer than SEG_MIN entries are cut into segments of
-	// SEG_LEN, one workgroup each, in the fused single-rank sweep (VBFM_LONG=0: one workgroup
-	// per column as for the rest)
-	{
-		constexpr uint32_t SEG_MIN = 8192, SEG_LEN = 4096;
-		const char *lg = getenv("VBFM_LONG");
-		const bool on = !(lg && lg[0] == '0');
-		std::vector<LongSeg> segs;
-		c->seg_ptr.assign((size_t)L + 1, 0);
-		uint32_t maxs = 0;
-		for (uint32_t l = 0; l < L; l++) {
-			c->seg_ptr[l] = (uint32_t)segs.size();
-			for (uint32_t i = c->level_ptr[l]; on && i < c->level_ptr[l + 1]; i++) {
-				const uint64_t len = lcp[i + 1] - lcp[i];
-				if (len <= SEG_MIN) continue;
-				// seg0: the column's first segment, counted from the level's first (blockIdx in lord_long)
-				const uint32_t ns = (uint32_t)((len + SEG_LEN - 1) / SEG_LEN), s0 = (uint32_t)segs.size() - c->seg_ptr[l];
-				for (uint32_t q = 0; q < ns; q++)
-					segs.push_back({i - c->level_ptr[l], q * SEG_LEN,
-					                (uint32_t)std::min<uint64_t>(SEG_LEN, len - (uint64_t)q * SEG_LEN), s0, ns});
-			}
-			maxs = std::max(maxs, (uint32_t)segs.size() - c->seg_ptr[l]);
-		}
-		c->seg_ptr[L] = (uint32_t)segs.size();
-		if (!segs.empty()) {
-			c->long_min = SEG_MIN;
-			c->long_segs = dalloc<LongSeg>(segs.size());
-			HIPCHK(hipMemcpyAsync(c->long_segs, segs.data(), segs.size() * sizeof(LongSeg), hipMemcpyHostToDevice,
-			                      c->s));
-			c->seg_part = dalloc<double2>(2 * (size_t)maxs);
-			sync(c);
-		}
-	}
+	build_long_segs(c, lcp, dup, feats);
 	// x of every entry, unless all are 1.0f (one-hot libfm data): the level kernels then
 	// read no x at all (VBFM_LX=1 keeps the array)
 	{
@@ -641,7 +650,14 @@ void sweep_level(vbfm_ctx *c, uint32_t l, bool is_w, int f)
 		return;
 	}
 	if (!c->row_comm() && !c->force_split) {
+		if (c->long_min) {
+			a.long_min = c->long_min;
+			a.segs = c->long_segs + c->seg_ptr[l];
+			a.nsegs = c->seg_ptr[l + 1] - c->seg_ptr[l];
+			a.seg_part = c->seg_part;
+		}
 		HIPCHK(is_w ? vbk::w_level_fused(a, c->s) : vbk::v_level_fused(a, c->s));
+		HIPCHK(vbk::col_long(a, is_w, c->s));
 		prof_end(c, p);
 		return;
 	}

@@ -168,6 +168,8 @@ hipError_t qcache(const uint64_t *row_ptr, const uint2 *csr, const double2 *ms_f
 hipError_t lord_level(const LevelArgs &a, int is_w, hipStream_t s);
 // the long columns of a fused level (a.nsegs segments): statistics partials, then posterior + move
 hipError_t lord_long(const LevelArgs &a, int is_w, hipStream_t s);
+// the same for the column-gather layout's fused sweep (vbfm_kernels.hip)
+hipError_t col_long(const LevelArgs &a, int is_w, hipStream_t s);
 hipError_t lord_level_stats(const LevelArgs &a, int is_w, hipStream_t s);
 hipError_t lord_level_move(const LevelArgs &a, int is_w, hipStream_t s);
 // deferred form of the split (one pass over the records per level): previous level's

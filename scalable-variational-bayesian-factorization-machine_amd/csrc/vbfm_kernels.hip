@@ -47,6 +47,7 @@ __global__ __launch_bounds__(BLOCK) void k_v_level_fused(LevelArgs a)
 	const uint32_t j = a.feats[blockIdx.x];
 	const uint64_t cb = a.col_ptr[j];
 	const uint32_t n = (uint32_t)(a.col_ptr[j + 1] - cb);
+	if (a.long_min && n > a.long_min && !a.dup[j]) return;   // segment kernels (col_long)
 	const uint2 *col = a.csc + cb;
 	const double2 msj = a.ms[(size_t)j * a.ms_stride];
 	const double mo = msj.x, so = msj.y;
@@ -101,6 +102,66 @@ __global__ __launch_bounds__(BLOCK) void k_v_level_fused(LevelArgs a)
 		Rec v;
 		load_rec(a.rows, ent.x & ROW_MASK, v);
 		v_apply<P, NEXT>(v, ent_x(ent), (ent.x & a.first_mask) != 0, go, mo, so, mu, sig, nx);
+		store_rec(a.rows, ent.x & ROW_MASK, v);
+	}
+}
+
+// Long columns on the column-gather layout (as lord_long on the level store): the fused
+// kernels skip columns longer than a.long_min (except columns listing a row twice, which stay
+// sequential); one workgroup per segment writes the segment's statistics and the column's
+// parameters before the level, then one workgroup per segment sums the column's partials in
+// segment order, computes the (identical) posterior and corrects its rows.
+template <bool IS_W, int P>
+__global__ __launch_bounds__(256) void k_col_long_stats(LevelArgs a)
+{
+	__shared__ double lds[2 * (256 / 64)];
+	const LongSeg g = a.segs[blockIdx.x];
+	const uint32_t j = a.feats[g.col];
+	const uint2 *col = a.csc + a.col_ptr[j] + g.start;
+	const double2 msj = a.ms[(size_t)j * a.ms_stride];
+	double s1 = 0.0, s2 = 0.0;
+	for (uint32_t i = threadIdx.x; i < g.len; i += 256) {
+		const uint2 ent = col[i];
+		Rec v;
+		load_rec(a.rows, ent.x & ROW_MASK, v);
+		if constexpr (IS_W) w_stat(ent_x(ent), E(v), msj.x, s1, s2);
+		else v_stat(ent_x(ent), E(v), Q<P>(v), TQ<P>(v), msj.x, msj.y, s1, s2);
+	}
+	block_sum2<256>(s1, s2, lds);
+	if (threadIdx.x == 0) {
+		a.seg_part[2 * blockIdx.x] = make_double2(s1, s2);
+		a.seg_part[2 * blockIdx.x + 1] = msj;
+	}
+}
+
+template <bool IS_W, int P, bool NEXT>
+__global__ __launch_bounds__(256) void k_col_long_correct(LevelArgs a)
+{
+	const LongSeg g = a.segs[blockIdx.x];
+	const uint32_t j = a.feats[g.col];
+	const uint2 *col = a.csc + a.col_ptr[j] + g.start;
+	double s1 = 0.0, s2 = 0.0;
+	for (uint32_t q = 0; q < g.nseg; ++q) {
+		const double2 p = a.seg_part[2 * (g.seg0 + q)];
+		s1 += p.x;
+		s2 += p.y;
+	}
+	const double2 msj = a.seg_part[2 * g.seg0 + 1];
+	const double mo = msj.x, so = msj.y;
+	const double2 nx = NEXT ? a.ms_next[(size_t)j * a.ms_stride_next] : make_double2(0.0, 0.0);
+	const double hyp = a.hyp[(size_t)a.attr_group[j] * a.hyp_stride];
+	const bool lead = threadIdx.x == 0 && blockIdx.x == g.seg0;
+	double mu, sig;
+	const bool go = IS_W ? w_post(s1, s2, hyp, a.alpha, mo, so, mu, sig, a.counters, lead)
+	                     : v_post(s1, s2, hyp, a.alpha, mo, so, mu, sig, a.counters, lead);
+	if (lead) a.ms[(size_t)j * a.ms_stride] = make_double2(mu, sig);
+	if (!go && !NEXT) return;
+	for (uint32_t i = threadIdx.x; i < g.len; i += 256) {
+		const uint2 ent = col[i];
+		Rec v;
+		load_rec(a.rows, ent.x & ROW_MASK, v);
+		if constexpr (IS_W) w_apply<NEXT>(v, ent_x(ent), (ent.x & a.first_mask) != 0, go, mo, so, mu, sig, nx);
+		else v_apply<P, NEXT>(v, ent_x(ent), (ent.x & a.first_mask) != 0, go, mo, so, mu, sig, nx);
 		store_rec(a.rows, ent.x & ROW_MASK, v);
 	}
 }
@@ -178,6 +239,7 @@ __global__ __launch_bounds__(BLOCK) void k_w_level_fused(LevelArgs a)
 	const uint32_t j = a.feats[blockIdx.x];
 	const uint64_t cb = a.col_ptr[j];
 	const uint32_t n = (uint32_t)(a.col_ptr[j + 1] - cb);
+	if (a.long_min && n > a.long_min && !a.dup[j]) return;   // segment kernels (col_long)
 	const uint2 *col = a.csc + cb;
 	const double2 msj = a.ms[(size_t)j * a.ms_stride];
 	const double mo = msj.x, so = msj.y;
@@ -1086,6 +1148,25 @@ hipError_t w_level_fused(const LevelArgs &a, hipStream_t s)
 {
 	if (a.nfeat == 0) return hipSuccess;
 	return a.ms_next ? launch_w_fused<true>(a, s) : launch_w_fused<false>(a, s);
+}
+hipError_t col_long(const LevelArgs &a, int is_w, hipStream_t s)
+{
+	if (a.nsegs == 0) return hipSuccess;
+	const bool nx = a.ms_next != nullptr;
+	if (is_w) {
+		k_col_long_stats<true, 0><<<a.nsegs, 256, 0, s>>>(a);
+		if (nx) k_col_long_correct<true, 0, true><<<a.nsegs, 256, 0, s>>>(a);
+		else k_col_long_correct<true, 0, false><<<a.nsegs, 256, 0, s>>>(a);
+	} else if (a.slot == 0) {
+		k_col_long_stats<false, 0><<<a.nsegs, 256, 0, s>>>(a);
+		if (nx) k_col_long_correct<false, 0, true><<<a.nsegs, 256, 0, s>>>(a);
+		else k_col_long_correct<false, 0, false><<<a.nsegs, 256, 0, s>>>(a);
+	} else {
+		k_col_long_stats<false, 1><<<a.nsegs, 256, 0, s>>>(a);
+		if (nx) k_col_long_correct<false, 1, true><<<a.nsegs, 256, 0, s>>>(a);
+		else k_col_long_correct<false, 1, false><<<a.nsegs, 256, 0, s>>>(a);
+	}
+	return hipGetLastError();
 }
 hipError_t v_level_stats(const LevelArgs &a, hipStream_t s)
 {

@@ -351,10 +351,10 @@ def test_unit_x_store_bit_identical(method, split, monkeypatch):
 
 @pytest.mark.parametrize("k1", [1, 0])
 def test_long_columns_split_into_segments(k1, monkeypatch):
-    """Skewed two-field data (a Zipf item field: the top items hold 10k-20k rows): on the level
-    store the columns longer than 8192 entries are swept by segment workgroups (statistics
-    partials, then posterior + move). Against the oracle (1e-9), against one workgroup per
-    column (VBFM_LONG=0) and against the column layout (summation order only, 1e-12)."""
+    """Skewed two-field data (a Zipf item field: the top items hold 10k-20k rows): columns
+    longer than 8192 entries are swept by segment workgroups (statistics partials, then the
+    posterior + move / correction) on both layouts. Against the oracle (1e-9) and against one
+    workgroup per column (VBFM_LONG=0) on either layout (summation order only, 1e-12)."""
     n, U, I, k = 60000, 5000, 400, 4
     rng = np.random.default_rng(11)
     u = rng.integers(0, U, n).astype(np.uint32)
@@ -367,7 +367,8 @@ def test_long_columns_split_into_segments(k1, monkeypatch):
     nt = 2000
     D = U + I + 1
     res = {}
-    for name, env in (("seg", {}), ("noseg", {"VBFM_LONG": "0"}), ("column", {"VBFM_LAYOUT": "column"})):
+    for name, env in (("seg", {}), ("noseg", {"VBFM_LONG": "0"}), ("column", {"VBFM_LAYOUT": "column"}),
+                      ("column_noseg", {"VBFM_LAYOUT": "column", "VBFM_LONG": "0"})):
         for kk in ("VBFM_LONG", "VBFM_LAYOUT"):
             monkeypatch.delenv(kk, raising=False)
         for kk, vv in env.items():
@@ -381,7 +382,7 @@ def test_long_columns_split_into_segments(k1, monkeypatch):
         res[name] = ([s.rmse for s in st], [s.free_energy for s in st], g.get_params()["mu_v"], g.layout())
         g.close()
     assert res["seg"][3] == "level" and res["column"][3] == "column"
-    for other in ("noseg", "column"):
+    for other in ("noseg", "column", "column_noseg"):
         close(res["seg"][0], res[other][0], 1e-12)
         close(res["seg"][1], res[other][1], 1e-12)
         close(res["seg"][2], res[other][2], 1e-12)
