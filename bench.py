@@ -4,13 +4,22 @@
 One step = one full VB iteration of fm_learn_vb_simultaneous (update_all: w0, w sweep,
 k factor sweeps, hyper-parameters, free energy; then test prediction + RMSE) on synthetic
 field-structured data resident in HBM. value = nnz_train * k * steps / wall time of the
-timed steps, summed over all ranks (row-sharded weak scaling: every rank owns its own
-rows; per dependency level the per-feature statistics are all-reduced over RCCL).
+timed steps for the WHOLE data set (all ranks), wall time = max over ranks.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c4|c3|c2|tiny]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c4|c3|c2|multihot|tiny]
+                    [--scaling strong|weak] [--shard rows|features]
 
 Default workload: BASELINE configs[3] / the metric's "k=100 100M rows": 1e8 rows x 40
-one-hot fields x 125000 ids (D = 5e6), nnz = 4e9, k = 100, on each GPU.
+one-hot fields x 125000 ids (D = 5e6), nnz = 4e9, k = 100.
+
+Multi-GPU: `--gpus N` with no WORLD_SIZE in the environment starts N rank processes itself
+(before this process touches a GPU), each with RANK / LOCAL_RANK / WORLD_SIZE / MASTER_*;
+under torchrun the ranks come from the environment and must equal --gpus. One process per
+GPU; the per-level statistics are all-reduced over RCCL (xGMI). --scaling strong (default):
+the data set is the config's rows in total, rank r generating rows [r N/P, (r+1) N/P) of it,
+so every N describes the same problem. --scaling weak: every rank owns the config's rows
+(rows [r N, (r+1) N) of one larger data set). Train, test and every shard share one planted
+model (tests/synth.py), so test RMSE falls as the model fits.
 """
 import argparse
 import json
@@ -89,6 +98,51 @@ def cpu_baseline(cfg, sample_rows, sample_factors, seed=1):
         subprocess.run(["rm", "-rf", tmp])
 
 
+def shard_plan(rows, world, rank, mode):
+    """This rank's slice of the data set: strong = `rows` in total split into contiguous
+    near-equal slices, weak = `rows` per rank, features = every rank all rows."""
+    if mode == "features" or world == 1:
+        return {"rows": rows, "row_offset": 0, "rows_total": rows}
+    if mode == "weak":
+        return {"rows": rows, "row_offset": rank * rows, "rows_total": rows * world}
+    lo, hi = rows * rank // world, rows * (rank + 1) // world
+    return {"rows": hi - lo, "row_offset": lo, "rows_total": rows}
+
+
+def spawn_ranks(n):
+    """Start n rank processes of this script (one per GPU) and wait for them. This process
+    never touches a GPU; each child gets the torchrun environment."""
+    import socket
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    codes = [p.wait() for p in procs]
+    bad = [c for c in codes if c != 0]
+    if bad:
+        log("bench.py: rank exit codes %s" % codes)
+    return bad[0] if bad else 0
+
+
+def loaded_libs(name):
+    """Distinct files named like `name` mapped into this process (one RCCL, not two)."""
+    paths = set()
+    try:
+        with open("/proc/self/maps") as fh:
+            for line in fh:
+                p = line.split()[-1]
+                if os.path.basename(p).startswith(name):
+                    paths.add(os.path.realpath(p))
+    except OSError:
+        pass
+    return sorted(paths)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -108,27 +162,44 @@ def main():
                          "scaling, Jacobi across shards)")
     ap.add_argument("--layout", default="auto", choices=["auto", "column", "level"],
                     help="row-cache layout of the sweeps (include/vbfm.h VBFM_LAYOUT_*)")
+    ap.add_argument("--scaling", default="strong", choices=["strong", "weak"],
+                    help="row shards: strong = the config's rows in total (default), weak = per rank")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="print each rank's launch and shard plan as JSON and exit (no GPU)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-rows", type=int, default=1_000_000)
-    ap.add_argument("--cpu-factors", type=int, default=8)
+    ap.add_argument("--cpu-rows", type=int, default=2_000_000)
+    ap.add_argument("--cpu-factors", type=int, default=2)
     args = ap.parse_args()
 
-    import numpy as np
-    import torch
-    import torch.distributed as dist
-    import vbfm
-
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(spawn_ranks(args.gpus))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit("bench.py: --gpus %d but WORLD_SIZE=%d" % (args.gpus, world))
     cfg = dict(CONFIGS[args.config])
     if args.rows:
         cfg["rows"] = args.rows
     if args.k:
         cfg["k"] = args.k
-    N, F, S, k = cfg["rows"], cfg["fields"], cfg["ids"], cfg["k"]
+    F, S, k = cfg["fields"], cfg["ids"], cfg["k"]
     D = F * S + 1
-    n_test = max(N // 100, 1000)
+    fshard = args.shard == "features"
+    plan = shard_plan(cfg["rows"], world, rank, "features" if fshard else args.scaling)
+    N, row0, n_total = plan["rows"], plan["row_offset"], plan["rows_total"]
+    tplan = shard_plan(max(cfg["rows"] // 100, 1000), world, rank, "features" if fshard else args.scaling)
+    n_test, trow0 = tplan["rows"], tplan["row_offset"]
+    if args.dry_run:
+        print(json.dumps({"rank": rank, "local_rank": local_rank, "world_size": world,
+                          "master": "%s:%s" % (os.environ.get("MASTER_ADDR"), os.environ.get("MASTER_PORT")),
+                          "train": plan, "test": tplan, "config": args.config, "k": k}), flush=True)
+        return
+
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+    import vbfm
 
     if world > 1:
         dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -148,7 +219,6 @@ def main():
                                layout=args.layout)
     else:
         fml = vbfm.FMLearnVB(1, 1, k, D, min_target=1.0, max_target=5.0, device=device, layout=args.layout)
-    fshard = args.shard == "features"
     if fshard:
         if mc:
             raise SystemExit("--shard features is a VB mode")
@@ -159,9 +229,10 @@ def main():
         fml.comm_init(world, rank, obj[0])
     if not online:
         fml.init_device(42)
-    dseed = 0 if fshard else rank          # feature shards: every rank holds the same rows
-    fml.synth(0, N, F, S, seed=1000 + dseed, xmode=0)
-    fml.synth(1, n_test, F, S, seed=500000 + dseed, xmode=0)
+    # one data set, one planted model (tests/synth.py): this rank's slice of the train and
+    # test rows; feature shards hold every row
+    fml.synth(0, N, F, S, seed=1000, xmode=0, row_offset=row0)
+    fml.synth(1, n_test, F, S, seed=500000, xmode=0, row_offset=trow0)
     if online:
         # the reference's initial draws generated on the device, the rand() stream continued
         # into the epoch shuffles (vbfm_online_init, VBFM_ONLINE_INIT_REPLAY)
@@ -176,8 +247,14 @@ def main():
     def rmse_of(st):
         return st.rmse_all if mc else st.rmse
 
+    n_ranks_seen, _, transport = fml.comm_info()
+    rccl_libs = loaded_libs("librccl")
+    if len(rccl_libs) > 1:
+        raise SystemExit("more than one RCCL loaded: %s" % rccl_libs)
+    rmse_trace = []
     for i in range(args.warmup):
         st = fml.iterate()
+        rmse_trace.append(rmse_of(st))
         log("warmup %d: %.1f ms rmse %.6f" % (i, st.ms_total, rmse_of(st)))
 
     def barrier():
@@ -191,6 +268,7 @@ def main():
     for i in range(args.steps):
         stats.append(fml.iterate())
         st = stats[-1]
+        rmse_trace.append(rmse_of(st))
         log("step %d: %.1f ms (v sweep %.1f, w %.1f, hyper %.1f, %s %.1f) rmse %.6f" % (
             i, st.ms_total, st.ms_v, st.ms_w, st.ms_hyper, "predict" if mc or online else "test",
             st.ms_predict if mc or online else st.ms_test, rmse_of(st)))
@@ -201,9 +279,9 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
-    nnz = N * F
-    units = 1 if fshard else world       # rows processed per step, in units of one rank's rows
-    value = units * nnz * k * args.steps / elapsed
+    nnz = N * F                          # this rank's train entries
+    nnz_total = n_total * F              # the whole data set's (all ranks)
+    value = nnz_total * k * args.steps / elapsed
     levels = stats[-1].num_levels
     # roofline of the dominant kernel (k_level_lord / k_v_level_fused, one launch per factor
     # and level). It does the whole factor sweep of its level (stats, posterior, correction
@@ -254,11 +332,13 @@ def main():
     result = {
         "metric": METRIC, "value": value, "unit": "nnz*k/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": elapsed * 1000.0 / args.steps, "higher_is_better": True,
-        "scaling": "strong" if fshard else "weak", "vs_baseline": None, "dtype": "f64",
-        "data": "synthetic field-structured one-hot libfm data generated in HBM (tests/synth.py spec), "
+        "scaling": "strong" if fshard else args.scaling, "vs_baseline": None, "dtype": "f64",
+        "data": "synthetic field-structured one-hot libfm data generated in HBM (tests/synth.py spec: "
+                "planted bias + rank-2 interaction shared by train, test and all shards), "
                 "device random init of mu (0.1*N(0,1))",
-        "config": {"workload": cfg["desc"], "rows_per_gpu": N, "fields": F, "ids_per_field": S,
-                   "features": F * S, "k": k, "nnz_per_gpu": nnz, "test_rows_per_gpu": n_test,
+        "config": {"workload": cfg["desc"], "rows_total": n_total, "rows_per_gpu": N, "fields": F,
+                   "ids_per_field": S, "features": F * S, "k": k, "nnz_total": nnz_total, "nnz_per_gpu": nnz,
+                   "test_rows_per_gpu": n_test,
                    "levels": levels, "method": args.method,
                    "step": ("one full %s iteration (draw_all + train/test re-prediction, device RNG streams)"
                             % args.method.upper()) if mc else
@@ -273,8 +353,10 @@ def main():
                      "kernel": kernel, "avg_launch_ms": avg_ms,
                      "launches": n_launch, "bytes_per_launch": bytes_per_launch},
         "factor_sweep_ms_per_step": sweep_ms,
-        "factor_sweep_nnz_k_per_s": units * nnz * k / (sweep_ms * 1e-3),
+        "factor_sweep_nnz_k_per_s": nnz_total * k / (sweep_ms * 1e-3),
         "test_rmse": rmse_of(stats[-1]),
+        "test_rmse_trace": [round(x, 9) for x in rmse_trace],
+        "n_ranks_seen": n_ranks_seen, "transport": transport, "rccl_libs": rccl_libs,
         "free_energy": None if mc else stats[-1].free_energy_last if online else stats[-1].free_energy,
         "phase_ms": {kk: getattr(stats[-1], kk) for kk in (
             ("ms_hyper", "ms_w", "ms_v", "ms_predict", "ms_total") if mc else

@@ -109,9 +109,13 @@ int vbfm_abi_version(void);
 int vbfm_set_train(vbfm_ctx *ctx, const vbfm_csc *train);
 int vbfm_set_test(vbfm_ctx *ctx, const vbfm_csc *test);
 /* Field-structured synthetic data generated directly in HBM (tests/synth.py defines it):
- * rows x n_fields one-hot fields of ids_per_field ids each. which: 0 = train, 1 = test. */
+ * rows x n_fields one-hot fields of ids_per_field ids each. which: 0 = train, 1 = test.
+ * seed draws the rows, model_seed the planted model (bias + rank-2 interaction) that the
+ * train set, the test set and every rank's shard share; the rows generated are rows
+ * [row_offset, row_offset + num_rows) of the one-rank data set (a row shard). */
 int vbfm_synth_generate(vbfm_ctx *ctx, int32_t which, uint32_t num_rows, uint32_t n_fields,
-                        uint32_t ids_per_field, uint64_t seed, int32_t xmode);
+                        uint32_t ids_per_field, uint64_t seed, int32_t xmode, uint64_t model_seed,
+                        uint64_t row_offset);
 /* Copy back the device copy of a data set (parity of the device transpose / generator). */
 int vbfm_get_csc(vbfm_ctx *ctx, int32_t which, uint64_t *col_ptr /*[nf+1]*/, vbfm_entry *col_ent /*[nnz]*/,
                  float *target /*[rows]*/);
@@ -194,6 +198,9 @@ int vbfm_comm_init(vbfm_ctx *ctx, int32_t nranks, int32_t rank, const uint8_t ui
 #define VBFM_X_MAX 1
 typedef int (*vbfm_exchange_fn)(void *user, void *buf, uint64_t count, int32_t dtype, int32_t op);
 int vbfm_comm_init_host(vbfm_ctx *ctx, int32_t nranks, int32_t rank, vbfm_exchange_fn fn, void *user);
+/* The communicator as RCCL reports it (ncclCommCount / ncclCommUserRank): transport 0 = none
+ * (one rank), 1 = RCCL, 2 = host exchange (nranks / rank as given to vbfm_comm_init_host). */
+int vbfm_comm_info(vbfm_ctx *ctx, int32_t *nranks, int32_t *rank, int32_t *transport);
 
 /* Partition of the VB sweep over ranks (set before vbfm_set_train).
  *   VBFM_SHARD_ROWS (default): the exact row-sharded mode above.

@@ -956,7 +956,8 @@ int vbfm_set_test(vbfm_ctx *c, const vbfm_csc *in)
 	});
 }
 
-int vbfm_synth_generate(vbfm_ctx *c, int32_t which, uint32_t n, uint32_t F, uint32_t S, uint64_t seed, int32_t xmode)
+int vbfm_synth_generate(vbfm_ctx *c, int32_t which, uint32_t n, uint32_t F, uint32_t S, uint64_t seed, int32_t xmode,
+                        uint64_t model_seed, uint64_t row_offset)
 {
 	if (!c) return fail(nullptr, "null context");
 	return guarded(c, [&] {
@@ -975,7 +976,7 @@ int vbfm_synth_generate(vbfm_ctx *c, int32_t which, uint32_t n, uint32_t F, uint
 		d.target = dalloc<float>(n);
 		d.col_ptr = dalloc<uint64_t>((size_t)d.nf + 1);
 		d.csc = dalloc<uint2>(d.nnz);
-		HIPCHK(vbk::synth_csr(n, F, S, seed, xmode, d.row_ptr, d.csr, d.target, c->s));
+		HIPCHK(vbk::synth_csr(n, F, S, seed, xmode, model_seed, row_offset, d.row_ptr, d.csr, d.target, c->s));
 		// col_ptr: feature histogram + exclusive scan (padded columns stay empty)
 		uint64_t *counts = dalloc<uint64_t>((size_t)d.nf + 1);
 		HIPCHK(hipMemsetAsync(counts, 0, ((size_t)d.nf + 1) * 8, c->s));
@@ -1390,6 +1391,27 @@ int vbfm_comm_init(vbfm_ctx *c, int32_t nranks, int32_t rank, const uint8_t uid[
 		NCCLCHK(ncclCommInitRank(&c->comm, nranks, id, rank));
 		c->nranks = nranks;
 		c->rank = rank;
+	});
+}
+
+int vbfm_comm_info(vbfm_ctx *c, int32_t *nranks, int32_t *rank, int32_t *transport)
+{
+	if (!c) return fail(nullptr, "null context");
+	return guarded(c, [&] {
+		int n = c->nranks, r = c->rank, t = 0;
+		if (c->comm) {          // ask RCCL itself, not the context's copy
+			NCCLCHK(ncclCommCount(c->comm, &n));
+			NCCLCHK(ncclCommUserRank(c->comm, &r));
+			t = 1;
+		} else if (c->xfn) {
+			t = 2;
+		} else {
+			n = 1;
+			r = 0;
+		}
+		if (nranks) *nranks = n;
+		if (rank) *rank = r;
+		if (transport) *transport = t;
 	});
 }
 

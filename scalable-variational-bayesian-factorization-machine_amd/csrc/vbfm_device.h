@@ -247,8 +247,8 @@ hipError_t fs_unpack(RowRec *rows, uint32_t n, const double *base, const double 
 hipError_t fs_params(double2 *ms, uint32_t stride, const uint32_t *feats, uint32_t nfeat, double2 *pbuf, int to_buf,
                      hipStream_t s);
 // synthetic generator (tests/synth.py is the specification)
-hipError_t synth_csr(uint32_t n, uint32_t F, uint32_t S, uint64_t seed, int xmode, uint64_t *row_ptr,
-                     uint2 *csr, float *target, hipStream_t s);
+hipError_t synth_csr(uint32_t n, uint32_t F, uint32_t S, uint64_t seed, int xmode, uint64_t model_seed,
+                     uint64_t row0, uint64_t *row_ptr, uint2 *csr, float *target, hipStream_t s);
 hipError_t synth_field_keys(const uint2 *csr, uint32_t n, uint32_t F, uint32_t S, uint32_t field,
                             uint32_t *keys, uint32_t *vals, hipStream_t s);
 hipError_t synth_field_scatter(const uint32_t *sorted_rows, const uint2 *csr, uint32_t n, uint32_t F,

@@ -934,30 +934,46 @@ DEVI uint64_t hstream(uint64_t seed, uint64_t stream, uint64_t i)
 	return splitmix64(seed * 0x9E3779B97F4A7C15ull + stream * 0xD1B54A32D192ED03ull + i);
 }
 
-__global__ void k_synth_entries(uint32_t n, uint32_t F, uint32_t S, uint64_t seed, int xmode, uint2 *csr)
+__global__ void k_synth_entries(uint32_t n, uint32_t F, uint32_t S, uint64_t seed, int xmode, uint64_t row0, uint2 *csr)
 {
 	const uint64_t idx = (uint64_t)blockIdx.x * 256u + threadIdx.x;
 	if (idx >= (uint64_t)n * F) return;
 	const uint32_t fld = (uint32_t)(idx % F);
-	const uint32_t feat = fld * S + (uint32_t)(hstream(seed, 1, idx) % S);
+	const uint64_t g = idx + row0 * F;      // entry index in the global (one-rank) data set
+	const uint32_t feat = fld * S + (uint32_t)(hstream(seed, 1, g) % S);
 	float x = 1.0f;
-	if (xmode) x = 0.5f + (float)(hstream(seed, 2, idx) >> 40) * 0x1p-24f;
+	if (xmode) x = 0.5f + (float)(hstream(seed, 2, g) >> 40) * 0x1p-24f;
 	csr[idx] = make_uint2(feat, __float_as_uint(x));
 }
 
-__global__ void k_synth_rows(uint32_t n, uint32_t F, uint64_t seed, const uint2 *csr, uint64_t *row_ptr, float *target)
+DEVI double synth_unit(uint64_t seed, uint64_t stream, uint64_t i)
+{
+	return (double)(hstream(seed, stream, i) >> 11) * 0x1p-53;
+}
+
+// planted model: bias b(j) and rank-2 factors p(j, .) from the model seed, summed in field
+// order with separate multiply and add (the file is built with -ffp-contract=off)
+__global__ void k_synth_rows(uint32_t n, uint32_t F, uint64_t seed, uint64_t model_seed, uint64_t row0, double bgain,
+                             double igain, const uint2 *csr, uint64_t *row_ptr, float *target)
 {
 	const uint32_t r = blockIdx.x * 256u + threadIdx.x;
 	if (r > n) return;
 	row_ptr[r] = (uint64_t)r * F;
 	if (r == n) return;
-	double s = 0.0;
+	double s = 0.0, s0 = 0.0, s1 = 0.0, q0 = 0.0, q1 = 0.0;
 	for (uint32_t f = 0; f < F; ++f) {
-		const uint32_t j = csr[(uint64_t)r * F + f].x;
-		s = s + ((double)(hstream(seed, 3, j) >> 11) * 0x1p-53 - 0.5);
+		const uint64_t j = csr[(uint64_t)r * F + f].x;
+		s = s + (synth_unit(model_seed, 3, j) - 0.5) * bgain;
+		const double a0 = synth_unit(model_seed, 5, 2 * j) - 0.5;
+		const double a1 = synth_unit(model_seed, 5, 2 * j + 1) - 0.5;
+		s0 = s0 + a0;
+		s1 = s1 + a1;
+		q0 = q0 + a0 * a0;
+		q1 = q1 + a1 * a1;
 	}
-	const double noise = (double)(hstream(seed, 4, r) >> 11) * 0x1p-53 - 0.5;
-	double y = rint(3.0 + s + 1.5 * noise);
+	const double t = 0.5 * (s0 * s0 - q0) + 0.5 * (s1 * s1 - q1);
+	const double noise = synth_unit(seed, 4, row0 + r) - 0.5;
+	double y = rint(((3.0 + s) + igain * t) + 1.5 * noise);
 	y = y < 1.0 ? 1.0 : (y > 5.0 ? 5.0 : y);
 	target[r] = (float)y;
 }
@@ -1380,12 +1396,15 @@ hipError_t fs_params(double2 *ms, uint32_t stride, const uint32_t *feats, uint32
 	return hipGetLastError();
 }
 
-hipError_t synth_csr(uint32_t n, uint32_t F, uint32_t S, uint64_t seed, int xmode, uint64_t *row_ptr, uint2 *csr,
-                     float *target, hipStream_t s)
+hipError_t synth_csr(uint32_t n, uint32_t F, uint32_t S, uint64_t seed, int xmode, uint64_t model_seed, uint64_t row0,
+                     uint64_t *row_ptr, uint2 *csr, float *target, hipStream_t s)
 {
 	const uint64_t nnz = (uint64_t)n * F;
-	if (nnz) k_synth_entries<<<grid_for(nnz), 256, 0, s>>>(n, F, S, seed, xmode, csr);
-	k_synth_rows<<<grid_for((uint64_t)n + 1), 256, 0, s>>>(n, F, seed, csr, row_ptr, target);
+	const double bgain = sqrt(12.0 / (double)F);
+	const double igain = F >= 2 ? sqrt(72.0 / ((double)F * (double)(F - 1) / 2.0)) : 0.0;
+	if (nnz) k_synth_entries<<<grid_for(nnz), 256, 0, s>>>(n, F, S, seed, xmode, row0, csr);
+	k_synth_rows<<<grid_for((uint64_t)n + 1), 256, 0, s>>>(n, F, seed, model_seed, row0, bgain, igain, csr, row_ptr,
+	                                                      target);
 	return hipGetLastError();
 }
 

@@ -31,6 +31,7 @@ P_u32, P_u64, P_f32, P_f64, P_u8 = (C.POINTER(C.c_uint32), C.POINTER(C.c_uint64)
 
 
 LAYOUTS = {"auto": 0, "column": 1, "level": 2}   # VBFM_LAYOUT_* (include/vbfm.h)
+SYNTH_MODEL_SEED = 7   # tests/synth.py MODEL_SEED: the planted model shared by train, test and all shards
 
 
 class VbfmError(RuntimeError):
@@ -144,7 +145,7 @@ EXPORTS = ["vbfm_abi_version", "vbfm_last_error", "vbfm_create", "vbfm_destroy",
            "vbfm_step_w0", "vbfm_step_w", "vbfm_step_qcache", "vbfm_step_v", "vbfm_step_hyper",
            "vbfm_free_energy", "vbfm_get_rows", "vbfm_get_test_e", "vbfm_factor_sweep", "vbfm_set_profiling",
            "vbfm_set_layout", "vbfm_get_layout", "vbfm_set_shard_mode",
-           "vbfm_comm_unique_id", "vbfm_comm_init", "vbfm_comm_init_host", "vbfm_load_data", "vbfm_free_host_data", "vbfm_save_data",
+           "vbfm_comm_unique_id", "vbfm_comm_init", "vbfm_comm_init_host", "vbfm_comm_info", "vbfm_load_data", "vbfm_free_host_data", "vbfm_save_data",
            "vbfm_init_params_host", "vbfm_mcmc_init", "vbfm_mcmc_set_params", "vbfm_mcmc_get_params",
            "vbfm_mcmc_init_caches", "vbfm_mcmc_iterate", "vbfm_mcmc_get_test_pred", "vbfm_mcmc_factor_sweep",
            "vbfm_online_init", "vbfm_online_epoch", "vbfm_online_get_state"]
@@ -171,7 +172,8 @@ def lib():
         L.vbfm_destroy.restype = None
         L.vbfm_set_train.argtypes = [V, C.POINTER(Csc)]
         L.vbfm_set_test.argtypes = [V, C.POINTER(Csc)]
-        L.vbfm_synth_generate.argtypes = [V, C.c_int32, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint64, C.c_int32]
+        L.vbfm_synth_generate.argtypes = [V, C.c_int32, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint64, C.c_int32,
+                                          C.c_uint64, C.c_uint64]
         L.vbfm_get_csc.argtypes = [V, C.c_int32, P_u64, V, P_f32]
         L.vbfm_get_shape.argtypes = [V, C.c_int32, P_u32, P_u32, P_u64]
         L.vbfm_get_levels.argtypes = [V, P_u32, P_u32]
@@ -198,6 +200,7 @@ def lib():
         L.vbfm_comm_unique_id.argtypes = [C.POINTER(C.c_uint8)]
         L.vbfm_comm_init.argtypes = [V, C.c_int32, C.c_int32, C.POINTER(C.c_uint8)]
         L.vbfm_comm_init_host.argtypes = [V, C.c_int32, C.c_int32, EXCHANGE_FN, V]
+        L.vbfm_comm_info.argtypes = [V, C.POINTER(C.c_int32), C.POINTER(C.c_int32), C.POINTER(C.c_int32)]
         L.vbfm_load_data.argtypes = [C.c_char_p, C.POINTER(HostData)]
         L.vbfm_free_host_data.argtypes = [C.POINTER(HostData)]
         L.vbfm_save_data.argtypes = [C.c_char_p, C.POINTER(HostData)]
@@ -409,9 +412,12 @@ class FMLearnVB:
         _check(lib().vbfm_set_test(self._ctx, C.byref(self._test_csc)), self._ctx)
         self.n_train, self.n_test = train.num_cases, test.num_cases
 
-    def synth(self, which, num_rows, n_fields, ids_per_field, seed, xmode=0):
-        _check(lib().vbfm_synth_generate(self._ctx, which, num_rows, n_fields, ids_per_field, seed, xmode),
-               self._ctx)
+    def synth(self, which, num_rows, n_fields, ids_per_field, seed, xmode=0, model_seed=SYNTH_MODEL_SEED,
+              row_offset=0):
+        """tests/synth.py's generator on the device: seed draws the rows, model_seed the
+        planted model; rows [row_offset, row_offset + num_rows) of the one-rank data set."""
+        _check(lib().vbfm_synth_generate(self._ctx, which, num_rows, n_fields, ids_per_field, seed, xmode,
+                                         model_seed, row_offset), self._ctx)
         if which == 0:
             self.n_train = num_rows
         else:
@@ -539,6 +545,12 @@ class FMLearnVB:
                 return 1
         self._xfn = EXCHANGE_FN(_fn)          # kept alive as long as the context
         _check(lib().vbfm_comm_init_host(self._ctx, nranks, rank, self._xfn, None), self._ctx)
+
+    def comm_info(self):
+        """(nranks, rank, transport) as the communicator reports them (vbfm_comm_info)."""
+        n, r, t = C.c_int32(), C.c_int32(), C.c_int32()
+        _check(lib().vbfm_comm_info(self._ctx, C.byref(n), C.byref(r), C.byref(t)), self._ctx)
+        return n.value, r.value, {0: "none", 1: "rccl", 2: "host"}[t.value]
 
     def close(self):
         if self._ctx:

@@ -1,17 +1,29 @@
 """Field-structured synthetic libfm data, numpy version.
 
 The same generator is implemented on the device by the product library
-(`vbfm_synth_*` in csrc/vbfm_synth.hip) so that bench-scale data (10^8 rows) can be
+(`vbfm_synth_generate`, csrc/vbfm_kernels.hip k_synth_*) so that bench-scale data (10^8 rows) can be
 generated in HBM; the definition below is the specification both follow:
 
-  h(stream, i)   = splitmix64(seed * K1 + stream * K2 + i)           (uint64, wrapping)
-  feature(r, f)  = f * S + h(1, r * F + f) % S                       (one id per field)
-  x(r, f)        = 1.0f                              if xmode == 0
-                 = 0.5f + (h(2, r * F + f) >> 40) * 2^-24 (fp32)     if xmode == 1
-  b(j)           = ((h(3, j) >> 11) * 2^-53 - 0.5)                  (planted per-id bias)
-  y(r)           = clamp(rint(3 + sum_f b(feature(r, f)) + 1.5 * ((h(4, r) >> 11) * 2^-53 - 0.5)), 1, 5)
+Two seeds: the ROW seed draws the rows (ids, x, noise); the MODEL seed (shared by the
+train and test sets, and by every rank's shard) draws the planted model, so a model fitted
+on train predicts test. R = row_offset + r is the global row id, so a rank generating rows
+[R0, R0 + n) of a data set produces exactly that slice of the one-rank data set.
 
-Rows list their features in field order, i.e. in ascending feature id.
+  h_s(stream, i) = splitmix64(s * K1 + stream * K2 + i)              (uint64, wrapping)
+  u_s(stream, i) = (h_s(stream, i) >> 11) * 2^-53                    (fp64 in [0, 1))
+  feature(R, f)  = f * S + h_row(1, R * F + f) % S                   (one id per field)
+  x(R, f)        = 1.0f                                  if xmode == 0
+                 = 0.5f + (h_row(2, R * F + f) >> 40) * 2^-24 (fp32) if xmode == 1
+  b(j)           = (u_model(3, j) - 0.5) * c,  c = sqrt(12 / F)      (planted per-id bias,
+                                                                      unit variance summed)
+  p(j, d)        = u_model(5, 2 j + d) - 0.5, d = 0, 1               (planted rank-2 factors)
+  s    = sum_f b(j_f);  s_d = sum_f p(j_f, d);  q_d = sum_f p(j_f, d)^2   (field order)
+  t    = 0.5 * (s_0 * s_0 - q_0) + 0.5 * (s_1 * s_1 - q_1)           (= sum_{f<f'} <p_f, p_f'>)
+  g    = sqrt(72 / (F (F - 1) / 2))  (F >= 2; 0 for F = 1: unit-variance interaction)
+  y(R) = clamp(rint(((3 + s) + g * t) + 1.5 * (u_row(4, R) - 0.5)), 1, 5)
+
+All fp64 operations in the order written, no fused multiply-add. Rows list their features
+in field order, i.e. in ascending feature id.
 """
 import numpy as np
 
@@ -36,10 +48,25 @@ def h(seed, stream, i):
         return splitmix64(base + np.asarray(i, dtype=np.uint64))
 
 
-def generate(n_rows, n_fields, ids_per_field, seed, xmode=0):
+MODEL_SEED = 7      # the planted model every data set shares unless a test asks otherwise
+
+
+def _u(seed, stream, i):
+    return (h(seed, stream, i) >> np.uint64(11)).astype(np.float64) * 2.0 ** -53
+
+
+def bias_gain(F):
+    return float(np.sqrt(12.0 / F))
+
+
+def interaction_gain(F):
+    return float(np.sqrt(72.0 / (F * (F - 1) / 2.0))) if F >= 2 else 0.0
+
+
+def generate(n_rows, n_fields, ids_per_field, seed, xmode=0, model_seed=MODEL_SEED, row_offset=0):
     """Return (row_ptr uint64[N+1], feat uint32[N*F], val float32[N*F], y float32[N])."""
     N, F, S = int(n_rows), int(n_fields), int(ids_per_field)
-    idx = np.arange(N * F, dtype=np.uint64)
+    idx = np.arange(N * F, dtype=np.uint64) + np.uint64(int(row_offset) * F)
     fld = (idx % np.uint64(F)).astype(np.uint64)
     feat = (fld * np.uint64(S) + h(seed, 1, idx) % np.uint64(S)).astype(np.uint32)
     if xmode:
@@ -48,13 +75,24 @@ def generate(n_rows, n_fields, ids_per_field, seed, xmode=0):
     else:
         val = np.ones(N * F, dtype=np.float32)
     D = F * S
-    b = (h(seed, 3, np.arange(D, dtype=np.uint64)) >> np.uint64(11)).astype(np.float64) * 2.0 ** -53 - 0.5
+    jd = np.arange(D, dtype=np.uint64)
+    b = (_u(model_seed, 3, jd) - 0.5) * bias_gain(F)
+    p0 = _u(model_seed, 5, 2 * jd) - 0.5
+    p1 = _u(model_seed, 5, 2 * jd + np.uint64(1)) - 0.5
     s = np.zeros(N, dtype=np.float64)
+    s0, s1, q0, q1 = (np.zeros(N, dtype=np.float64) for _ in range(4))
     fe = feat.reshape(N, F)
     for f in range(F):            # summed in field order (the device generator does the same)
-        s = s + b[fe[:, f]]
-    noise = (h(seed, 4, np.arange(N, dtype=np.uint64)) >> np.uint64(11)).astype(np.float64) * 2.0 ** -53 - 0.5
-    y = np.clip(np.rint(3.0 + s + 1.5 * noise), 1.0, 5.0).astype(np.float32)
+        j = fe[:, f]
+        s = s + b[j]
+        a0, a1 = p0[j], p1[j]
+        s0 = s0 + a0
+        s1 = s1 + a1
+        q0 = q0 + a0 * a0
+        q1 = q1 + a1 * a1
+    t = 0.5 * (s0 * s0 - q0) + 0.5 * (s1 * s1 - q1)
+    noise = _u(seed, 4, np.arange(N, dtype=np.uint64) + np.uint64(int(row_offset))) - 0.5
+    y = np.clip(np.rint(((3.0 + s) + interaction_gain(F) * t) + 1.5 * noise), 1.0, 5.0).astype(np.float32)
     row_ptr = np.arange(N + 1, dtype=np.uint64) * np.uint64(F)
     return row_ptr, feat, val, y
 

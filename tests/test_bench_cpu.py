@@ -1,0 +1,88 @@
+"""bench.py's launch contract and its synthetic data (no GPU).
+
+* `--gpus N` without WORLD_SIZE starts N rank processes with the torchrun environment;
+* strong scaling slices the config's rows into contiguous shards that cover it exactly;
+* every shard and the test set come from one planted model, so a fitted model predicts the
+  test set better than the constant predictor (tests/synth.py; the oracle is the learner).
+"""
+import json
+import os
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+import oracle_ctypes as oc
+import synth
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+BENCH = os.path.join(ROOT, "bench.py")
+
+
+def _dry(args, env_extra=None):
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env.update(env_extra or {})
+    out = subprocess.run([sys.executable, BENCH, "--dry-run"] + args, env=env, capture_output=True, text=True,
+                         timeout=120)
+    return out
+
+
+@pytest.mark.parametrize("n,scaling", [(2, "strong"), (4, "strong"), (3, "weak")])
+def test_gpus_flag_spawns_configured_ranks(n, scaling):
+    out = _dry(["--gpus", str(n), "--scaling", scaling])
+    assert out.returncode == 0, out.stderr
+    plans = sorted((json.loads(l) for l in out.stdout.splitlines() if l.startswith("{")), key=lambda p: p["rank"])
+    assert [p["rank"] for p in plans] == list(range(n))
+    assert all(p["world_size"] == n and p["local_rank"] == p["rank"] for p in plans)
+    assert len({p["master"] for p in plans}) == 1 and plans[0]["master"].startswith("127.0.0.1:")
+    rows = 100_000_000
+    for part, total in (("train", rows), ("test", rows // 100)):
+        off = 0
+        for p in plans:
+            sh = p[part]
+            assert sh["row_offset"] == off
+            off += sh["rows"]
+            assert sh["rows_total"] == (total if scaling == "strong" else total * n)
+        assert off == plans[0][part]["rows_total"]
+
+
+def test_one_gpu_runs_in_process_and_mismatch_fails():
+    out = _dry([])
+    plans = [json.loads(l) for l in out.stdout.splitlines() if l.startswith("{")]
+    assert len(plans) == 1 and plans[0]["world_size"] == 1 and plans[0]["train"]["rows"] == 100_000_000
+    bad = _dry(["--gpus", "2"], {"WORLD_SIZE": "1", "RANK": "0", "LOCAL_RANK": "0"})
+    assert bad.returncode != 0 and "WORLD_SIZE" in bad.stderr
+
+
+def test_features_shard_holds_every_row():
+    out = _dry(["--gpus", "2", "--shard", "features"])
+    for l in out.stdout.splitlines():
+        p = json.loads(l)
+        assert p["train"] == {"rows": 100_000_000, "row_offset": 0, "rows_total": 100_000_000}
+
+
+def test_row_shards_are_slices_of_one_data_set():
+    n, F, S = 3001, 6, 50
+    full = synth.generate(n, F, S, 1000, 1)
+    parts = [synth.generate(hi - lo, F, S, 1000, 1, row_offset=lo)
+             for lo, hi in ((0, 1000), (1000, 2500), (2500, 3001))]
+    np.testing.assert_array_equal(np.concatenate([p[1] for p in parts]), full[1])
+    np.testing.assert_array_equal(np.concatenate([p[2] for p in parts]), full[2])
+    np.testing.assert_array_equal(np.concatenate([p[3] for p in parts]), full[3])
+
+
+def test_planted_model_is_learnable_on_held_out_rows():
+    """The bench's train/test pairing: different row seeds, one model seed. VB (the oracle)
+    beats the constant predictor on the test rows and its test RMSE falls over iterations."""
+    n, F, S, k = 20000, 8, 100, 4
+    rp, f, v, y = synth.generate(n, F, S, 1000, 0)
+    rpt, ft, vt, yt = synth.generate(4000, F, S, 500000, 0)
+    o = oc.VB(1, 1, k, F * S + 1)
+    o.init_params(3, 0.1)
+    o.attach(oc.Data(csr=(n, rp, f, v, y)), oc.Data(csr=(4000, rpt, ft, vt, yt)))
+    o.init_caches()
+    trace = [o.iterate()[0] for _ in range(12)]
+    const = float(np.sqrt(np.mean((yt - y.mean()) ** 2)))
+    assert trace[-1] < 0.85 * const, (trace, const)
+    assert trace[-1] < trace[2] < trace[0]

@@ -173,13 +173,15 @@ def test_trace_movielens_split_vs_reference(sa_split, split, layout, monkeypatch
     close(fml.get_params()["mu_w"], a["final_mu_w"])
 
 
-def test_device_generator_matches_spec():
-    """vbfm_synth_generate (device) == tests/synth.py (numpy), CSC bit-exact."""
+@pytest.mark.parametrize("model_seed,row_offset", [(synth.MODEL_SEED, 0), (12345, 0), (synth.MODEL_SEED, 777_777)])
+def test_device_generator_matches_spec(model_seed, row_offset):
+    """vbfm_synth_generate (device) == tests/synth.py (numpy), CSC and targets bit-exact,
+    with the default and another planted model, and as a row shard of a larger data set."""
     n, F, S, seed = 5000, 7, 300, 99
     fml = vbfm.FMLearnVB(1, 1, 2, F * S + 1)
-    fml.synth(0, n, F, S, seed, xmode=1)
+    fml.synth(0, n, F, S, seed, xmode=1, model_seed=model_seed, row_offset=row_offset)
     cp, ent, tg = fml.get_csc(0)
-    rp, f, v, y = synth.generate(n, F, S, seed, 1)
+    rp, f, v, y = synth.generate(n, F, S, seed, 1, model_seed=model_seed, row_offset=row_offset)
     ecp, erow, eval_ = synth.csr_to_csc(n, F * S, rp, f, v)
     np.testing.assert_array_equal(cp, ecp)
     np.testing.assert_array_equal(ent["id"], erow)

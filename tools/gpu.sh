@@ -1,0 +1,47 @@
+#!/bin/bash
+# One parameterised GPU-box runner (replaces the per-session scripts).
+# usage (from gpurun): bash tools/gpu.sh <outdir> <step> [<step> ...]
+#   tests[=<pytest -k expr>]   the -m gpu suite (or a subset), one process, per-test timeout
+#   smoke                      __graft_entry__.smoke()
+#   bench[=<args>]             python bench.py <args> > bench.json (args: '+' separates words)
+#   prof[=<args>]              rocprofv3 --kernel-trace --stats of bench.py <args>
+#   pmc[=<args>]               FETCH_SIZE then WRITE_SIZE, one --pmc pass each, of bench.py <args>
+#   py=<script>[+args]         python -u <script> <args>
+# Every step runs under its own timeout; the first failure ends the call.
+cd "$GRAFT_REPO_ROOT" || exit 1
+export TMPDIR=/tmp
+O=gpurun_out/$1; shift
+mkdir -p "$O"
+n=0
+for step in "$@"; do
+  n=$((n + 1))
+  name=${step%%=*}; arg=""; [ "$name" != "$step" ] && arg=${step#*=}
+  args=${arg//+/ }
+  echo "step $n $step start $(date +%T)" >> "$O/progress.txt"
+  case $name in
+    tests)
+      if [ -n "$arg" ]; then
+        timeout -k 10 1100 python -u -m pytest tests -x -v -m gpu -k "$arg" -p no:cacheprovider --timeout 400 \
+          --timeout-method thread > "$O/tests_$n.txt" 2>&1
+      else
+        timeout -k 10 1100 python -u -m pytest tests -x -v -m gpu -p no:cacheprovider --timeout 400 \
+          --timeout-method thread > "$O/tests_$n.txt" 2>&1
+      fi ;;
+    smoke) timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > "$O/smoke_$n.txt" 2>&1 ;;
+    bench) timeout -k 10 900 python -u bench.py $args > "$O/bench_$n.json" 2> "$O/bench_$n.txt" ;;
+    prof)
+      timeout -k 10 900 rocprofv3 --kernel-trace --stats -d "$O/prof_$n" -o kt --output-format csv -- \
+        python3 bench.py $args > "$O/prof_$n.json" 2> "$O/prof_$n.txt" ;;
+    pmc)
+      for c in FETCH_SIZE WRITE_SIZE; do
+        timeout -k 10 600 rocprofv3 --pmc $c --kernel-trace -d "$O/pmc_${n}_$c" -o p --output-format csv -- \
+          python3 bench.py $args > "$O/pmc_${n}_$c.json" 2> "$O/pmc_${n}_$c.txt" || break
+      done ;;
+    py) timeout -k 10 900 python -u $args > "$O/py_$n.txt" 2>&1 ;;
+    *) echo "unknown step $step" >> "$O/progress.txt"; exit 2 ;;
+  esac
+  rc=$?
+  echo "step $n $step rc=$rc $(date +%T)" >> "$O/progress.txt"
+  [ $rc -ne 0 ] && exit $rc
+done
+exit 0
