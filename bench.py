@@ -164,6 +164,9 @@ def main():
                     help="row-cache layout of the sweeps (include/vbfm.h VBFM_LAYOUT_*)")
     ap.add_argument("--scaling", default="strong", choices=["strong", "weak"],
                     help="row shards: strong = the config's rows in total (default), weak = per rank")
+    ap.add_argument("--transport", default="rccl", choices=["rccl", "host"],
+                    help="rank exchange: rccl (one GPU per rank, xGMI) or host (every all-reduce staged "
+                         "through host memory and a gloo all_reduce: a rehearsal of N ranks on fewer GPUs)")
     ap.add_argument("--dry-run", action="store_true",
                     help="print each rank's launch and shard plan as JSON and exit (no GPU)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -223,7 +226,15 @@ def main():
         if mc:
             raise SystemExit("--shard features is a VB mode")
         fml.set_shard_mode("features")
-    if world > 1:
+    if world > 1 and args.transport == "host":
+        def host_allreduce(arr, op):
+            t = torch.from_numpy(arr.astype(np.float64) if arr.dtype == np.uint32 else arr.copy())
+            if arr.dtype == np.uint8:
+                t = t.to(torch.int32)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX if op == "max" else dist.ReduceOp.SUM)
+            arr[:] = t.numpy().astype(arr.dtype)
+        fml.comm_init_host(world, rank, host_allreduce)
+    elif world > 1:
         obj = [vbfm.FMLearnVB.comm_unique_id() if rank == 0 else None]
         dist.broadcast_object_list(obj, src=0)
         fml.comm_init(world, rank, obj[0])

@@ -1,0 +1,195 @@
+"""Parity at the BASELINE configurations' own sizes (BASELINE.json configs[1..4]).
+
+* C2 (ML-1M shaped): 900,209 train / 100,000 test rows, 6,040 users + 3,952 items with a
+  skewed item popularity (long item columns take the segmented kernels), k = 20, three VB
+  iterations against the oracle.
+* C3 (1e7 rows x 40 one-hot fields x 25,000 ids), k = 2, one VB iteration against the
+  oracle on the full data set (the oracle reads the device-generated data back).
+* C4 rows (1e8 x 40 x 125,000 ids), k = 2: two iterations on every kernel form the sizes
+  select -- level and column layouts, fused and deferred-split (row-shard) kernels -- agree
+  to summation order; the split form is the fused one bit for bit.
+* C5: the MCMC Gibbs sweep with device RNG streams at C4 rows, k = 2: the fused and the
+  row-shard split kernels draw the same chain bit for bit; ALS (no sampling) on the level
+  and column layouts agrees to summation order.
+
+The oracle (tests/oracle_ctypes.py, the C restatement pinned to the reference's fixtures) is
+the checker; the tolerance is REL = 1e-9 relative (the north star's gate is 1e-6).
+"""
+import os
+
+import numpy as np
+import pytest
+
+import oracle_ctypes as oc
+import synth
+import vbfm
+
+pytestmark = pytest.mark.gpu
+
+REL = 1e-9
+
+
+def rel_err(a, b):
+    a, b = np.asarray(a, dtype=np.float64), np.asarray(b, dtype=np.float64)
+    scale = max(float(np.max(np.abs(b))) if b.size else 0.0, 1e-300)
+    return float(np.max(np.abs(a - b))) / scale if a.size else 0.0
+
+
+def close(a, b, tol=REL):
+    assert rel_err(a, b) <= tol, (rel_err(a, b), a, b)
+
+
+def c2_data(n, seed):
+    """ML-1M-shaped rows: user uniform over 6,040 ids, item over 3,952 ids with popularity
+    ~ u^3 (a few items own thousands of rows), targets from the planted model's shape."""
+    U, I = 6040, 3952
+    idx = np.arange(n, dtype=np.uint64)
+    user = (synth.h(seed, 1, idx) % np.uint64(U)).astype(np.uint32)
+    u = synth._u(seed, 2, idx)
+    item = (U + np.minimum((u ** 3 * I).astype(np.int64), I - 1)).astype(np.uint32)
+    feat = np.stack([user, item], axis=1).reshape(-1)
+    val = np.ones(2 * n, dtype=np.float32)
+    bu = synth._u(synth.MODEL_SEED, 3, np.arange(U + I, dtype=np.uint64)) - 0.5
+    y = np.clip(np.rint(3.0 + 1.5 * (bu[user] + bu[item]) + 1.5 * (synth._u(seed, 4, idx) - 0.5)), 1, 5)
+    rp = np.arange(n + 1, dtype=np.uint64) * np.uint64(2)
+    return rp, feat, val, y.astype(np.float32)
+
+
+def test_c2_movielens_shape_three_iterations_vs_oracle():
+    n, n_test, k = 900_209, 100_000, 20
+    tr = c2_data(n, 31)
+    te = c2_data(n_test, 32)
+    nf = 6040 + 3952
+    assert np.bincount(tr[1], minlength=nf).max() > 8192     # long columns: the segmented kernels
+    D = nf + 1
+    g = vbfm.FMLearnVB(1, 1, k, D, min_target=float(tr[3].min()), max_target=float(tr[3].max()))
+    g.init(42, 0.1)
+    g.set_data(vbfm.DataSubset.from_csr(*tr, nf), vbfm.DataSubset.from_csr(*te, nf))
+    g.init_caches()
+    o = oc.VB(1, 1, k, D)
+    o.init_params(42, 0.1)
+    o.attach(oc.Data(csr=(n,) + tr), oc.Data(csr=(n_test,) + te))
+    o.init_caches()
+    for it in range(3):
+        st = g.iterate()
+        rmse, mae, quirk = o.iterate()
+        close(st.rmse, rmse)
+        close(st.mae, mae)
+        close(st.train_quirk, quirk)
+        close(st.free_energy, o.s.last_free_energy)
+        close(st.alpha, o.s.alpha)
+    p, op = g.get_params(), o.params()
+    for key in ("mu_w", "sigma_w", "mu_v", "sigma_v", "hyp_sigma_v"):
+        close(p[key], op[key])
+
+
+def _csr_from_field_csc(n, F, S, cp, ent):
+    """CSR of one-hot field data (row r holds exactly one id of every field) from its CSC."""
+    nf = len(cp) - 1
+    col = np.repeat(np.arange(nf, dtype=np.uint32), np.diff(cp.astype(np.int64)))
+    pos = ent["id"].astype(np.int64) * F + col // np.uint32(S)
+    feat = np.empty(n * F, dtype=np.uint32)
+    val = np.empty(n * F, dtype=np.float32)
+    feat[pos] = col
+    val[pos] = ent["value"]
+    return np.arange(n + 1, dtype=np.uint64) * np.uint64(F), feat, val
+
+
+def test_c3_full_size_one_iteration_vs_oracle():
+    n, F, S, k, n_test = 10_000_000, 40, 25_000, 2, 100_000
+    D = F * S + 1
+    g = vbfm.FMLearnVB(1, 1, k, D, min_target=1.0, max_target=5.0)
+    g.init(3, 0.1)
+    g.synth(0, n, F, S, 1000, 1)
+    g.synth(1, n_test, F, S, 500000, 1)
+    cp, ent, y = g.get_csc(0)
+    rp, feat, val = _csr_from_field_csc(n, F, S, cp, ent)
+    del cp, ent
+    tr = oc.Data(csr=(n, rp, feat, val, y))
+    del rp, feat, val
+    te = oc.Data(csr=(n_test,) + synth.generate(n_test, F, S, 500000, 1))
+    g.init_caches()
+    assert g.layout() == "level"
+    o = oc.VB(1, 1, k, D)
+    o.init_params(3, 0.1)
+    o.attach(tr, te)
+    o.init_caches()
+    st = g.iterate()
+    rmse, mae, _ = o.iterate()
+    assert st.num_levels == F
+    close(st.rmse, rmse)
+    close(st.mae, mae)
+    close(st.free_energy, o.s.last_free_energy)
+    close(st.alpha, o.s.alpha)
+    p, op = g.get_params(), o.params()
+    for key in ("mu_w", "mu_v", "sigma_v"):
+        close(p[key], op[key])
+
+
+C4 = dict(n=100_000_000, F=40, S=125_000, k=2, n_test=1_000_000)
+
+
+def _c4_vb(layout, split, defer=True):
+    os.environ["VBFM_FORCE_SPLIT"] = split
+    if not defer:
+        os.environ["VBFM_DEFER"] = "0"
+    try:
+        c = C4
+        g = vbfm.FMLearnVB(1, 1, c["k"], c["F"] * c["S"] + 1, min_target=1.0, max_target=5.0, layout=layout)
+        g.init_device(42)
+        g.synth(0, c["n"], c["F"], c["S"], 1000, 0)
+        g.synth(1, c["n_test"], c["F"], c["S"], 500000, 0)
+        g.init_caches()
+        assert g.layout() == layout
+        st = [g.iterate() for _ in range(2)]
+        out = ([s.free_energy for s in st], [s.rmse for s in st], [s.alpha for s in st], g.get_params()["mu_v"])
+        g.close()
+        return out
+    finally:
+        os.environ.pop("VBFM_FORCE_SPLIT", None)
+        os.environ.pop("VBFM_DEFER", None)
+
+
+def test_c4_rows_layouts_and_split_agree():
+    base = _c4_vb("level", "0")
+    assert all(np.isfinite(base[0])) and base[1][1] < base[1][0]
+    split = _c4_vb("level", "1")
+    assert split[0] == base[0] and split[1] == base[1]          # deferred split == fused, bit for bit
+    np.testing.assert_array_equal(split[3], base[3])
+    for r in (_c4_vb("column", "0"), _c4_vb("column", "1")):
+        for a, b in zip(r, base):
+            close(a, b, 1e-11)
+
+
+def _c4_mc(method, layout, split):
+    os.environ["VBFM_FORCE_SPLIT"] = split
+    try:
+        c = C4
+        g = vbfm.FMLearnMCMC(1, 1, c["k"], c["F"] * c["S"] + 1, min_target=1.0, max_target=5.0, method=method,
+                             layout=layout)
+        g.init_device(42)
+        g.synth(0, c["n"], c["F"], c["S"], 1000, 0)
+        g.synth(1, c["n_test"], c["F"], c["S"], 500000, 0)
+        g.init_caches()
+        assert g.layout() == layout
+        st = [g.iterate() for _ in range(2)]
+        out = ([s.rmse_all for s in st], [s.alpha for s in st], g.get_params()["v"])
+        g.close()
+        return out
+    finally:
+        os.environ.pop("VBFM_FORCE_SPLIT", None)
+
+
+def test_c5_mcmc_device_rng_fused_equals_split():
+    a = _c4_mc("mcmc", "level", "0")
+    b = _c4_mc("mcmc", "level", "1")
+    assert all(np.isfinite(a[0]))
+    assert a[0] == b[0] and a[1] == b[1]
+    np.testing.assert_array_equal(a[2], b[2])
+
+
+def test_c5_als_layouts_agree():
+    a = _c4_mc("als", "level", "0")
+    b = _c4_mc("als", "column", "0")
+    for x, y in zip(a, b):
+        close(x, y, 1e-10)
