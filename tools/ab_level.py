@@ -2,7 +2,7 @@
 the scatter-bound launch time moves by up to +-10 % from one process (allocation) to the next.
 usage: python tools/ab_level.py ROUNDS label=libpath[:ENV=V,...] ...
 Each child: C4 rows (1e8 x 40 fields x 125000 ids), k=8, 1 warm-up + 2 iterations, prints the
-average v-level launch ms."""
+average v-level launch ms. AB_METHOD=mcmc|als in the environment: the MCMC / ALS learner."""
 import json, os, subprocess, sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -11,7 +11,11 @@ import os, sys, json
 sys.path.insert(0, os.environ["AB_PKG"])
 import vbfm
 N, F, S, k = 100000000, 40, 125000, 8
-fml = vbfm.FMLearnVB(1, 1, k, F * S + 1, min_target=1.0, max_target=5.0, device=0)
+meth = os.environ.get("AB_METHOD", "vb")
+if meth == "vb":
+    fml = vbfm.FMLearnVB(1, 1, k, F * S + 1, min_target=1.0, max_target=5.0, device=0)
+else:
+    fml = vbfm.FMLearnMCMC(1, 1, k, F * S + 1, min_target=1.0, max_target=5.0, device=0, method=meth)
 fml.init_device(42)
 fml.synth(0, N, F, S, seed=1000, xmode=0)
 fml.synth(1, N // 100, F, S, seed=500000, xmode=0)
@@ -20,7 +24,8 @@ fml.set_profiling(True)
 fml.iterate()
 st = [fml.iterate() for _ in range(2)]
 ms = sum(s.ms_vlevel_kernels for s in st) / sum(s.n_vlevel_launches for s in st)
-print(json.dumps({"ms_launch": ms, "ms_iter": sum(s.ms_total for s in st) / 2, "ms_w": st[-1].ms_w, "rmse": st[-1].rmse}))
+print(json.dumps({"ms_launch": ms, "ms_iter": sum(s.ms_total for s in st) / 2, "ms_w": st[-1].ms_w,
+                  "rmse": st[-1].rmse if meth == "vb" else st[-1].rmse_all}))
 fml.close()
 '''
 
