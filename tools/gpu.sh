@@ -7,6 +7,7 @@
 #   prof[=<args>]              rocprofv3 --kernel-trace --stats of bench.py <args>
 #   pmc[=<args>]               FETCH_SIZE then WRITE_SIZE, one --pmc pass each, of bench.py <args>
 #   py=<script>[+args]         python -u <script> <args>
+#   exe=<binary>[+args]        a built probe binary
 # Every step runs under its own timeout; the first failure ends the call.
 cd "$GRAFT_REPO_ROOT" || exit 1
 export TMPDIR=/tmp
@@ -38,6 +39,7 @@ for step in "$@"; do
           python3 bench.py $args > "$O/pmc_${n}_$c.json" 2> "$O/pmc_${n}_$c.txt" || break
       done ;;
     py) timeout -k 10 900 python -u $args > "$O/py_$n.txt" 2>&1 ;;
+    exe) timeout -k 10 600 $args > "$O/exe_$n.txt" 2>&1 ;;
     *) echo "unknown step $step" >> "$O/progress.txt"; exit 2 ;;
   esac
   rc=$?
