@@ -372,7 +372,8 @@ def main():
         "phase_ms": {kk: getattr(stats[-1], kk) for kk in (
             ("ms_hyper", "ms_w", "ms_v", "ms_predict", "ms_total") if mc else
             ("ms_regroup", "ms_predict", "ms_w0", "ms_w", "ms_v", "ms_hyper", "ms_test", "ms_total") if online else
-            ("ms_w0", "ms_w", "ms_qcache_kernels", "ms_v", "ms_hyper", "ms_test", "ms_total"))},
+            ("ms_w0", "ms_w", "ms_qcache_kernels", "ms_v", "ms_hyper", "ms_test", "ms_test_predict",
+             "ms_total"))},
         "cpu_baseline": None,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline and not mc and not online:

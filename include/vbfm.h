@@ -97,6 +97,9 @@ typedef struct {
 	double ms_vlevel_kernels, ms_wlevel_kernels, ms_qcache_kernels;
 	int32_t n_vlevel_launches, n_wlevel_launches, n_qcache_launches;
 	uint64_t nnz_train;         /* nnz of this shard's train data */
+	/* device time of the test prediction itself; it runs on a second stream under the
+	 * hyper-parameter step (ms_test then covers only what follows it: metrics, train quirk) */
+	double ms_test_predict;
 } vbfm_iter_stats;
 
 /* ---- lifecycle ---------------------------------------------------------------------- */

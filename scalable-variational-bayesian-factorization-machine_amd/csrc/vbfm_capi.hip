@@ -775,10 +775,22 @@ int blocked_predict(const vbfm_ctx *c, const DevData &d)
 	return (double)d.nnz * c->k > 5e7 ? 2 : 0;
 }
 
-void test_predict(vbfm_ctx *c)
+void test_predict(vbfm_ctx *c, hipStream_t s)
 {
 	HIPCHK(vbk::predict_e(c->te.row_ptr, c->te.csr, c->ms_v, c->ms_w, c->k, c->k1, c->k0, c->mu0, c->e_test, c->te.n,
-	                      blocked_predict(c, c->te), c->s));
+	                      blocked_predict(c, c->te), s));
+}
+
+// The per-iteration test prediction (fm_learn_vb_simultaneous.h:125) reads mu0, mu_w, mu_v,
+// which are final once the factor sweeps end; the hyper-parameter step and the free energy
+// (fm_learn_vb.h:446-498, :646-681) only read them. So the prediction runs on its own stream
+// from the end of the sweeps, under the hyper step (its reductions, host arithmetic and
+// syncs), and the metrics wait for it: the same kernel on the same inputs, bit-identical
+// (VBFM_TEST_OVERLAP=0 runs it after the hyper step on the main stream).
+bool test_overlap()
+{
+	const char *e = getenv("VBFM_TEST_OVERLAP");
+	return !(e && e[0] == '0');
 }
 
 void read_counters(vbfm_ctx *c, vbfm_iter_stats *o)
@@ -831,6 +843,7 @@ int vbfm_create(vbfm_ctx **out, const vbfm_config *cfg)
 	}
 	int rc = guarded(c, [&] {
 		HIPCHK(hipStreamCreateWithFlags(&c->s, hipStreamNonBlocking));
+		HIPCHK(hipStreamCreateWithFlags(&c->s_test, hipStreamNonBlocking));
 		for (int i = 0; i < EV_N; i++) HIPCHK(hipEventCreate(&c->ev[i]));
 		c->group_h.assign(c->D, 0);
 		if (cfg->attr_group)
@@ -889,6 +902,7 @@ void vbfm_destroy(vbfm_ctx *c)
 	for (int i = 0; i < EV_N; i++)
 		if (c->ev[i]) (void)hipEventDestroy(c->ev[i]);
 	if (c->s) (void)hipStreamDestroy(c->s);
+	if (c->s_test) (void)hipStreamDestroy(c->s_test);
 	delete c;
 }
 
@@ -1136,7 +1150,7 @@ int vbfm_init_caches(vbfm_ctx *c)
 		const int bl = blocked_predict(c, c->tr);
 		HIPCHK(vbk::predict_et(c->tr.row_ptr, c->tr.csr, c->ms_v, c->ms_w, c->k, c->k1, c->k0, c->mu0, c->s0d,
 		                       c->tr.target, c->scratch_n, c->rows, c->tr.n, bl, c->s));
-		if (c->e_test) test_predict(c);
+		if (c->e_test) test_predict(c, c->s);
 		sync(c);
 	});
 }
@@ -1281,6 +1295,13 @@ int vbfm_iterate(vbfm_ctx *c, vbfm_iter_stats *o)
 		c->carry_ok = 0;
 		if (c->carry) throw std::string("internal: a deferred correction was left pending");
 		HIPCHK(hipEventRecord(c->ev[EV_V], c->s));
+		const bool overlap = test_overlap();
+		if (overlap) {
+			HIPCHK(hipStreamWaitEvent(c->s_test, c->ev[EV_V], 0));
+			HIPCHK(hipEventRecord(c->ev[EV_TP0], c->s_test));
+			test_predict(c, c->s_test);
+			HIPCHK(hipEventRecord(c->ev[EV_TP1], c->s_test));
+		}
 		double energy = 0.0;
 		bool early;
 		{
@@ -1292,7 +1313,13 @@ int vbfm_iterate(vbfm_ctx *c, vbfm_iter_stats *o)
 		HIPCHK(hipEventRecord(c->ev[EV_HYPER], c->s));
 		// test prediction and metrics (fm_learn_vb_simultaneous.h:125-222)
 		Range r_test("test prediction");
-		test_predict(c);
+		if (overlap) {
+			HIPCHK(hipStreamWaitEvent(c->s, c->ev[EV_TP1], 0));
+		} else {
+			HIPCHK(hipEventRecord(c->ev[EV_TP0], c->s));
+			test_predict(c, c->s);
+			HIPCHK(hipEventRecord(c->ev[EV_TP1], c->s));
+		}
 		const double mn = c->min_target, mx = c->max_target;
 		HIPCHK(vbk::test_metrics(c->e_test, c->te.target, c->te.n, mn, mx, c->pred_test, c->red_d, c->RED_BLOCKS, c->s));
 		HIPCHK(hipMemcpyAsync(c->red_h.data(), c->red_d, 2 * c->RED_BLOCKS * 8, hipMemcpyDeviceToHost, c->s));
@@ -1316,6 +1343,7 @@ int vbfm_iterate(vbfm_ctx *c, vbfm_iter_stats *o)
 		st.ms_qcache = 0.0;
 		st.ms_hyper = ev_ms(c, EV_V, EV_HYPER);
 		st.ms_test = ev_ms(c, EV_HYPER, EV_TEST);
+		st.ms_test_predict = ev_ms(c, EV_TP0, EV_TP1);
 		st.ms_total = ev_ms(c, EV_BEGIN, EV_TEST);
 		st.nnz_train = c->tr.nnz;
 		for (const auto &sp : c->spans) {

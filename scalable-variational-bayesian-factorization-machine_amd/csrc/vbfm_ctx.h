@@ -62,7 +62,7 @@ template <class T> inline void dfree(T *&p)
 	p = nullptr;
 }
 
-enum { EV_BEGIN, EV_W0, EV_W, EV_V, EV_HYPER, EV_TEST, EV_N };
+enum { EV_BEGIN, EV_W0, EV_W, EV_V, EV_HYPER, EV_TEST, EV_TP0, EV_TP1, EV_N };
 
 // roctx ranges around the phases of an iteration (VBFM_ROCTX=1; 2 adds one per level launch)
 // for rocprofv3 --marker-trace timelines
@@ -85,6 +85,7 @@ struct vbfm_ctx {
 	std::string err;
 	int dev = 0;
 	hipStream_t s = nullptr;
+	hipStream_t s_test = nullptr;   // the test prediction, overlapping the hyper-parameter step
 	int k0 = 1, k1 = 1, k = 0;
 	uint32_t D = 0, G = 1;
 	std::vector<uint32_t> group_h, per_group;
@@ -225,7 +226,7 @@ void step_v(vbfm_ctx *c, int f);
 double rows_energy(vbfm_ctx *c);
 std::vector<double> param_sums(vbfm_ctx *c, int mode);
 double free_energy(vbfm_ctx *c, double energy);
-void test_predict(vbfm_ctx *c);
+void test_predict(vbfm_ctx *c, hipStream_t s);
 void read_counters(vbfm_ctx *c, vbfm_iter_stats *o);
 void upload_hyp(vbfm_ctx *c);
 void lord_release(vbfm_ctx *c, bool keep_rows);

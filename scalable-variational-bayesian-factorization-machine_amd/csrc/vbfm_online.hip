@@ -1150,7 +1150,7 @@ int vbfm_online_epoch(vbfm_ctx *c, vbfm_online_stats *out)
 		}
 		HIPCHK(hipEventRecord(o.ev[2], c->s));
 		// test prediction and metrics (:190-245)
-		test_predict(c);
+		test_predict(c, c->s);
 		const double mn = c->min_target, mx = c->max_target;
 		HIPCHK(vbk::test_metrics(c->e_test, c->te.target, c->te.n, mn, mx, c->pred_test, c->red_d, c->RED_BLOCKS, c->s));
 		HIPCHK(hipMemcpyAsync(c->red_h.data(), c->red_d, 2 * c->RED_BLOCKS * 8, hipMemcpyDeviceToHost, c->s));

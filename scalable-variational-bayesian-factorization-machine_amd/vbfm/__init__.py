@@ -75,7 +75,8 @@ class IterStats(C.Structure):
                 ("ms_hyper", C.c_double), ("ms_test", C.c_double), ("ms_total", C.c_double),
                 ("ms_vlevel_kernels", C.c_double), ("ms_wlevel_kernels", C.c_double),
                 ("ms_qcache_kernels", C.c_double), ("n_vlevel_launches", C.c_int32),
-                ("n_wlevel_launches", C.c_int32), ("n_qcache_launches", C.c_int32), ("nnz_train", C.c_uint64)]
+                ("n_wlevel_launches", C.c_int32), ("n_qcache_launches", C.c_int32), ("nnz_train", C.c_uint64),
+                ("ms_test_predict", C.c_double)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}

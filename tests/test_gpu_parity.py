@@ -587,3 +587,29 @@ def test_init_replay_equals_host_draws(seed, init_stdev):
         assert pa[key] == pb[key]
     np.testing.assert_array_equal(a.fm_v, b.fm_v)
     np.testing.assert_array_equal(a.fm_w, b.fm_w)
+
+
+def test_test_prediction_overlap_is_bit_identical(monkeypatch):
+    """The per-iteration test prediction runs on its own stream under the hyper-parameter
+    step (fm_learn_vb_simultaneous.h:125 after update_all): the same kernel on the same
+    parameters, so RMSE / MAE / predictions equal the serial order (VBFM_TEST_OVERLAP=0) bit
+    for bit, on both prediction forms."""
+    n, F, S, k = 60_000, 12, 500, 6
+    runs = {}
+    for overlap in ("1", "0"):
+        for predict in ("exact", "wave"):
+            monkeypatch.setenv("VBFM_TEST_OVERLAP", overlap)
+            monkeypatch.setenv("VBFM_PREDICT", predict)
+            g = vbfm.FMLearnVB(1, 1, k, F * S + 1, min_target=1.0, max_target=5.0)
+            g.init(4, 0.1)
+            g.synth(0, n, F, S, 1000, 1)
+            g.synth(1, 5000, F, S, 500000, 1)
+            g.init_caches()
+            st = [g.iterate() for _ in range(3)]
+            assert all(s.ms_test_predict > 0 for s in st)
+            runs[(overlap, predict)] = ([(s.rmse, s.mae, s.free_energy) for s in st], g.test_e())
+            g.close()
+    for predict in ("exact", "wave"):
+        a, b = runs[("1", predict)], runs[("0", predict)]
+        assert a[0] == b[0]
+        np.testing.assert_array_equal(a[1], b[1])
