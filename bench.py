@@ -45,6 +45,11 @@ CONFIGS = {
     "c2": dict(rows=900_209, fields=2, ids=6_040, k=20,
                desc="C2-shaped: 900k rows x 2 fields (users/items), k=20, -method vb"),
     "tiny": dict(rows=200_000, fields=10, ids=2_000, k=8, desc="smoke-sized synthetic"),
+    # no field structure: rows of 5..60 distinct ids out of 1e6 (tests/synth.py generate_multihot);
+    # the dependency levels miss rows, so the sweeps run on the column-gather layout
+    "multihot": dict(rows=10_000_000, features=1_000_000, lo=5, hi=60, k=50,
+                     desc="multi-hot: 10M rows x U(5,60) distinct ids of 1M features (no fields), nnz ~3.25e8, "
+                          "k=50, -method vb"),
 }
 
 
@@ -169,6 +174,9 @@ def main():
                          "through host memory and a gloo all_reduce: a rehearsal of N ranks on fewer GPUs)")
     ap.add_argument("--dry-run", action="store_true",
                     help="print each rank's launch and shard plan as JSON and exit (no GPU)")
+    ap.add_argument("--no-launch-events", action="store_true",
+                    help="no HIP event pair around every level launch (the roofline then divides the "
+                         "sweep phase by the launch count: gaps between launches included)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-rows", type=int, default=2_000_000)
     ap.add_argument("--cpu-factors", type=int, default=2)
@@ -186,8 +194,11 @@ def main():
         cfg["rows"] = args.rows
     if args.k:
         cfg["k"] = args.k
-    F, S, k = cfg["fields"], cfg["ids"], cfg["k"]
-    D = F * S + 1
+    k = cfg["k"]
+    multihot = "features" in cfg
+    F, S = (0, 0) if multihot else (cfg["fields"], cfg["ids"])
+    NF = cfg["features"] if multihot else F * S       # train features
+    D = NF + 1
     fshard = args.shard == "features"
     plan = shard_plan(cfg["rows"], world, rank, "features" if fshard else args.scaling)
     N, row0, n_total = plan["rows"], plan["row_offset"], plan["rows_total"]
@@ -242,18 +253,25 @@ def main():
         fml.init_device(42)
     # one data set, one planted model (tests/synth.py): this rank's slice of the train and
     # test rows; feature shards hold every row
-    fml.synth(0, N, F, S, seed=1000, xmode=0, row_offset=row0)
-    fml.synth(1, n_test, F, S, seed=500000, xmode=0, row_offset=trow0)
+    if multihot:
+        fml.synth_multihot(0, N, NF, cfg["lo"], cfg["hi"], seed=1000, xmode=0, row_offset=row0)
+        fml.synth_multihot(1, n_test, NF, cfg["lo"], cfg["hi"], seed=500000, xmode=0, row_offset=trow0)
+    else:
+        fml.synth(0, N, F, S, seed=1000, xmode=0, row_offset=row0)
+        fml.synth(1, n_test, F, S, seed=500000, xmode=0, row_offset=trow0)
     if online:
         # the reference's initial draws generated on the device, the rand() stream continued
         # into the epoch shuffles (vbfm_online_init, VBFM_ONLINE_INIT_REPLAY)
         fml.init(42, 0.1, args.batch, replay=True)
     else:
         fml.init_caches()
-    if not online:   # per-launch event pairs: the online epoch has num_batch * k * levels launches
+    launch_events = not online and not args.no_launch_events
+    if launch_events:   # per-launch event pairs: the online epoch has num_batch * k * levels launches
         fml.set_profiling(True)
     layout = fml.layout()
-    log("rank %d: setup %.1f s (N=%d F=%d S=%d k=%d, %s layout)" % (rank, time.time() - t0, N, F, S, k, layout))
+    nnz = fml.shape(0)[2]                # this rank's train entries
+    log("rank %d: setup %.1f s (N=%d F=%d S=%d features=%d nnz=%d k=%d, %s layout)" % (
+        rank, time.time() - t0, N, F, S, NF, nnz, k, layout))
 
     def rmse_of(st):
         return st.rmse_all if mc else st.rmse
@@ -290,8 +308,12 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
-    nnz = N * F                          # this rank's train entries
-    nnz_total = n_total * F              # the whole data set's (all ranks)
+    if fshard or world == 1:
+        nnz_total = nnz                  # the whole data set's (all ranks)
+    else:
+        tn = torch.tensor([float(nnz)], dtype=torch.float64)
+        dist.all_reduce(tn)
+        nnz_total = int(tn.item())
     value = nnz_total * k * args.steps / elapsed
     levels = stats[-1].num_levels
     # roofline of the dominant kernel (k_level_lord / k_v_level_fused, one launch per factor
@@ -306,15 +328,19 @@ def main():
     # OVBFM: the same per-factor model per mini-batch; every batch reads the parameters of the
     # columns it touches (<= all F*S), the level launches are num_batch * k * levels per epoch,
     # timed as the summed factor-sweep phase of the batches
-    n_launch = sum(s.n_vlevel_launches for s in stats)
-    ms_launch = sum(s.ms_v if online else s.ms_vlevel_kernels for s in stats)
+    if launch_events:
+        n_launch = sum(s.n_vlevel_launches for s in stats)
+        ms_launch = sum(s.ms_vlevel_kernels for s in stats)
+    else:   # no event pairs: the sweep phase over its launches (an upper bound: gaps included)
+        n_launch = sum(s.n_vlevel_launches if online else s.num_levels * k for s in stats)
+        ms_launch = sum(s.ms_v for s in stats)
     avg_ms = ms_launch / max(1, n_launch)
     if online:
-        bytes_per_launch = (128.0 * nnz + 24.0 * N + 32.0 * (F * S) * args.batch) / max(1, levels * args.batch)
+        bytes_per_launch = (128.0 * nnz + 24.0 * N + 32.0 * NF * args.batch) / max(1, levels * args.batch)
     elif mc:
-        bytes_per_launch = (72.0 * nnz + 8.0 * N + 16.0 * (F * S)) / max(1, levels)
+        bytes_per_launch = (72.0 * nnz + 8.0 * N + 16.0 * NF) / max(1, levels)
     else:
-        bytes_per_launch = (128.0 * nnz + 24.0 * N + 32.0 * (F * S)) / max(1, levels)
+        bytes_per_launch = (128.0 * nnz + 24.0 * N + 32.0 * NF) / max(1, levels)
     if fshard:
         bytes_per_launch /= world          # each rank sweeps 1/world of every level's columns
     achieved = bytes_per_launch / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else 0.0
@@ -348,7 +374,7 @@ def main():
                 "planted bias + rank-2 interaction shared by train, test and all shards), "
                 "device random init of mu (0.1*N(0,1))",
         "config": {"workload": cfg["desc"], "rows_total": n_total, "rows_per_gpu": N, "fields": F,
-                   "ids_per_field": S, "features": F * S, "k": k, "nnz_total": nnz_total, "nnz_per_gpu": nnz,
+                   "ids_per_field": S, "features": NF, "k": k, "nnz_total": nnz_total, "nnz_per_gpu": nnz,
                    "test_rows_per_gpu": n_test,
                    "levels": levels, "method": args.method,
                    "step": ("one full %s iteration (draw_all + train/test re-prediction, device RNG streams)"
@@ -376,7 +402,7 @@ def main():
              "ms_total"))},
         "cpu_baseline": None,
     }
-    if rank == 0 and world == 1 and not args.no_cpu_baseline and not mc and not online:
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and not mc and not online and not multihot:
         try:
             rows = min(args.cpu_rows, N)
             result["cpu_baseline"] = cpu_baseline(cfg, rows, min(args.cpu_factors, k))

@@ -119,6 +119,12 @@ int vbfm_set_test(vbfm_ctx *ctx, const vbfm_csc *test);
 int vbfm_synth_generate(vbfm_ctx *ctx, int32_t which, uint32_t num_rows, uint32_t n_fields,
                         uint32_t ids_per_field, uint64_t seed, int32_t xmode, uint64_t model_seed,
                         uint64_t row_offset);
+/* Multi-hot rows WITHOUT field structure (tests/synth.py generate_multihot defines it): row R
+ * holds lo..hi (<= 64) distinct ids out of num_features, one per stratum of the id range, and
+ * the same planted model; the levels of such data miss rows, so the sweeps take the
+ * column-gather layout. Rows [row_offset, row_offset + num_rows) of the one-rank data set. */
+int vbfm_synth_multihot(vbfm_ctx *ctx, int32_t which, uint32_t num_rows, uint32_t num_features, uint32_t lo,
+                        uint32_t hi, uint64_t seed, int32_t xmode, uint64_t model_seed, uint64_t row_offset);
 /* Copy back the device copy of a data set (parity of the device transpose / generator). */
 int vbfm_get_csc(vbfm_ctx *ctx, int32_t which, uint64_t *col_ptr /*[nf+1]*/, vbfm_entry *col_ent /*[nnz]*/,
                  float *target /*[rows]*/);

@@ -562,8 +562,10 @@ size_t prof_begin(vbfm_ctx *c, int kind)
 	if (c->pev_used + 2 > c->pev.size()) {
 		const size_t add = std::max<size_t>(256, c->pev.size());
 		for (size_t i = 0; i < add; i++) {
+			// timestamps only: no system-scope release / acquire (a default event's cache
+			// writeback + invalidate costs ~4 us per record between short level launches)
 			hipEvent_t e;
-			HIPCHK(hipEventCreate(&e));
+			HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableSystemFence));
 			c->pev.push_back(e);
 		}
 	}
@@ -970,6 +972,38 @@ int vbfm_set_test(vbfm_ctx *c, const vbfm_csc *in)
 	});
 }
 
+}  // extern "C"
+
+namespace vbi {
+// the end of a synthetic data set's construction: target range, then (train) the first-entry
+// marks and the row records, (test) the prediction buffers
+void synth_finish(vbfm_ctx *c, int32_t which)
+{
+	DevData &d = which ? c->te : c->tr;
+	const uint32_t n = d.n;
+	// target range (min/max over the targets: 1..5 by construction, computed exactly)
+	std::vector<float> t(n);
+	if (n) HIPCHK(hipMemcpy(t.data(), d.target, (size_t)n * 4, hipMemcpyDeviceToHost));
+	float mn = 3.40282347e+38f, mx = -3.40282347e+38f;
+	for (float v : t) { mn = std::min(v, mn); mx = std::max(v, mx); }
+	d.min_target = mn; d.max_target = mx;
+	if (which == 0) {
+		if (n > ROW_MASK) throw std::string("too many rows for one shard (max 2^31-1)");
+		HIPCHK(vbk::mark_first(d.row_ptr, d.csr, d.col_ptr, d.csc, n, c->s));
+		alloc_rows(c);
+	} else {
+		dfree(c->e_test); dfree(c->pred_test);
+		c->e_test = dalloc<double>(n);
+		c->pred_test = dalloc<double>(n);
+		double v = n;
+		allreduce_host(c, &v, 1);
+		c->test_n_global = (uint32_t)v;
+	}
+}
+}  // namespace vbi
+
+extern "C" {
+
 int vbfm_synth_generate(vbfm_ctx *c, int32_t which, uint32_t n, uint32_t F, uint32_t S, uint64_t seed, int32_t xmode,
                         uint64_t model_seed, uint64_t row_offset)
 {
@@ -1017,24 +1051,72 @@ int vbfm_synth_generate(vbfm_ctx *c, int32_t which, uint32_t n, uint32_t F, uint
 		}
 		sync(c);
 		dfree(stmp); dfree(ki); dfree(ko); dfree(vi); dfree(vo);
-		// target range (min/max over the targets: 1..5 by construction, computed exactly)
-		std::vector<float> t(n);
-		if (n) HIPCHK(hipMemcpy(t.data(), d.target, (size_t)n * 4, hipMemcpyDeviceToHost));
-		float mn = 3.40282347e+38f, mx = -3.40282347e+38f;
-		for (float v : t) { mn = std::min(v, mn); mx = std::max(v, mx); }
-		d.min_target = mn; d.max_target = mx;
-		if (which == 0) {
-			if (n > ROW_MASK) throw std::string("too many rows for one shard (max 2^31-1)");
-			HIPCHK(vbk::mark_first(d.row_ptr, d.csr, d.col_ptr, d.csc, n, c->s));
-			alloc_rows(c);
-		} else {
-			dfree(c->e_test); dfree(c->pred_test);
-			c->e_test = dalloc<double>(n);
-			c->pred_test = dalloc<double>(n);
-			double v = n;
-			allreduce_host(c, &v, 1);
-			c->test_n_global = (uint32_t)v;
+		synth_finish(c, which);
+	});
+}
+
+int vbfm_synth_multihot(vbfm_ctx *c, int32_t which, uint32_t n, uint32_t D, uint32_t lo, uint32_t hi, uint64_t seed,
+                        int32_t xmode, uint64_t model_seed, uint64_t row_offset)
+{
+	if (!c) return fail(nullptr, "null context");
+	return guarded(c, [&] {
+		if (which != 0 && which != 1) throw std::string("which must be 0 (train) or 1 (test)");
+		if (lo < 1 || hi < lo || hi > 64 || D < hi || D >= c->D)
+			throw std::string("multi-hot shape: need 1 <= lo <= hi <= 64, hi <= num_features < num_attribute");
+		DevData &d = which ? c->te : c->tr;
+		free_data(d);
+		d.n = n;
+		d.nf_local = D;
+		d.nf = which ? d.nf_local : global_nf(c, d.nf_local);
+		d.row_ptr = dalloc<uint64_t>((size_t)n + 1);
+		HIPCHK(vbk::synth_mh_len(n, lo, hi, seed, row_offset, d.row_ptr, c->s));
+		size_t tb = 0;
+		HIPCHK(vbk::exclusive_scan_u64(nullptr, &tb, d.row_ptr, d.row_ptr, (size_t)n + 1, c->s));
+		void *tmp = dalloc<uint8_t>(tb);
+		HIPCHK(vbk::exclusive_scan_u64(tmp, &tb, d.row_ptr, d.row_ptr, (size_t)n + 1, c->s));
+		HIPCHK(hipMemcpyAsync(&d.nnz, d.row_ptr + n, 8, hipMemcpyDeviceToHost, c->s));
+		sync(c);
+		dfree(tmp);
+		if (d.nnz >= 0xFFFFFFFFull) throw std::string("multi-hot data set too large (nnz >= 2^32)");
+		// bias / interaction gains per row length L (host sqrt: correctly rounded, as tests/synth.py)
+		std::vector<double> gh(2 * (size_t)(hi - lo + 1));
+		for (uint32_t L = lo; L <= hi; L++) {
+			gh[2 * (L - lo)] = std::sqrt(12.0 / (double)L);
+			gh[2 * (L - lo) + 1] = L >= 2 ? std::sqrt(72.0 / ((double)L * (double)(L - 1) / 2.0)) : 0.0;
 		}
+		double *gains = dalloc<double>(gh.size());
+		HIPCHK(hipMemcpy(gains, gh.data(), gh.size() * 8, hipMemcpyHostToDevice));
+		d.csr = dalloc<uint2>(d.nnz);
+		d.target = dalloc<float>(n);
+		uint32_t *row_of = dalloc<uint32_t>(d.nnz);
+		HIPCHK(vbk::synth_mh_fill(n, D, seed, xmode, model_seed, row_offset, gains, lo, d.row_ptr, d.csr, row_of,
+		                          d.target, c->s));
+		// CSC: entries stably sorted by feature (rows stay ascending inside a column)
+		d.col_ptr = dalloc<uint64_t>((size_t)d.nf + 1);
+		d.csc = dalloc<uint2>(d.nnz);
+		uint64_t *counts = dalloc<uint64_t>((size_t)d.nf + 1);
+		HIPCHK(hipMemsetAsync(counts, 0, ((size_t)d.nf + 1) * 8, c->s));
+		HIPCHK(vbk::count_features(d.csr, d.nnz, counts, c->s));
+		tb = 0;
+		HIPCHK(vbk::exclusive_scan_u64(nullptr, &tb, counts, d.col_ptr, (size_t)d.nf + 1, c->s));
+		tmp = dalloc<uint8_t>(tb);
+		HIPCHK(vbk::exclusive_scan_u64(tmp, &tb, counts, d.col_ptr, (size_t)d.nf + 1, c->s));
+		sync(c);
+		dfree(tmp);
+		dfree(counts);
+		uint32_t *ki = dalloc<uint32_t>(d.nnz), *ko = dalloc<uint32_t>(d.nnz), *vi = dalloc<uint32_t>(d.nnz),
+		         *vo = dalloc<uint32_t>(d.nnz);
+		HIPCHK(vbk::mh_keys(d.csr, d.nnz, ki, vi, c->s));
+		int bits = 1;
+		while ((1ull << bits) < D) bits++;
+		tb = 0;
+		HIPCHK(vbk::sort_pairs_u32(nullptr, &tb, ki, ko, vi, vo, d.nnz, bits, c->s));
+		void *stmp = dalloc<uint8_t>(tb);
+		HIPCHK(vbk::sort_pairs_u32(stmp, &tb, ki, ko, vi, vo, d.nnz, bits, c->s));
+		HIPCHK(vbk::synth_mh_scatter(vo, d.csr, row_of, d.nnz, d.csc, c->s));
+		sync(c);
+		dfree(stmp); dfree(ki); dfree(ko); dfree(vi); dfree(vo); dfree(row_of); dfree(gains);
+		synth_finish(c, which);
 	});
 }
 

@@ -253,6 +253,14 @@ hipError_t synth_field_keys(const uint2 *csr, uint32_t n, uint32_t F, uint32_t S
                             uint32_t *keys, uint32_t *vals, hipStream_t s);
 hipError_t synth_field_scatter(const uint32_t *sorted_rows, const uint2 *csr, uint32_t n, uint32_t F,
                                uint32_t field, uint2 *csc_field, hipStream_t s);
+hipError_t synth_mh_len(uint32_t n, uint32_t lo, uint32_t hi, uint64_t seed, uint64_t row0, uint64_t *len,
+                        hipStream_t s);
+hipError_t synth_mh_fill(uint32_t n, uint32_t D, uint64_t seed, int xmode, uint64_t model_seed, uint64_t row0,
+                         const double *gains, uint32_t lo, const uint64_t *row_ptr, uint2 *csr, uint32_t *row_of,
+                         float *target, hipStream_t s);
+hipError_t mh_keys(const uint2 *csr, uint64_t nnz, uint32_t *keys, uint32_t *vals, hipStream_t s);
+hipError_t synth_mh_scatter(const uint32_t *sorted_p, const uint2 *csr, const uint32_t *row_of, uint64_t nnz,
+                            uint2 *csc, hipStream_t s);
 hipError_t count_features(const uint2 *csr, uint64_t nnz, uint64_t *counts, hipStream_t s);
 // schedule check: owner[n] preset to ~0; *bad counts rows claimed by two columns of the level
 hipError_t check_level(const uint32_t *feats, uint32_t nfeat, const uint64_t *col_ptr, const uint2 *csc,

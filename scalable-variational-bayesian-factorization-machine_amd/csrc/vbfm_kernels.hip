@@ -996,6 +996,64 @@ __global__ void k_synth_field_scatter(const uint32_t *sorted_rows, const uint2 *
 	out[p] = make_uint2(r, csr[(uint64_t)r * F + field].y);
 }
 
+// multi-hot rows without field structure (tests/synth.py generate_multihot is the
+// specification): row R holds L = lo + h(6, R) % (hi - lo + 1) distinct ids, id i drawn in
+// stratum [i D / L, (i + 1) D / L) (ascending by construction); gains per L from the host table
+__global__ void k_mh_len(uint32_t n, uint32_t lo, uint32_t hi, uint64_t seed, uint64_t row0, uint64_t *len)
+{
+	const uint32_t r = blockIdx.x * 256u + threadIdx.x;
+	if (r > n) return;
+	len[r] = r < n ? lo + hstream(seed, 6, row0 + r) % (uint64_t)(hi - lo + 1) : 0;
+}
+
+__global__ void k_mh_fill(uint32_t n, uint32_t D, uint64_t seed, int xmode, uint64_t model_seed, uint64_t row0,
+                          const double *gains, uint32_t lo, const uint64_t *row_ptr, uint2 *csr, uint32_t *row_of,
+                          float *target)
+{
+	const uint32_t r = blockIdx.x * 256u + threadIdx.x;
+	if (r >= n) return;
+	const uint64_t R = row0 + r, b = row_ptr[r];
+	const uint32_t L = (uint32_t)(row_ptr[r + 1] - b);
+	double s = 0.0, s0 = 0.0, s1 = 0.0, q0 = 0.0, q1 = 0.0;
+	for (uint32_t i = 0; i < L; ++i) {
+		const uint64_t a = (uint64_t)i * D / L, e = (uint64_t)(i + 1) * D / L;
+		const uint64_t j = a + hstream(seed, 7, R * 64 + i) % (e - a);
+		float x = 1.0f;
+		if (xmode) x = 0.5f + (float)(hstream(seed, 2, R * 64 + i) >> 40) * 0x1p-24f;
+		csr[b + i] = make_uint2((uint32_t)j, __float_as_uint(x));
+		row_of[b + i] = r;
+		s = s + (synth_unit(model_seed, 3, j) - 0.5);
+		const double a0 = synth_unit(model_seed, 5, 2 * j) - 0.5;
+		const double a1 = synth_unit(model_seed, 5, 2 * j + 1) - 0.5;
+		s0 = s0 + a0;
+		s1 = s1 + a1;
+		q0 = q0 + a0 * a0;
+		q1 = q1 + a1 * a1;
+	}
+	const double t = 0.5 * (s0 * s0 - q0) + 0.5 * (s1 * s1 - q1);
+	const double noise = synth_unit(seed, 4, R) - 0.5;
+	double y = rint(((3.0 + gains[2 * (L - lo)] * s) + gains[2 * (L - lo) + 1] * t) + 1.5 * noise);
+	y = y < 1.0 ? 1.0 : (y > 5.0 ? 5.0 : y);
+	target[r] = (float)y;
+}
+
+__global__ void k_mh_keys(const uint2 *csr, uint64_t nnz, uint32_t *keys, uint32_t *vals)
+{
+	const uint64_t p = (uint64_t)blockIdx.x * 256u + threadIdx.x;
+	if (p >= nnz) return;
+	keys[p] = csr[p].x;
+	vals[p] = (uint32_t)p;
+}
+
+// CSC entries from the entries sorted (stably) by feature: {row, x} of entry p
+__global__ void k_mh_scatter(const uint32_t *sorted_p, const uint2 *csr, const uint32_t *row_of, uint64_t nnz, uint2 *csc)
+{
+	const uint64_t q = (uint64_t)blockIdx.x * 256u + threadIdx.x;
+	if (q >= nnz) return;
+	const uint32_t p = sorted_p[q];
+	csc[q] = make_uint2(row_of[p], csr[p].y);
+}
+
 __global__ void k_count_features(const uint2 *csr, uint64_t nnz, unsigned long long *counts)
 {
 	const uint64_t i = (uint64_t)blockIdx.x * 256u + threadIdx.x;
@@ -1421,6 +1479,36 @@ hipError_t synth_field_scatter(const uint32_t *sorted_rows, const uint2 *csr, ui
 {
 	if (n == 0) return hipSuccess;
 	k_synth_field_scatter<<<grid_for(n), 256, 0, s>>>(sorted_rows, csr, n, F, field, out);
+	return hipGetLastError();
+}
+
+hipError_t synth_mh_len(uint32_t n, uint32_t lo, uint32_t hi, uint64_t seed, uint64_t row0, uint64_t *len, hipStream_t s)
+{
+	k_mh_len<<<grid_for((uint64_t)n + 1), 256, 0, s>>>(n, lo, hi, seed, row0, len);
+	return hipGetLastError();
+}
+
+hipError_t synth_mh_fill(uint32_t n, uint32_t D, uint64_t seed, int xmode, uint64_t model_seed, uint64_t row0,
+                         const double *gains, uint32_t lo, const uint64_t *row_ptr, uint2 *csr, uint32_t *row_of,
+                         float *target, hipStream_t s)
+{
+	if (n == 0) return hipSuccess;
+	k_mh_fill<<<grid_for(n), 256, 0, s>>>(n, D, seed, xmode, model_seed, row0, gains, lo, row_ptr, csr, row_of, target);
+	return hipGetLastError();
+}
+
+hipError_t mh_keys(const uint2 *csr, uint64_t nnz, uint32_t *keys, uint32_t *vals, hipStream_t s)
+{
+	if (nnz == 0) return hipSuccess;
+	k_mh_keys<<<grid_for(nnz), 256, 0, s>>>(csr, nnz, keys, vals);
+	return hipGetLastError();
+}
+
+hipError_t synth_mh_scatter(const uint32_t *sorted_p, const uint2 *csr, const uint32_t *row_of, uint64_t nnz, uint2 *csc,
+                            hipStream_t s)
+{
+	if (nnz == 0) return hipSuccess;
+	k_mh_scatter<<<grid_for(nnz), 256, 0, s>>>(sorted_p, csr, row_of, nnz, csc);
 	return hipGetLastError();
 }
 

@@ -141,7 +141,7 @@ class HostData(C.Structure):
 
 # every symbol include/vbfm.h declares (checked by tests/test_capi_cpu.py)
 EXPORTS = ["vbfm_abi_version", "vbfm_last_error", "vbfm_create", "vbfm_destroy", "vbfm_set_train",
-           "vbfm_set_test", "vbfm_synth_generate", "vbfm_get_csc", "vbfm_get_shape", "vbfm_get_levels",
+           "vbfm_set_test", "vbfm_synth_generate", "vbfm_synth_multihot", "vbfm_get_csc", "vbfm_get_shape", "vbfm_get_levels",
            "vbfm_set_params", "vbfm_get_params", "vbfm_init_params_device", "vbfm_init_params_replay", "vbfm_init_caches", "vbfm_iterate", "vbfm_get_test_pred",
            "vbfm_step_w0", "vbfm_step_w", "vbfm_step_qcache", "vbfm_step_v", "vbfm_step_hyper",
            "vbfm_free_energy", "vbfm_get_rows", "vbfm_get_test_e", "vbfm_factor_sweep", "vbfm_set_profiling",
@@ -175,6 +175,8 @@ def lib():
         L.vbfm_set_test.argtypes = [V, C.POINTER(Csc)]
         L.vbfm_synth_generate.argtypes = [V, C.c_int32, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint64, C.c_int32,
                                           C.c_uint64, C.c_uint64]
+        L.vbfm_synth_multihot.argtypes = [V, C.c_int32, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint64,
+                                          C.c_int32, C.c_uint64, C.c_uint64]
         L.vbfm_get_csc.argtypes = [V, C.c_int32, P_u64, V, P_f32]
         L.vbfm_get_shape.argtypes = [V, C.c_int32, P_u32, P_u32, P_u64]
         L.vbfm_get_levels.argtypes = [V, P_u32, P_u32]
@@ -419,6 +421,16 @@ class FMLearnVB:
         planted model; rows [row_offset, row_offset + num_rows) of the one-rank data set."""
         _check(lib().vbfm_synth_generate(self._ctx, which, num_rows, n_fields, ids_per_field, seed, xmode,
                                          model_seed, row_offset), self._ctx)
+        if which == 0:
+            self.n_train = num_rows
+        else:
+            self.n_test = num_rows
+
+    def synth_multihot(self, which, num_rows, num_features, lo, hi, seed, xmode=0, model_seed=SYNTH_MODEL_SEED,
+                       row_offset=0):
+        """tests/synth.py generate_multihot on the device (rows of lo..hi distinct ids, no fields)."""
+        _check(lib().vbfm_synth_multihot(self._ctx, which, num_rows, num_features, lo, hi, seed, xmode, model_seed,
+                                         row_offset), self._ctx)
         if which == 0:
             self.n_train = num_rows
         else:

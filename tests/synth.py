@@ -147,3 +147,54 @@ def write_binary(base, n_feature, row_ptr, feat, val, y):
     with open(base + ".y", "wb") as fh:
         fh.write(np.array([1, 4, N], dtype="<u4").tobytes())
         fh.write(y.astype("<f4").tobytes())
+
+
+def generate_multihot(n_rows, n_features, lo, hi, seed, xmode=0, model_seed=MODEL_SEED, row_offset=0):
+    """Multi-hot rows without field structure (the device's vbfm_synth_multihot follows this):
+
+      L(R)    = lo + h_row(6, R) % (hi - lo + 1)                        (lo <= L <= hi <= 64)
+      id i    = a_i + h_row(7, 64 R + i) % (a_{i+1} - a_i),  a_i = floor(i D / L)
+                (one id per stratum: distinct and ascending within the row)
+      x       = 1.0f, or 0.5f + (h_row(2, 64 R + i) >> 40) * 2^-24 if xmode
+      s, t    = as generate() over the row's ids, with the raw bias u_model(3, j) - 0.5
+      y(R)    = clamp(rint(((3 + c_L s) + g_L t) + 1.5 (u_row(4, R) - 0.5)), 1, 5),
+                c_L = sqrt(12 / L), g_L = interaction_gain(L)
+    Return (row_ptr uint64[N+1], feat uint32[nnz], val float32[nnz], y float32[N])."""
+    N, D = int(n_rows), int(n_features)
+    R = np.arange(N, dtype=np.uint64) + np.uint64(int(row_offset))
+    L = (np.uint64(lo) + h(seed, 6, R) % np.uint64(hi - lo + 1)).astype(np.int64)
+    row_ptr = np.zeros(N + 1, dtype=np.uint64)
+    np.cumsum(L, out=row_ptr[1:])
+    nnz = int(row_ptr[-1])
+    row = np.repeat(np.arange(N, dtype=np.int64), L)
+    i = np.arange(nnz, dtype=np.int64) - row_ptr[:-1].astype(np.int64)[row]
+    Lr = L[row]
+    a = i * D // Lr
+    e = (i + 1) * D // Lr
+    key = R[row] * np.uint64(64) + i.astype(np.uint64)
+    feat = (a.astype(np.uint64) + h(seed, 7, key) % (e - a).astype(np.uint64)).astype(np.uint32)
+    if xmode:
+        val = (np.float32(0.5) + (h(seed, 2, key) >> np.uint64(40)).astype(np.float32)
+               * np.float32(2.0 ** -24)).astype(np.float32)
+    else:
+        val = np.ones(nnz, dtype=np.float32)
+    j = feat.astype(np.uint64)
+    b = _u(model_seed, 3, j) - 0.5
+    p0 = _u(model_seed, 5, 2 * j) - 0.5
+    p1 = _u(model_seed, 5, 2 * j + np.uint64(1)) - 0.5
+    s = np.zeros(N)
+    s0, s1, q0, q1 = (np.zeros(N) for _ in range(4))
+    for k in range(int(L.max()) if N else 0):   # the k-th entry of every row, in row order (sequential sums)
+        m = L > k
+        idx = row_ptr[:-1].astype(np.int64)[m] + k
+        s[m] = s[m] + b[idx]
+        s0[m] = s0[m] + p0[idx]
+        s1[m] = s1[m] + p1[idx]
+        q0[m] = q0[m] + p0[idx] * p0[idx]
+        q1[m] = q1[m] + p1[idx] * p1[idx]
+    t = 0.5 * (s0 * s0 - q0) + 0.5 * (s1 * s1 - q1)
+    cl = np.sqrt(12.0 / L)
+    gl = np.array([interaction_gain(int(x)) for x in range(0, 65)])[L]
+    noise = _u(seed, 4, R) - 0.5
+    y = np.clip(np.rint(((3.0 + cl * s) + gl * t) + 1.5 * noise), 1.0, 5.0).astype(np.float32)
+    return row_ptr, feat, val, y
