@@ -478,7 +478,10 @@ void build_schedule(vbfm_ctx *c)
 	build_lorder(c, cp, feats);
 }
 
-// segments of the hyper / free-energy sums: (w or factor f) x group, chunked by 64K attrs
+// segments of the hyper / free-energy sums: (w or factor f) x group. The attributes are
+// ordered by group (perm) and cut into chunks of 4096 inside a group; one chunk list serves
+// the w segments (one workgroup per chunk and segment) and the factors (one workgroup per
+// chunk for all k factors: k_vsums)
 void build_chunks(vbfm_ctx *c)
 {
 	std::vector<uint32_t> perm(c->D), gptr((size_t)c->G + 1, 0);
@@ -487,30 +490,59 @@ void build_chunks(vbfm_ctx *c)
 	std::vector<uint32_t> pos(gptr.begin(), gptr.end() - 1);
 	for (uint32_t i = 0; i < c->D; i++) perm[pos[c->group_h[i]]++] = i;
 	c->chunks_h.clear();
-	const uint32_t CH = 65536;
-	for (int f = -1; f < c->k; f++)
-		for (uint32_t g = 0; g < c->G; g++)
-			for (uint32_t b = gptr[g]; b < gptr[g + 1]; b += CH)
-				c->chunks_h.push_back(vbk::Chunk{b, std::min(b + CH, gptr[g + 1]), f, g});
+	std::vector<uint32_t> gchunk((size_t)c->G + 1, 0);
+	const uint32_t CH = 4096;
+	for (uint32_t g = 0; g < c->G; g++) {
+		gchunk[g] = (uint32_t)c->chunks_h.size();
+		for (uint32_t b = gptr[g]; b < gptr[g + 1]; b += CH)
+			c->chunks_h.push_back(vbk::Chunk{b, std::min(b + CH, gptr[g + 1]), -1, g});
+	}
+	gchunk[c->G] = (uint32_t)c->chunks_h.size();
+	const size_t nc = c->chunks_h.size();
 	c->perm_d = dalloc<uint32_t>(c->D);
 	if (c->D) HIPCHK(hipMemcpy(c->perm_d, perm.data(), c->D * 4, hipMemcpyHostToDevice));
-	c->chunks_d = dalloc<vbk::Chunk>(c->chunks_h.size());
-	if (!c->chunks_h.empty())
-		HIPCHK(hipMemcpy(c->chunks_d, c->chunks_h.data(), c->chunks_h.size() * sizeof(vbk::Chunk), hipMemcpyHostToDevice));
-	c->chunk_out_d = dalloc<double>(c->chunks_h.size());
+	c->chunks_d = dalloc<vbk::Chunk>(nc);
+	if (nc) HIPCHK(hipMemcpy(c->chunks_d, c->chunks_h.data(), nc * sizeof(vbk::Chunk), hipMemcpyHostToDevice));
+	c->gchunk_d = dalloc<uint32_t>(gchunk.size());
+	HIPCHK(hipMemcpy(c->gchunk_d, gchunk.data(), gchunk.size() * 4, hipMemcpyHostToDevice));
+	c->chunk_out_d = dalloc<double>(nc);
+	c->vpart_d = dalloc<double>(nc * (size_t)std::max(c->k, 1));
+	c->vseg_d = dalloc<double>((size_t)std::max(c->k, 1) * c->G);
 }
 
-// sum of chunk results per segment, in chunk order; seg index = (f+1)*G + g
-std::vector<double> param_sums(vbfm_ctx *c, int mode)
+// w: chunk results summed per group in chunk order on the host; factors: k_vsums (fixed
+// order on the device). seg index = (f+1)*G + g
+std::vector<double> seg_sums(vbfm_ctx *c, int model, int mode, const double *hw, const double *hv, bool want_w,
+                             bool want_v)
 {
 	const size_t nc = c->chunks_h.size();
-	HIPCHK(vbk::param_sums(c->ms_w, c->ms_v, c->perm_d, c->D, c->chunks_d, (uint32_t)nc, mode, c->hyp_w_d, c->hyp_v_d,
-	                       c->k, c->chunk_out_d, c->s));
-	std::vector<double> out(nc), seg((size_t)(c->k + 1) * c->G, 0.0);
-	if (nc) HIPCHK(hipMemcpyAsync(out.data(), c->chunk_out_d, nc * 8, hipMemcpyDeviceToHost, c->s));
+	const size_t G = c->G, kg = (size_t)c->k * G;
+	std::vector<double> out(nc), seg((size_t)(c->k + 1) * G, 0.0);
+	want_w = want_w && nc;
+	want_v = want_v && nc && kg;
+	if (want_w) {
+		if (model == 0)
+			HIPCHK(vbk::param_sums(c->ms_w, c->ms_v, c->perm_d, c->D, c->chunks_d, (uint32_t)nc, mode, hw, hv, c->k,
+			                       c->chunk_out_d, c->s));
+		else
+			HIPCHK(vbk::mc_param_sums(c->ms_w, c->ms_v, c->perm_d, c->chunks_d, (uint32_t)nc, mode, hw, hv, c->k,
+			                          c->chunk_out_d, c->s));
+		HIPCHK(hipMemcpyAsync(out.data(), c->chunk_out_d, nc * 8, hipMemcpyDeviceToHost, c->s));
+	}
+	if (want_v) {
+		HIPCHK(vbk::vsums(c->ms_v, c->perm_d, c->chunks_d, (uint32_t)nc, c->gchunk_d, c->G, model, mode, hv, c->k,
+		                  c->vpart_d, c->vseg_d, c->s));
+		HIPCHK(hipMemcpyAsync(seg.data() + G, c->vseg_d, kg * 8, hipMemcpyDeviceToHost, c->s));
+	}
 	sync(c);
-	for (size_t i = 0; i < nc; i++) seg[(size_t)(c->chunks_h[i].f + 1) * c->G + c->chunks_h[i].g] += out[i];
+	if (want_w)
+		for (size_t i = 0; i < nc; i++) seg[c->chunks_h[i].g] += out[i];
 	return seg;
+}
+
+std::vector<double> param_sums(vbfm_ctx *c, int mode)
+{
+	return seg_sums(c, 0, mode, c->hyp_w_d, c->hyp_v_d, true, true);
 }
 
 void upload_hyp(vbfm_ctx *c)
@@ -894,7 +926,7 @@ void vbfm_destroy(vbfm_ctx *c)
 	dfree(c->rows); dfree(c->scratch_n); dfree(c->e_test); dfree(c->pred_test);
 	dfree(c->ms_v); dfree(c->ms_w); dfree(c->hyp_w_d); dfree(c->hyp_v_d); dfree(c->group_d);
 	dfree(c->level_feats); dfree(c->dup); dfree(c->red_d); dfree(c->perm_d); dfree(c->chunks_d);
-	dfree(c->chunk_out_d); dfree(c->counters); dfree(c->stats);
+	dfree(c->chunk_out_d); dfree(c->gchunk_d); dfree(c->vpart_d); dfree(c->vseg_d); dfree(c->counters); dfree(c->stats);
 	dfree(c->rows_alt); dfree(c->lcp); dfree(c->lx); dfree(c->lnext); dfree(c->lrow0); dfree(c->lpos0);
 	fs_free(c);
 	mc_free(c);

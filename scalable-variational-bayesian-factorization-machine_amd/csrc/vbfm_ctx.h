@@ -112,8 +112,11 @@ struct vbfm_ctx {
 	std::vector<double> red_h;
 	uint32_t *perm_d = nullptr;
 	vbk::Chunk *chunks_d = nullptr;
-	std::vector<vbk::Chunk> chunks_h;
-	double *chunk_out_d = nullptr;
+	std::vector<vbk::Chunk> chunks_h;   // attribute chunks, group by group (build_chunks)
+	uint32_t *gchunk_d = nullptr;       // [G+1] each group's chunk range
+	double *chunk_out_d = nullptr;      // [chunks] w partials
+	double *vpart_d = nullptr;          // [chunks * k] factor partials
+	double *vseg_d = nullptr;           // [k * G] factor sums
 	uint32_t *counters = nullptr;
 	// row-sharded multi-GPU
 	int nranks = 1, rank = 0;
@@ -225,6 +228,11 @@ void step_qcache(vbfm_ctx *c, int f);
 void step_v(vbfm_ctx *c, int f);
 double rows_energy(vbfm_ctx *c);
 std::vector<double> param_sums(vbfm_ctx *c, int mode);
+// the per-(w | factor f, group g) segment sums at [(f + 1) * G + g]; model 0: VB, 1: MCMC
+// (their modes: param_sums / mc_param_sums; hw [G] / hv [G*k] their mode-1 constants); a
+// segment not wanted is left 0
+std::vector<double> seg_sums(vbfm_ctx *c, int model, int mode, const double *hw, const double *hv, bool want_w,
+                             bool want_v);
 double free_energy(vbfm_ctx *c, double energy);
 void test_predict(vbfm_ctx *c, hipStream_t s);
 void read_counters(vbfm_ctx *c, vbfm_iter_stats *o);

@@ -233,6 +233,12 @@ struct Chunk { uint32_t begin, end; int32_t f; uint32_t g; };
 hipError_t param_sums(const double2 *ms_w, const double2 *ms_v, const uint32_t *perm, uint32_t D,
                       const Chunk *chunks, uint32_t nchunks, int mode, const double *hyp_w,
                       const double *hyp_v, int k, double *out, hipStream_t s);
+// the factors' segment sums in one coalesced pass over ms_v: chunks of one group's attributes
+// (Chunk::f unused), gchunk[G+1] = each group's chunk range; part[nchunks * k] per-chunk
+// partials, seg[f * G + g] the sums. model 0: VB (param_sums' modes), 1: MCMC (mc_param_sums')
+hipError_t vsums(const double2 *ms_v, const uint32_t *perm, const Chunk *chunks, uint32_t nchunks,
+                 const uint32_t *gchunk, uint32_t G, int model, int mode, const double *hv, int k, double *part,
+                 double *seg, hipStream_t s);
 // level schedule
 hipError_t level_init(uint32_t *level, uint32_t nf, hipStream_t s);
 hipError_t level_relax(const uint64_t *row_ptr, const uint2 *csr, uint32_t n, uint32_t nf, uint32_t *level,

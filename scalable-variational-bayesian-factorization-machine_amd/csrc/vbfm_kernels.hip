@@ -883,6 +883,74 @@ __global__ __launch_bounds__(BLOCK) void k_param_sums(const double2 *ms_w, const
 	if (threadIdx.x == 0) out[blockIdx.x] = s;
 }
 
+// The same sums over the factors, every factor of a chunk of one group's attributes in one
+// workgroup: ms_v is feature-major, so attribute j's {mu, sigma} of all k factors are one
+// contiguous run of 16k bytes, and P = 256 / k attributes are read side by side, one factor per
+// thread (coalesced, each byte of ms_v read once; the per-(f, g) chunk walk above reads every
+// 16-B pair on its own line, k times over the array). Per-factor partials of the chunk in a
+// fixed order: part[chunk * k + f].
+//   MODEL 0 (VB):   mode 0  mu^2 + sigma                               (fm_learn_vb.h:477-497)
+//                   mode 1  the free-energy term with h = hyp_v[g][f]   (:665-676)
+//   MODEL 1 (MCMC): mode 0  v ; mode 1 (v - h)^2 with h = v_mu[g][f]   (fm_learn_mcmc.h:1010-1089)
+template <int MODEL>
+__global__ __launch_bounds__(256) void k_vsums(const double2 *ms_v, const uint32_t *perm, const vbk::Chunk *chunks,
+                                               int mode, const double *hv, int k, double *part)
+{
+	__shared__ double lds[256];
+	const vbk::Chunk c = chunks[blockIdx.x];
+	for (int fb = 0; fb < k; fb += 256) {
+		const int kk = min(k - fb, 256);
+		const int P = 256 / kk;
+		const int sub = (int)threadIdx.x / kk;
+		const int f = fb + (int)threadIdx.x % kk;
+		double s = 0.0;
+		if (sub < P) {
+			const double h = mode == 0 ? 0.0 : hv[(size_t)c.g * k + f];
+#pragma unroll 4
+			for (uint32_t i = c.begin + sub; i < c.end; i += P) {
+				const double2 m = ms_v[(size_t)perm[i] * k + f];
+				if constexpr (MODEL == 0) {
+					if (mode == 0) s += m.x * m.x + m.y;
+					else s += -0.5 * h * (m.x * m.x + m.y) + 0.5 * log(m.y * h) + .5;
+				} else {
+					s += mode == 0 ? m.x : (m.x - h) * (m.x - h);
+				}
+			}
+		}
+		lds[threadIdx.x] = s;
+		__syncthreads();
+		if ((int)threadIdx.x < kk) {
+			double t = lds[threadIdx.x];
+			for (int p = 1; p < P; ++p) t += lds[p * kk + threadIdx.x];
+			part[(size_t)blockIdx.x * k + f] = t;
+		}
+		__syncthreads();
+	}
+}
+
+// seg[f * G + g] = group g's chunk partials of factor f summed in a fixed order (16 strided
+// runs of chunks, then the 16 run sums in order); 64 factors per 1024-thread workgroup
+__global__ __launch_bounds__(1024) void k_vsums_finish(const double *part, const uint32_t *gchunk, int k, uint32_t G,
+                                                       double *seg)
+{
+	__shared__ double lds[1024];
+	const uint32_t g = blockIdx.y;
+	const int fl = (int)threadIdx.x % 64, sub = (int)threadIdx.x / 64;
+	const int f = (int)blockIdx.x * 64 + fl;
+	double s = 0.0;
+	if (f < k) {
+#pragma unroll 4
+		for (uint32_t ch = gchunk[g] + sub; ch < gchunk[g + 1]; ch += 16) s += part[(size_t)ch * k + f];
+	}
+	lds[threadIdx.x] = s;
+	__syncthreads();
+	if (sub == 0 && f < k) {
+		double t = lds[fl];
+		for (int p = 1; p < 16; ++p) t += lds[p * 64 + fl];
+		seg[(size_t)f * G + g] = t;
+	}
+}
+
 // ------------------------------------------------------------------------------------
 // dependency levels: relax level[b] >= level[a] + 1 over consecutive distinct features
 // a < b of every row until nothing changes (least fixed point = longest-path levels).
@@ -1398,6 +1466,17 @@ hipError_t param_sums(const double2 *ms_w, const double2 *ms_v, const uint32_t *
 {
 	if (nchunks == 0) return hipSuccess;
 	k_param_sums<256><<<nchunks, 256, 0, s>>>(ms_w, ms_v, perm, D, chunks, mode, hyp_w, hyp_v, k, out);
+	return hipGetLastError();
+}
+
+hipError_t vsums(const double2 *ms_v, const uint32_t *perm, const Chunk *chunks, uint32_t nchunks,
+                 const uint32_t *gchunk, uint32_t G, int model, int mode, const double *hv, int k, double *part,
+                 double *seg, hipStream_t s)
+{
+	if (nchunks == 0 || k <= 0 || G == 0) return hipSuccess;
+	if (model == 0) k_vsums<0><<<nchunks, 256, 0, s>>>(ms_v, perm, chunks, mode, hv, k, part);
+	else k_vsums<1><<<nchunks, 256, 0, s>>>(ms_v, perm, chunks, mode, hv, k, part);
+	k_vsums_finish<<<dim3((unsigned)(k + 63) / 64, G), 1024, 0, s>>>(part, gchunk, k, G, seg);
 	return hipGetLastError();
 }
 

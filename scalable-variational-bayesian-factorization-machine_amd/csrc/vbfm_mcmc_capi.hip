@@ -117,17 +117,10 @@ void apply_regular(vbfm_ctx *c, const double *reg, int n)
 }
 
 // per-(w | factor f, group g) sums of the parameters, mode 0: sum p, 1: sum (p - mu)^2;
-// segment index (f + 1) * G + g, chunk results added in chunk order
-std::vector<double> mc_param_sums(vbfm_ctx *c, int mode)
+// segment index (f + 1) * G + g (seg_sums); only the w or only the factor segments
+std::vector<double> mc_param_sums(vbfm_ctx *c, int mode, bool is_v)
 {
-	const size_t nc = c->chunks_h.size();
-	HIPCHK(vbk::mc_param_sums(c->ms_w, c->ms_v, c->perm_d, c->chunks_d, (uint32_t)nc, mode, d_w_mu(c), d_v_mu(c), c->k,
-	                          c->chunk_out_d, c->s));
-	std::vector<double> out(nc), seg((size_t)(c->k + 1) * c->G, 0.0);
-	if (nc) HIPCHK(hipMemcpyAsync(out.data(), c->chunk_out_d, nc * 8, hipMemcpyDeviceToHost, c->s));
-	sync(c);
-	for (size_t i = 0; i < nc; i++) seg[(size_t)(c->chunks_h[i].f + 1) * c->G + c->chunks_h[i].g] += out[i];
-	return seg;
+	return seg_sums(c, 1, mode, d_w_mu(c), d_v_mu(c), !is_v, is_v);
 }
 
 double mc_row_sum(vbfm_ctx *c, int mode, double w0)
@@ -192,13 +185,13 @@ void draw_w_hyper(vbfm_ctx *c)
 		upload_hyper(c);
 		return;
 	}
-	const std::vector<double> sq = mc_param_sums(c, 1);   // sum (w - w_mu(g))^2
+	const std::vector<double> sq = mc_param_sums(c, 1, false);   // sum (w - w_mu(g))^2
 	for (uint32_t g = 0; g < c->G; g++) {
 		const double gam = BETA_0 * (m.w_mu[g] - MU_0) * (m.w_mu[g] - MU_0) + GAMMA_0 + sq[g];
 		const double shape = ALPHA_0 + c->per_group[g] + 1;
 		if (!draw_lambda(m, shape, gam, m.w_lambda[g], &m.hc[HC_NAN_WL], &m.hc[HC_INF_WL])) break;
 	}
-	const std::vector<double> sum = mc_param_sums(c, 0);  // sum w
+	const std::vector<double> sum = mc_param_sums(c, 0, false);  // sum w
 	for (uint32_t g = 0; g < c->G; g++) {
 		const double mean = (sum[g] + BETA_0 * MU_0) / (c->per_group[g] + BETA_0);
 		const double s2 = (double)1.0 / ((c->per_group[g] + BETA_0) * m.w_lambda[g]);
@@ -216,7 +209,7 @@ void draw_v_hyper(vbfm_ctx *c)
 		upload_hyper(c);
 		return;
 	}
-	const std::vector<double> sq = mc_param_sums(c, 1);   // sum (v_f - v_mu(g, f))^2
+	const std::vector<double> sq = mc_param_sums(c, 1, true);   // sum (v_f - v_mu(g, f))^2
 	[&] {
 		for (int f = 0; f < k; f++)
 			for (uint32_t g = 0; g < c->G; g++) {
@@ -227,7 +220,7 @@ void draw_v_hyper(vbfm_ctx *c)
 					return;
 			}
 	}();
-	const std::vector<double> sum = mc_param_sums(c, 0);
+	const std::vector<double> sum = mc_param_sums(c, 0, true);
 	[&] {
 		for (int f = 0; f < k; f++)
 			for (uint32_t g = 0; g < c->G; g++) {

@@ -398,6 +398,100 @@ def test_long_columns_split_into_segments(k1, monkeypatch):
     close(res["seg"][2], o.params()["mu_v"])
 
 
+def _skewed_two_fields(n, U, I, seed, onehot):
+    rng = np.random.default_rng(seed)
+    u = rng.integers(0, U, n).astype(np.uint32)
+    it = ((rng.zipf(1.4, n) - 1) % I).astype(np.uint32)
+    f = np.empty(2 * n, np.uint32); f[0::2] = u; f[1::2] = U + it
+    v = np.ones(2 * n, np.float32) if onehot else (0.5 + rng.random(2 * n)).astype(np.float32)
+    y = rng.integers(1, 6, n).astype(np.float32)
+    return np.arange(0, 2 * n + 1, 2, dtype=np.uint64), f, v, y, it
+
+
+COUNTERS = ("nan_mu_w", "nan_sigma_w", "inf_mu_w", "nan_mu_v", "nan_sigma_v", "inf_mu_v", "nan_alpha")
+
+
+@pytest.mark.parametrize("case", ["onehot", "dup", "nan"])
+def test_long_column_segments_edge_cases(case, monkeypatch):
+    """The long-column segment kernels (k_lord_long_* / k_col_long_*) on the inputs the
+    parametrised skew test does not cover, each against the oracle and against one
+    workgroup per column (VBFM_LONG=0) on every layout that applies:
+      * onehot: every x is 1.0f, so the level store keeps no x array (lx elided);
+      * dup: rows of the popular items list the item twice (a libfm line with a repeated
+        feature): the column layout keeps those columns on the sequential path;
+      * nan: one row of the most popular item has a NaN target (the reference parses "nan"),
+        so that column's (and the row's user column's) posterior is NaN in every sweep: the
+        guard (fm_learn_vb.h:597-619) restores mu and skips the correction, the counters
+        count it once per column, alpha turns NaN and the hyper step returns early."""
+    n, U, I, k = 60000, 5000, 400, 3
+    rp, f, v, y, it = _skewed_two_fields(n, U, I, 17, case == "onehot")
+    top = int(np.argmax(np.bincount(it)))
+    assert np.bincount(it).max() > 2 * 8192
+    k0 = 1
+    if case == "dup":
+        # every 3rd row of the top item lists it twice: rows of 2 or 3 entries
+        rows = [list(f[2 * r:2 * r + 2]) for r in range(n)]
+        vals = [list(v[2 * r:2 * r + 2]) for r in range(n)]
+        for r in np.flatnonzero(it == top)[::3]:
+            rows[r].append(rows[r][1]); vals[r].append(np.float32(0.75))
+        f = np.concatenate([np.asarray(x, np.uint32) for x in rows])
+        v = np.concatenate([np.asarray(x, np.float32) for x in vals])
+        rp = np.concatenate([[0], np.cumsum([len(x) for x in rows])]).astype(np.uint64)
+    if case == "nan":
+        y = y.copy()
+        y[np.flatnonzero(it == top)[7]] = np.nan
+        k0 = 0   # update_w0 has no guard: a NaN row would reach every row through mu_0
+    nt = 2000
+    rt, ftu, vtt, yt, _ = _skewed_two_fields(nt, U, I, 18, case == "onehot")
+    D = U + I + 1
+    variants = [("column_seg", {"VBFM_LAYOUT": "column"}), ("column_noseg", {"VBFM_LAYOUT": "column", "VBFM_LONG": "0"})]
+    if case != "dup":
+        variants += [("level_seg", {"VBFM_LAYOUT": "level"}), ("level_noseg", {"VBFM_LAYOUT": "level", "VBFM_LONG": "0"})]
+    res = {}
+    for name, env in variants:
+        for kk in ("VBFM_LONG", "VBFM_LAYOUT"):
+            monkeypatch.delenv(kk, raising=False)
+        for kk, vv in env.items():
+            monkeypatch.setenv(kk, vv)
+        g = vbfm.FMLearnVB(k0, 1, k, D, min_target=1.0, max_target=5.0)
+        g.init(5, 0.1)
+        g.set_data(vbfm.DataSubset.from_csr(rp, f, v, y, U + I), vbfm.DataSubset.from_csr(rt, ftu, vtt, yt, U + I))
+        g.init_caches()
+        st = [g.iterate() for _ in range(2)]
+        res[name] = dict(rmse=[s.rmse for s in st], mae=[s.mae for s in st], quirk=[s.train_quirk for s in st],
+                         fe_valid=[s.free_energy_valid for s in st],
+                         fe=[s.free_energy for s in st if s.free_energy_valid],
+                         cnt=[[getattr(s, c) for c in COUNTERS] for s in st],
+                         mu_v=g.get_params()["mu_v"], layout=g.layout())
+        g.close()
+    for name, env in variants:
+        assert res[name]["layout"] == env["VBFM_LAYOUT"]
+    o = oc.VB(k0, 1, k, D)
+    o.init_params(5, 0.1)
+    o.attach(oc.Data(csr=(n, rp, f, v, y)), oc.Data(csr=(nt, rt, ftu, vtt, yt)))
+    o.init_caches()
+    for i in range(2):
+        ro, mo, qo = o.iterate()
+        cnt = [getattr(o.s, c) for c in COUNTERS]
+        for name, _ in variants:
+            r = res[name]
+            assert abs(r["rmse"][i] - ro) <= REL * ro, (name, i)
+            assert abs(r["mae"][i] - mo) <= REL * mo, (name, i)
+            assert abs(r["quirk"][i] - qo) <= REL * qo, (name, i)
+            assert r["cnt"][i] == cnt, (name, i, r["cnt"][i], cnt)
+            assert r["fe_valid"][i] == (0 if o.s.hyper_skipped else 1), (name, i)
+            if not o.s.hyper_skipped:
+                close(r["fe"][i], o.s.last_free_energy)
+    if case == "nan":
+        assert o.s.hyper_skipped and o.s.nan_mu_v >= 2 * k and o.s.nan_alpha == 1
+    else:
+        assert not o.s.hyper_skipped and o.s.nan_mu_v == 0
+    for name, _ in variants:
+        close(res[name]["mu_v"], o.params()["mu_v"])
+        close(res[name]["mu_v"], res[variants[0][0]]["mu_v"], 1e-12)
+        close(res[name]["fe"], res[variants[0][0]]["fe"], 1e-12)
+
+
 def test_level_layout_refused_when_levels_incomplete():
     """tiny has rows of different lengths: a level misses rows, the level layout cannot
     apply -- auto falls back to the column layout, an explicit request fails loudly."""
