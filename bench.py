@@ -363,9 +363,14 @@ def main():
                   "k_mc_v_level": "k_mc_v_level stats + all-reduce + draw (per level)"}.get(kernel, kernel)
     tf = os.path.join(ROOT, "profiles", "traffic_%s_%s%s.json" % (args.config, layout,
                                                                    "_" + args.method if mc or online else ""))
+    traffic_source = None
     if os.path.exists(tf) and not split:
+        # PMC counters cannot be read inside this timed run: the traffic comes from the
+        # rocprofv3 --pmc passes of an earlier run of this bench configuration (named here)
         with open(tf) as fh:
-            traffic = json.load(fh).get("bytes_per_launch")
+            tj = json.load(fh)
+        traffic = tj.get("bytes_per_launch")
+        traffic_source = "%s (earlier PMC profile: %s)" % (os.path.relpath(tf, ROOT), tj.get("source", "?").split(" (")[0])
     result = {
         "metric": METRIC, "value": value, "unit": "nnz*k/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": elapsed * 1000.0 / args.steps, "higher_is_better": True,
@@ -386,7 +391,7 @@ def main():
                    "row_layout": ("level (per mini-batch)" if stats[-1].n_lord_batches else "column") if online
                    else layout},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_source,
                      "kernel": kernel, "avg_launch_ms": avg_ms,
                      "launches": n_launch, "bytes_per_launch": bytes_per_launch},
         "factor_sweep_ms_per_step": sweep_ms,
