@@ -184,6 +184,18 @@ int vbfm_get_layout(vbfm_ctx *ctx, int32_t *layout);
 /* per-launch event timing of the sweep kernels inside vbfm_iterate (off by default) */
 int vbfm_set_profiling(vbfm_ctx *ctx, int32_t on);
 
+/* ---- checkpoint / resume ----------------------------------------------------------------
+ * No reference counterpart: the reference always starts from its initial draws
+ * (num_complete_iter = 0, fm_learn_vb_simultaneous.h:20) and keeps no state on disk. The VB
+ * learner's state between two vbfm_iterate calls -- {mu, sigma} of w and v, the hyper
+ * parameters, alpha, sigma_0, mu_0_dash, sigma_0_dash and this rank's train row caches -- goes
+ * to one file. vbfm_load_state, on a context created with the same configuration, rank and
+ * train data (checked: shape and a fingerprint of the train CSC and targets; the test set is
+ * free), replaces vbfm_init_caches and the run continues bit for bit. iter: the caller's
+ * iteration count, stored and returned. VB learner (vbfm_iterate) only. */
+int vbfm_save_state(vbfm_ctx *ctx, const char *path, uint32_t iter);
+int vbfm_load_state(vbfm_ctx *ctx, const char *path, uint32_t *iter);
+
 /* ---- the factor sweep alone (the metric's timed unit: q-cache + v sweep, all factors) -- */
 int vbfm_factor_sweep(vbfm_ctx *ctx, double *ms_device);
 

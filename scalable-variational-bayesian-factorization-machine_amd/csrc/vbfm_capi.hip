@@ -479,9 +479,10 @@ void build_schedule(vbfm_ctx *c)
 }
 
 // segments of the hyper / free-energy sums: (w or factor f) x group. The attributes are
-// ordered by group (perm) and cut into chunks of 4096 inside a group; one chunk list serves
-// the w segments (one workgroup per chunk and segment) and the factors (one workgroup per
-// chunk for all k factors: k_vsums)
+// ordered by group (perm) and cut into chunks inside a group, ~2048 of them for a large D
+// (256..4096 attributes each: enough workgroups to keep the loads in flight); one chunk list
+// serves the w segments (one workgroup per chunk) and the factors (one workgroup per chunk for
+// all k factors: k_vsums)
 void build_chunks(vbfm_ctx *c)
 {
 	std::vector<uint32_t> perm(c->D), gptr((size_t)c->G + 1, 0);
@@ -491,7 +492,7 @@ void build_chunks(vbfm_ctx *c)
 	for (uint32_t i = 0; i < c->D; i++) perm[pos[c->group_h[i]]++] = i;
 	c->chunks_h.clear();
 	std::vector<uint32_t> gchunk((size_t)c->G + 1, 0);
-	const uint32_t CH = 4096;
+	const uint32_t CH = std::min<uint32_t>(4096, std::max<uint32_t>(256, (c->D + 2047) / 2048));
 	for (uint32_t g = 0; g < c->G; g++) {
 		gchunk[g] = (uint32_t)c->chunks_h.size();
 		for (uint32_t b = gptr[g]; b < gptr[g + 1]; b += CH)
@@ -505,9 +506,9 @@ void build_chunks(vbfm_ctx *c)
 	if (nc) HIPCHK(hipMemcpy(c->chunks_d, c->chunks_h.data(), nc * sizeof(vbk::Chunk), hipMemcpyHostToDevice));
 	c->gchunk_d = dalloc<uint32_t>(gchunk.size());
 	HIPCHK(hipMemcpy(c->gchunk_d, gchunk.data(), gchunk.size() * 4, hipMemcpyHostToDevice));
-	c->chunk_out_d = dalloc<double>(nc);
+	c->chunk_out_d = dalloc<double>(nc + (size_t)c->k * c->G);   // w partials, then the factor sums
+	c->vseg_d = c->chunk_out_d + nc;
 	c->vpart_d = dalloc<double>(nc * (size_t)std::max(c->k, 1));
-	c->vseg_d = dalloc<double>((size_t)std::max(c->k, 1) * c->G);
 }
 
 // w: chunk results summed per group in chunk order on the host; factors: k_vsums (fixed
@@ -517,7 +518,7 @@ std::vector<double> seg_sums(vbfm_ctx *c, int model, int mode, const double *hw,
 {
 	const size_t nc = c->chunks_h.size();
 	const size_t G = c->G, kg = (size_t)c->k * G;
-	std::vector<double> out(nc), seg((size_t)(c->k + 1) * G, 0.0);
+	std::vector<double> out(nc + kg), seg((size_t)(c->k + 1) * G, 0.0);
 	want_w = want_w && nc;
 	want_v = want_v && nc && kg;
 	if (want_w) {
@@ -527,16 +528,17 @@ std::vector<double> seg_sums(vbfm_ctx *c, int model, int mode, const double *hw,
 		else
 			HIPCHK(vbk::mc_param_sums(c->ms_w, c->ms_v, c->perm_d, c->chunks_d, (uint32_t)nc, mode, hw, hv, c->k,
 			                          c->chunk_out_d, c->s));
-		HIPCHK(hipMemcpyAsync(out.data(), c->chunk_out_d, nc * 8, hipMemcpyDeviceToHost, c->s));
 	}
-	if (want_v) {
+	if (want_v)
 		HIPCHK(vbk::vsums(c->ms_v, c->perm_d, c->chunks_d, (uint32_t)nc, c->gchunk_d, c->G, model, mode, hv, c->k,
 		                  c->vpart_d, c->vseg_d, c->s));
-		HIPCHK(hipMemcpyAsync(seg.data() + G, c->vseg_d, kg * 8, hipMemcpyDeviceToHost, c->s));
-	}
+	// one copy of what was computed: [w partials | factor sums]
+	const size_t lo = want_w ? 0 : nc, hi = want_v ? nc + kg : nc;
+	if (hi > lo) HIPCHK(hipMemcpyAsync(out.data() + lo, c->chunk_out_d + lo, (hi - lo) * 8, hipMemcpyDeviceToHost, c->s));
 	sync(c);
 	if (want_w)
 		for (size_t i = 0; i < nc; i++) seg[c->chunks_h[i].g] += out[i];
+	if (want_v) std::copy(out.begin() + nc, out.end(), seg.begin() + G);
 	return seg;
 }
 
@@ -926,7 +928,7 @@ void vbfm_destroy(vbfm_ctx *c)
 	dfree(c->rows); dfree(c->scratch_n); dfree(c->e_test); dfree(c->pred_test);
 	dfree(c->ms_v); dfree(c->ms_w); dfree(c->hyp_w_d); dfree(c->hyp_v_d); dfree(c->group_d);
 	dfree(c->level_feats); dfree(c->dup); dfree(c->red_d); dfree(c->perm_d); dfree(c->chunks_d);
-	dfree(c->chunk_out_d); dfree(c->gchunk_d); dfree(c->vpart_d); dfree(c->vseg_d); dfree(c->counters); dfree(c->stats);
+	dfree(c->chunk_out_d); c->vseg_d = nullptr; dfree(c->gchunk_d); dfree(c->vpart_d); dfree(c->counters); dfree(c->stats);
 	dfree(c->rows_alt); dfree(c->lcp); dfree(c->lx); dfree(c->lnext); dfree(c->lrow0); dfree(c->lpos0);
 	fs_free(c);
 	mc_free(c);
@@ -1353,6 +1355,173 @@ int vbfm_get_test_pred(vbfm_ctx *c, double *pred)
 	if (!c || !pred) return fail(c, "null argument");
 	return guarded(c, [&] {
 		if (c->te.n) HIPCHK(hipMemcpy(pred, c->pred_test, (size_t)c->te.n * 8, hipMemcpyDeviceToHost));
+	});
+}
+
+}  // extern "C"
+
+// ---- checkpoint / resume ---------------------------------------------------------------------
+// The reference always starts from its initial draws (num_complete_iter = 0,
+// fm_learn_vb_simultaneous.h:20) and keeps no state on disk. Between two vbfm_iterate calls the
+// VB learner's state is the parameters, the hyper parameters, the four scalars and the train
+// row records (row order; their q-cache slots are rebuilt inside the next sweeps, they are kept
+// only so that a resumed context holds the same bytes).
+namespace {
+
+struct StateHeader {
+	char magic[8];        // "VBFMST01"
+	uint32_t version;
+	int32_t k0, k1, k;
+	uint32_t D, G;
+	uint32_t n_train, nf_train;
+	uint64_t nnz_train;
+	uint64_t data_fp;     // fingerprint of the train CSC (col_ptr, entries) and targets
+	int32_t nranks, rank;
+	uint32_t iter;
+	uint32_t level_order; // the records were in level-0 order (data-set sums add them in that order)
+	uint64_t reserved[4];
+};
+static_assert(sizeof(StateHeader) == 104, "checkpoint header layout");
+constexpr char STATE_MAGIC[8] = {'V', 'B', 'F', 'M', 'S', 'T', '0', '1'};
+constexpr size_t IO_CHUNK = (size_t)64 << 20;
+
+uint64_t train_fingerprint(vbfm_ctx *c)
+{
+	unsigned long long *d = dalloc<unsigned long long>(1);
+	HIPCHK(hipMemsetAsync(d, 0, 8, c->s));
+	HIPCHK(vbk::fingerprint(c->tr.col_ptr, (uint64_t)c->tr.nf + 1, 8, 1, d, c->s));
+	HIPCHK(vbk::fingerprint(c->tr.csc, c->tr.nnz, 8, 2, d, c->s));
+	HIPCHK(vbk::fingerprint(c->tr.target, c->tr.n, 4, 3, d, c->s));
+	unsigned long long h = 0;
+	HIPCHK(hipMemcpyAsync(&h, d, 8, hipMemcpyDeviceToHost, c->s));
+	sync(c);
+	dfree(d);
+	return h;
+}
+
+StateHeader state_header(vbfm_ctx *c, uint32_t iter)
+{
+	StateHeader h;
+	memset(&h, 0, sizeof(h));
+	memcpy(h.magic, STATE_MAGIC, 8);
+	h.version = 1;
+	h.k0 = c->k0; h.k1 = c->k1; h.k = c->k;
+	h.D = c->D; h.G = c->G;
+	h.n_train = c->tr.n; h.nf_train = c->tr.nf; h.nnz_train = c->tr.nnz;
+	h.data_fp = train_fingerprint(c);
+	h.nranks = c->nranks; h.rank = c->rank;
+	h.iter = iter;
+	return h;
+}
+
+struct File {
+	FILE *f;
+	std::string path;
+	File(const char *p, const char *mode) : f(fopen(p, mode)), path(p)
+	{
+		if (!f) throw std::string("cannot open checkpoint file ") + p;
+	}
+	~File() { if (f) fclose(f); }
+	void write(const void *p, size_t n)
+	{
+		if (n && fwrite(p, 1, n, f) != n) throw std::string("short write to ") + path;
+	}
+	void read(void *p, size_t n)
+	{
+		if (n && fread(p, 1, n, f) != n) throw std::string("checkpoint file truncated: ") + path;
+	}
+};
+
+void dev_to_file(vbfm_ctx *c, File &f, const void *d, size_t bytes)
+{
+	std::vector<uint8_t> buf(std::min(bytes, IO_CHUNK));
+	for (size_t o = 0; o < bytes; o += IO_CHUNK) {
+		const size_t n = std::min(IO_CHUNK, bytes - o);
+		HIPCHK(hipMemcpyAsync(buf.data(), (const uint8_t *)d + o, n, hipMemcpyDeviceToHost, c->s));
+		sync(c);
+		f.write(buf.data(), n);
+	}
+}
+
+void file_to_dev(vbfm_ctx *c, File &f, void *d, size_t bytes)
+{
+	std::vector<uint8_t> buf(std::min(bytes, IO_CHUNK));
+	for (size_t o = 0; o < bytes; o += IO_CHUNK) {
+		const size_t n = std::min(IO_CHUNK, bytes - o);
+		f.read(buf.data(), n);
+		HIPCHK(hipMemcpyAsync((uint8_t *)d + o, buf.data(), n, hipMemcpyHostToDevice, c->s));
+		sync(c);
+	}
+}
+
+void require_vb_state(vbfm_ctx *c, const char *fn)
+{
+	if (c->mc || c->ov) throw std::string(fn) + ": the VB learner's state only (not MCMC / ALS / online)";
+	require_train(c);
+}
+
+}  // namespace
+
+extern "C" {
+
+int vbfm_save_state(vbfm_ctx *c, const char *path, uint32_t iter)
+{
+	if (!c || !path) return fail(c, "null argument");
+	return guarded(c, [&] {
+		require_vb_state(c, "vbfm_save_state");
+		StateHeader h = state_header(c, iter);
+		h.level_order = c->rows_lorder ? 1 : 0;
+		rows_row_order(c);
+		File f(path, "wb");
+		f.write(&h, sizeof(h));
+		dev_to_file(c, f, c->ms_w, (size_t)c->D * sizeof(double2));
+		dev_to_file(c, f, c->ms_v, (size_t)c->k * c->D * sizeof(double2));
+		f.write(c->hyp_w.data(), c->hyp_w.size() * 8);
+		f.write(c->hyp_v.data(), c->hyp_v.size() * 8);
+		const double sc[4] = {c->alpha, c->sigma_0, c->mu0, c->s0d};
+		f.write(sc, sizeof(sc));
+		dev_to_file(c, f, c->rows, (size_t)c->tr.n * sizeof(RowRec));
+		if (fflush(f.f) != 0) throw std::string("short write to ") + path;
+		if (h.level_order) rows_level_order(c);   // the run goes on exactly as without the save
+	});
+}
+
+int vbfm_load_state(vbfm_ctx *c, const char *path, uint32_t *iter)
+{
+	if (!c || !path) return fail(c, "null argument");
+	return guarded(c, [&] {
+		require_vb_state(c, "vbfm_load_state");
+		File f(path, "rb");
+		StateHeader h;
+		f.read(&h, sizeof(h));
+		if (memcmp(h.magic, STATE_MAGIC, 8) != 0 || h.version != 1)
+			throw std::string("not a libvbfm VB checkpoint: ") + path;
+		if (h.k0 != c->k0 || h.k1 != c->k1 || h.k != c->k || h.D != c->D || h.G != c->G)
+			throw std::string("checkpoint of another model configuration (-dim / num_attribute / groups)");
+		if (h.nranks != c->nranks || h.rank != c->rank)
+			throw std::string("checkpoint of another rank (each rank resumes from its own file)");
+		if (h.n_train != c->tr.n || h.nf_train != c->tr.nf || h.nnz_train != c->tr.nnz ||
+		    h.data_fp != train_fingerprint(c))
+			throw std::string("checkpoint of another train data set");
+		rows_row_order(c);
+		file_to_dev(c, f, c->ms_w, (size_t)c->D * sizeof(double2));
+		file_to_dev(c, f, c->ms_v, (size_t)c->k * c->D * sizeof(double2));
+		f.read(c->hyp_w.data(), c->hyp_w.size() * 8);
+		f.read(c->hyp_v.data(), c->hyp_v.size() * 8);
+		upload_hyp(c);
+		double sc[4];
+		f.read(sc, sizeof(sc));
+		c->alpha = sc[0]; c->sigma_0 = sc[1]; c->mu0 = sc[2]; c->s0d = sc[3];
+		file_to_dev(c, f, c->rows, (size_t)c->tr.n * sizeof(RowRec));
+		c->rows_lorder = false;
+		if (h.level_order) {
+			if (!c->lord) throw std::string("checkpoint of a level-ordered run: resume with the same row layout");
+			rows_level_order(c);
+		}
+		c->q_ready[0] = c->q_ready[1] = -1;
+		c->carry = 0;
+		sync(c);
+		if (iter) *iter = h.iter;
 	});
 }
 

@@ -116,7 +116,7 @@ struct vbfm_ctx {
 	uint32_t *gchunk_d = nullptr;       // [G+1] each group's chunk range
 	double *chunk_out_d = nullptr;      // [chunks] w partials
 	double *vpart_d = nullptr;          // [chunks * k] factor partials
-	double *vseg_d = nullptr;           // [k * G] factor sums
+	double *vseg_d = nullptr;           // [k * G] factor sums (inside chunk_out_d)
 	uint32_t *counters = nullptr;
 	// row-sharded multi-GPU
 	int nranks = 1, rank = 0;

@@ -94,7 +94,8 @@ struct LevelArgs {
 	int pend_kind;             // level 0 of a v sweep: the pending correction is the previous sweep's last
 	                           // level (1: v of the other q-cache slot, 2: w); 0: this sweep's own
 	// online VB (vbfm_online.hip): natural-gradient steps on a mini-batch; nat == nullptr: VB
-	double2 *nat;              // natural parameters {mu, sigma} of each feature, laid out like ms
+	double2 *nat;              // natural parameters {mu, sigma} of each feature: nat[j * nat_stride]
+	uint32_t nat_stride;       // 1: factor-major (nat_v + f * D), so a level's columns read one run
 	double *rho;               // step size of each feature (new_wj / new_vj)
 	const uint32_t *ccount;    // entries of each feature in the whole train set (col_count)
 	uint32_t *tcount;          // w: t_wj (+= batch entries, rho refreshed); v of factor 0: t_vj; else nullptr
@@ -151,6 +152,12 @@ struct McArgs {
 	const uint4 *lpay;         // as LevelArgs::lpay
 	const uint2 *lpay2;        // as LevelArgs::lpay2
 	int pending;               // bit 0: apply the previous level's correction; bit 1: nt loads
+	// the train re-prediction of draw_all's end (fm_learn_mcmc.h:117-348) accumulated inside the
+	// v sweeps: while factor f is swept, v_{f-1} is final, so every entry the sweep visits adds
+	// its factor-(f-1) terms to the row's record (mc_pred_acc); pk: 0 off, 1 sweep of factor 1
+	// (the accumulators start), 2 a later factor; par_prev = v_{f-1} (stride next_stride)
+	const double2 *par_prev;
+	int pk;
 };
 
 // kernels launched from the C-ABI layer (vbfm_kernels.hip)
@@ -239,6 +246,9 @@ hipError_t param_sums(const double2 *ms_w, const double2 *ms_v, const uint32_t *
 hipError_t vsums(const double2 *ms_v, const uint32_t *perm, const Chunk *chunks, uint32_t nchunks,
                  const uint32_t *gchunk, uint32_t G, int model, int mode, const double *hv, int k, double *part,
                  double *seg, hipStream_t s);
+// *out += an order-independent fingerprint of n words of 4 or 8 bytes (checkpoint data check)
+hipError_t fingerprint(const void *a, uint64_t n, int word_bytes, uint64_t salt, unsigned long long *out,
+                       hipStream_t s);
 // level schedule
 hipError_t level_init(uint32_t *level, uint32_t nf, hipStream_t s);
 hipError_t level_relax(const uint64_t *row_ptr, const uint2 *csr, uint32_t n, uint32_t nf, uint32_t *level,
@@ -306,6 +316,12 @@ hipError_t mc_lord_defer_flush(const McArgs &a, int is_w, uint32_t n, hipStream_
 // per-block sums over rows; mode 0: e*e ; mode 1: e - w0
 hipError_t mc_row_sums(const RowRec *rows, uint32_t n, int mode, double w0, double *out, uint32_t nblocks,
                        hipStream_t s);
+// the end of the fused train re-prediction: the last factor's and the w terms from the rows'
+// entries, yhat = E + Q2 (+ w0), then as mc_train_update (e = yhat - y, per block the clipped
+// squared error); pk_done: the v sweeps accumulated factors 0..k-2 into the records
+hipError_t mc_pred_final(const uint64_t *row_ptr, const uint2 *csr, const double2 *ms_v, const double2 *ms_w, int k,
+                         int k1, int k0, double w0, int pk_done, RowRec *rows, const uint32_t *pos, const float *target,
+                         uint32_t n, double mn, double mx, double *out, uint32_t nblocks, hipStream_t s);
 hipError_t mc_e_shift(RowRec *rows, uint32_t n, double d, hipStream_t s);
 hipError_t mc_train_update(RowRec *rows, const double *yhat, const float *target, uint32_t n, double mn, double mx,
                            double *out, uint32_t nblocks, const uint32_t *pos, hipStream_t s);

@@ -1002,6 +1002,18 @@ DEVI uint64_t hstream(uint64_t seed, uint64_t stream, uint64_t i)
 	return splitmix64(seed * 0x9E3779B97F4A7C15ull + stream * 0xD1B54A32D192ED03ull + i);
 }
 
+// order-independent 64-bit fingerprint of n words: the wrapping sum of splitmix64(word ^ f(index))
+// (integer, so the atomic sum is exact in any order)
+template <class W>
+__global__ __launch_bounds__(256) void k_fingerprint(const W *a, uint64_t n, uint64_t salt, unsigned long long *out)
+{
+	unsigned long long s = 0;
+	for (uint64_t i = (uint64_t)blockIdx.x * 256u + threadIdx.x; i < n; i += (uint64_t)gridDim.x * 256u)
+		s += splitmix64((uint64_t)a[i] ^ (i * 0xD1B54A32D192ED03ull + salt));
+	for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+	if ((threadIdx.x & 63) == 0) atomicAdd(out, s);
+}
+
 __global__ void k_synth_entries(uint32_t n, uint32_t F, uint32_t S, uint64_t seed, int xmode, uint64_t row0, uint2 *csr)
 {
 	const uint64_t idx = (uint64_t)blockIdx.x * 256u + threadIdx.x;
@@ -1466,6 +1478,16 @@ hipError_t param_sums(const double2 *ms_w, const double2 *ms_v, const uint32_t *
 {
 	if (nchunks == 0) return hipSuccess;
 	k_param_sums<256><<<nchunks, 256, 0, s>>>(ms_w, ms_v, perm, D, chunks, mode, hyp_w, hyp_v, k, out);
+	return hipGetLastError();
+}
+
+hipError_t fingerprint(const void *a, uint64_t n, int word_bytes, uint64_t salt, unsigned long long *out,
+                       hipStream_t s)
+{
+	if (n == 0) return hipSuccess;
+	const unsigned grid = (unsigned)std::min<uint64_t>(4096, (n + 255) / 256);
+	if (word_bytes == 8) k_fingerprint<uint64_t><<<grid, 256, 0, s>>>((const uint64_t *)a, n, salt, out);
+	else k_fingerprint<uint32_t><<<grid, 256, 0, s>>>((const uint32_t *)a, n, salt, out);
 	return hipGetLastError();
 }
 

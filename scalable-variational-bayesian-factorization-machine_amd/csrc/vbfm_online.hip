@@ -142,6 +142,16 @@ __global__ void k_ov_nat_init(const double2 *ms, size_t n, double2 *nat)
 	if (i < n) nat[i] = make_double2(ms[i].x / 0.02, 1 / ms[i].y);
 }
 
+// the same for v: ms_v feature-major [j][f] -> nat_v factor-major [f][j]
+__global__ void k_ov_nat_init_v(const double2 *ms, uint32_t k, uint32_t D, double2 *nat)
+{
+	const size_t i = (size_t)blockIdx.x * 256u + threadIdx.x;   // index in nat: f * D + j
+	if (i >= (size_t)k * D) return;
+	const size_t f = i / D, j = i % D;
+	const double2 m = ms[j * k + f];
+	nat[i] = make_double2(m.x / 0.02, 1 / m.y);
+}
+
 __global__ void k_ov_fill(double *p, uint32_t n, double v)
 {
 	const uint32_t i = blockIdx.x * 256u + threadIdx.x;
@@ -207,7 +217,7 @@ __global__ __launch_bounds__(256) void k_ov_v_level(LevelArgs a)
 		load_rec(a.rows, ent1.x & ROW_MASK, v1);
 	}
 	const size_t pi = (size_t)j * a.ms_stride;
-	const double2 msj = a.ms[pi], natj = a.nat[pi];
+	const double2 msj = a.ms[pi], natj = a.nat[(size_t)j * a.nat_stride];
 	const double mo = msj.x, so = msj.y;
 	const double rho = a.rho[j];
 	const uint32_t cc = a.ccount[j];
@@ -251,7 +261,7 @@ __global__ __launch_bounds__(256) void k_ov_v_level(LevelArgs a)
 		go = false;
 	}
 	if (leader) {
-		a.nat[pi] = make_double2(nmu, nsig);
+		a.nat[(size_t)j * a.nat_stride] = make_double2(nmu, nsig);
 		a.ms[pi] = make_double2(mu, sig);
 		if (a.tcount) a.tcount[j] += n;   // t_vj(i) += size at factor 0 (:396-399)
 	}
@@ -301,7 +311,7 @@ __global__ __launch_bounds__(256) void k_ov_w_level(LevelArgs a)
 	const uint32_t j = a.feats[col_i];
 	const uint2 *col = a.csc + cb;
 	const size_t pi = (size_t)j * a.ms_stride;
-	const double2 msj = a.ms[pi], natj = a.nat[pi];
+	const double2 msj = a.ms[pi], natj = a.nat[(size_t)j * a.nat_stride];
 	const double mo = msj.x, so = msj.y;
 	const double rho = a.rho[j];
 	const uint32_t cc = a.ccount[j];
@@ -339,7 +349,7 @@ __global__ __launch_bounds__(256) void k_ov_w_level(LevelArgs a)
 		go = false;
 	}
 	if (leader) {
-		a.nat[pi] = make_double2(nmu, nsig);
+		a.nat[(size_t)j * a.nat_stride] = make_double2(nmu, nsig);
 		a.ms[pi] = make_double2(mu, sig);
 		const uint32_t t = a.tcount[j] + n;
 		a.tcount[j] = t;
@@ -467,7 +477,7 @@ __global__ __launch_bounds__(256) void k_ov_lord(LevelArgs a)
 	const size_t pi = (size_t)j * a.ms_stride;
 	if (n) {   // every per-column load issued here, one dependent step after the feature id
 		msj = a.ms[pi];
-		natj = a.nat[pi];
+		natj = a.nat[(size_t)j * a.nat_stride];
 		rho = a.rho[j];
 		cc = a.ccount[j];
 		if (!a.hyp_uniform) hg = a.hyp[(size_t)a.attr_group[j] * a.hyp_stride];
@@ -539,7 +549,7 @@ __global__ __launch_bounds__(256) void k_ov_lord(LevelArgs a)
 			go = false;
 		}
 		if (leader) {
-			a.nat[pi] = make_double2(nmu, nsig);
+			a.nat[(size_t)j * a.nat_stride] = make_double2(nmu, nsig);
 			a.ms[pi] = make_double2(mu, sig);
 			if constexpr (IS_W) {
 				const uint32_t t = tc + n;
@@ -646,7 +656,10 @@ struct OvState {
 	uint32_t size = 0;             // size_except_last = ceil(N / num_batch)
 	vbrng::Glibc stream;           // the reference's rand() after the initial draws
 	std::vector<uint32_t> shuffle; // kept across epochs (:58-62)
-	double2 *nat_w = nullptr, *nat_v = nullptr;   // natural_{mu,sigma}_{w,v}_dash, laid out like ms_w / ms_v
+	double2 *nat_w = nullptr, *nat_v = nullptr;   // natural_{mu,sigma}_{w,v}_dash; nat_v factor-major [f][j]
+	                                              // (the reference's layout): a level's columns are
+	                                              // consecutive ids, so their natural parameters are one
+	                                              // coalesced run instead of one line per column
 	double *new_wj = nullptr, *new_vj = nullptr;
 	uint32_t *t_wj = nullptr, *t_vj = nullptr, *ccount = nullptr;
 	double nat_mu0 = 0.0, nat_sig0 = 0.0, new_w0 = 1.0;
@@ -711,7 +724,8 @@ void ov_free(vbfm_ctx *c)
 void ov_level_args(vbfm_ctx *c, LevelArgs &a, bool is_w, int f)
 {
 	OvState &o = *c->ov;
-	a.nat = is_w ? o.nat_w : o.nat_v + f;
+	a.nat = is_w ? o.nat_w : o.nat_v + (size_t)f * c->D;   // factor-major: the level's columns are one run
+	a.nat_stride = 1;
 	a.rho = is_w ? o.new_wj : o.new_vj;
 	a.ccount = o.ccount;
 	a.tcount = is_w ? o.t_wj : (f == 0 ? o.t_vj : nullptr);
@@ -994,7 +1008,7 @@ int vbfm_online_init(vbfm_ctx *c, const vbfm_online_config *cfg)
 				k_ov_ccount<<<grid_of(D), 256, 0, c->s>>>(c->tr.col_ptr, nf, D, o.ccount);
 				k_ov_nat_init<<<grid_of(D), 256, 0, c->s>>>(c->ms_w, D, o.nat_w);
 			}
-			if (kd) k_ov_nat_init<<<grid_of(kd), 256, 0, c->s>>>(c->ms_v, kd, o.nat_v);
+			if (kd) k_ov_nat_init_v<<<grid_of(kd), 256, 0, c->s>>>(c->ms_v, (uint32_t)c->k, c->D, o.nat_v);
 			HIPCHK(hipGetLastError());
 			o.t_w0 = 0;
 			o.new_w0 = std::pow((double)(T0 + o.t_w0), -LAMDA);
@@ -1199,7 +1213,7 @@ int vbfm_online_get_state(vbfm_ctx *c, double *nat_mu_w, double *nat_sigma_w, do
 		if (nat_mu_w) HIPCHK(hipMemcpy(nat_mu_w, tmp, (size_t)c->D * 8, hipMemcpyDeviceToHost));
 		if (nat_sigma_w) HIPCHK(hipMemcpy(nat_sigma_w, tmp + c->D, (size_t)c->D * 8, hipMemcpyDeviceToHost));
 		if (kd) {
-			HIPCHK(vbk::unpack_pairs(o.nat_v, tmp, tmp + kd, (uint32_t)c->k, c->D, c->s));
+			HIPCHK(vbk::unpack_pairs(o.nat_v, tmp, tmp + kd, 1, kd, c->s));   // already [f][j]
 			sync(c);
 			if (nat_mu_v) HIPCHK(hipMemcpy(nat_mu_v, tmp, kd * 8, hipMemcpyDeviceToHost));
 			if (nat_sigma_v) HIPCHK(hipMemcpy(nat_sigma_v, tmp + kd, kd * 8, hipMemcpyDeviceToHost));

@@ -420,6 +420,8 @@ int main(int argc, char **argv)
 		const std::string p_batch = cmd.reg("batch", "How many batches for online algorithm");
 		const std::string p_dev = cmd.reg("device", "HIP device ordinal; default=0");
 		const std::string p_vfile = cmd.reg("vfile", "write v_file.txt like the reference (1) or not (0); default=1");
+		const std::string p_save = cmd.reg("save_state", "vb: write the learner's state to this file after the last iteration");
+		const std::string p_resume = cmd.reg("resume", "vb: continue from a -save_state file (same data and -dim) instead of the initial draws");
 		if (cmd.has(p_help) || argc == 1) { cmd.print_help(); return 0; }
 		cmd.check();
 
@@ -486,15 +488,17 @@ int main(int argc, char **argv)
 		check(vbfm_set_test(ctx, &te), ctx);
 
 		// fm.init + fm.w.init_normal + fml->init draws (libfm.cpp:123-366): the same stream on
-		// the host (small models) or generated on the device (VBFM_INIT=host|replay overrides)
+		// the host (small models) or generated on the device (VBFM_INIT=host|replay overrides).
+		// -resume takes the state from its file instead (no draws, no v_file.txt)
+		const bool resume = cmd.has(p_resume);
 		const size_t kd = (size_t)k * D;
-		const bool vfile = cmd.geti(p_vfile, 1) != 0;
+		const bool vfile = cmd.geti(p_vfile, 1) != 0 && !resume;
 		const char *init_env = getenv("VBFM_INIT");
 		const bool replay = init_env ? std::string(init_env) == "replay" : kd + D >= 2000000;
-		std::vector<double> fm_v(vfile || !replay ? kd : 0);
-		if (replay) {
+		std::vector<double> fm_v(vfile || (!replay && !resume) ? kd : 0);
+		if (replay && !resume) {
 			check(vbfm_init_params_replay(ctx, seed, init_stdev, vfile ? fm_v.data() : nullptr, nullptr), ctx);
-		} else {
+		} else if (!resume) {
 			std::vector<double> mu_w(D), sig_w(D), mu_v(kd), sig_v(kd), hw(G), hv((size_t)G * k);
 			vbfm_params p{mu_w.data(), sig_w.data(), mu_v.data(), sig_v.data(), hw.data(), hv.data(), 0, 0, 0, 0};
 			check(vbfm_init_params_host(seed, init_stdev, k, D, G, &p, fm_v.data(), nullptr), nullptr);
@@ -528,12 +532,18 @@ int main(int argc, char **argv)
 		}
 
 		// fm_learn_vb_simultaneous::_learn
-		check(vbfm_init_caches(ctx), ctx);
+		uint32_t it0 = 0;
+		if (resume) {
+			check(vbfm_load_state(ctx, cmd.get(p_resume).c_str(), &it0), ctx);
+			std::cout << "resuming from " << cmd.get(p_resume) << " after " << it0 << " iterations" << std::endl;
+		} else {
+			check(vbfm_init_caches(ctx), ctx);
+		}
 		std::ostringstream tag;
 		tag << k0 << k1 << k;
 		const std::string f_rmse = "test_rmse_" + tag.str() + "_vb", f_fe = "free_energy_" + tag.str() + "_vb";
-		{ std::ofstream a(f_rmse.c_str()); std::ofstream b(f_fe.c_str()); }   // truncate (:58-73)
-		for (uint32_t it = 0; it < num_iter; it++) {
+		if (!resume) { std::ofstream a(f_rmse.c_str()); std::ofstream b(f_fe.c_str()); }   // truncate (:58-73); a resumed run appends
+		for (uint32_t it = it0; it < it0 + num_iter; it++) {
 			time_t now = time(0);
 			std::cout << ctime(&now) << std::endl;
 			const double t_user = usertime();
@@ -559,6 +569,7 @@ int main(int argc, char **argv)
 			fr << st.rmse << "\n";
 			std::cout << "#Iter=" << std::setw(3) << it << "\tTrain=" << st.train_quirk << "\tTest=" << st.rmse << std::endl;
 		}
+		if (cmd.has(p_save)) check(vbfm_save_state(ctx, cmd.get(p_save).c_str(), it0 + num_iter), ctx);
 		// libfm.cpp:509-511: fm_learn_vb::evaluate returns NaN
 		std::cout << "Final\tTrain=" << NAN << "\tTest=" << NAN << std::endl;
 		if (cmd.has(p_out)) {   // libfm.cpp:514-519, DVector::save (matrix.h:284-295)

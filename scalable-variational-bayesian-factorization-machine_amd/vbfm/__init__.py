@@ -149,7 +149,7 @@ EXPORTS = ["vbfm_abi_version", "vbfm_last_error", "vbfm_create", "vbfm_destroy",
            "vbfm_comm_unique_id", "vbfm_comm_init", "vbfm_comm_init_host", "vbfm_comm_info", "vbfm_load_data", "vbfm_free_host_data", "vbfm_save_data",
            "vbfm_init_params_host", "vbfm_mcmc_init", "vbfm_mcmc_set_params", "vbfm_mcmc_get_params",
            "vbfm_mcmc_init_caches", "vbfm_mcmc_iterate", "vbfm_mcmc_get_test_pred", "vbfm_mcmc_factor_sweep",
-           "vbfm_online_init", "vbfm_online_epoch", "vbfm_online_get_state"]
+           "vbfm_online_init", "vbfm_online_epoch", "vbfm_online_get_state", "vbfm_save_state", "vbfm_load_state"]
 
 # vbfm_exchange_fn: int fn(void *user, void *buf, uint64_t count, int32_t dtype, int32_t op)
 EXCHANGE_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_void_p, C.c_uint64, C.c_int32, C.c_int32)
@@ -220,6 +220,8 @@ def lib():
         L.vbfm_online_init.argtypes = [V, C.POINTER(OnlineConfig)]
         L.vbfm_online_epoch.argtypes = [V, C.POINTER(OnlineStats)]
         L.vbfm_online_get_state.argtypes = [V, P_f64, P_f64, P_f64, P_f64, P_f64, P_f64, P_f64]
+        L.vbfm_save_state.argtypes = [V, C.c_char_p, C.c_uint32]
+        L.vbfm_load_state.argtypes = [V, C.c_char_p, C.POINTER(C.c_uint32)]
         _lib = L
     return _lib
 
@@ -473,6 +475,18 @@ class FMLearnVB:
         self.init_caches()
         for _ in range(num_iter):
             yield self.iterate()
+
+    def save_state(self, path, num_iter=None):
+        """Checkpoint the learner between iterations (include/vbfm.h vbfm_save_state)."""
+        it = self.num_iter_done if num_iter is None else num_iter
+        _check(lib().vbfm_save_state(self._ctx, os.fsencode(path), int(it)), self._ctx)
+
+    def load_state(self, path):
+        """Resume from vbfm_save_state's file instead of init_caches; returns its iteration count."""
+        it = C.c_uint32()
+        _check(lib().vbfm_load_state(self._ctx, os.fsencode(path), C.byref(it)), self._ctx)
+        self.num_iter_done = it.value
+        return it.value
 
     def predict(self):
         """pred_this: clipped test predictions of the last iteration."""

@@ -1,0 +1,131 @@
+"""Checkpoint / resume of the VB learner (include/vbfm.h vbfm_save_state / vbfm_load_state).
+
+The reference has no counterpart (it always starts from its initial draws,
+fm_learn_vb_simultaneous.h:20): the contract is that a run stopped after i iterations and
+resumed from its file in a fresh context continues bit for bit -- every later iteration's
+RMSE, free energy, alpha and the final parameters equal the uninterrupted run's -- and that a
+file is refused for another model configuration or another train data set.
+"""
+import os
+import re
+
+import numpy as np
+import pytest
+
+import synth
+import vbfm
+from conftest import GOLDEN, ROOT, load_case
+
+pytestmark = pytest.mark.gpu
+CLI = os.path.join(ROOT, "scalable-variational-bayesian-factorization-machine_amd", "bin", "libFM")
+
+
+def _data(n=30000, F=6, S=300, seed=41):
+    tr = synth.generate(n, F, S, seed, 1)
+    te = synth.generate(1000, F, S, seed + 1, 1)
+    return tr, te, F * S
+
+
+def _learner(tr, te, nf, k, layout, dim=(1, 1)):
+    rp, f, v, y = tr
+    g = vbfm.FMLearnVB(dim[0], dim[1], k, nf + 1, min_target=float(y.min()), max_target=float(y.max()),
+                       layout=layout)
+    g.init(7, 0.1)
+    g.set_data(vbfm.DataSubset.from_csr(rp, f, v, y, nf), vbfm.DataSubset.from_csr(*te, nf))
+    return g
+
+
+def _trace(stats):
+    return [(s.rmse, s.mae, s.train_quirk, s.free_energy, s.alpha, s.mu_0_dash) for s in stats]
+
+
+@pytest.mark.parametrize("split", ["0", "1"])
+@pytest.mark.parametrize("layout", ["level", "column"])
+def test_resume_continues_bit_for_bit(layout, split, tmp_path, monkeypatch):
+    """4 iterations in one go against 2 + save, then load into a fresh context + 2: equal
+    bit for bit (level-ordered store and column layout, fused and deferred-split sweeps)."""
+    monkeypatch.setenv("VBFM_FORCE_SPLIT", split)
+    tr, te, nf = _data()
+    k = 5
+    a = _learner(tr, te, nf, k, layout)
+    a.init_caches()
+    full = [a.iterate() for _ in range(4)]
+    pa = a.get_params()
+    a.close()
+
+    b = _learner(tr, te, nf, k, layout)
+    b.init_caches()
+    first = [b.iterate() for _ in range(2)]
+    path = str(tmp_path / "vb.state")
+    b.save_state(path)
+    b.close()
+
+    c = _learner(tr, te, nf, k, layout)
+    assert c.load_state(path) == 2
+    assert c.layout() == layout
+    rest = [c.iterate() for _ in range(2)]
+    pc = c.get_params()
+    c.close()
+    assert _trace(first + rest) == _trace(full)
+    for key in ("mu_w", "sigma_w", "mu_v", "sigma_v", "hyp_sigma_w", "hyp_sigma_v"):
+        np.testing.assert_array_equal(np.asarray(pc[key]), np.asarray(pa[key]), err_msg=key)
+
+
+def test_load_refuses_other_model_or_data(tmp_path):
+    tr, te, nf = _data(n=5000)
+    g = _learner(tr, te, nf, 3, "auto")
+    g.init_caches()
+    g.iterate()
+    path = str(tmp_path / "vb.state")
+    g.save_state(path)
+    g.close()
+    # another factor count
+    h = _learner(tr, te, nf, 4, "auto")
+    with pytest.raises(vbfm.VbfmError, match="another model configuration"):
+        h.load_state(path)
+    h.close()
+    # the same shape, one target changed
+    rp, f, v, y = tr
+    y2 = y.copy()
+    y2[123] += 0.5
+    h = _learner((rp, f, v, y2), te, nf, 3, "auto")
+    with pytest.raises(vbfm.VbfmError, match="another train data set"):
+        h.load_state(path)
+    h.close()
+    # not a checkpoint
+    bad = tmp_path / "bad.state"
+    bad.write_bytes(b"\0" * 200)
+    h = _learner(tr, te, nf, 3, "auto")
+    with pytest.raises(vbfm.VbfmError, match="not a libvbfm VB checkpoint"):
+        h.load_state(str(bad))
+    h.close()
+
+
+def test_cli_save_state_and_resume(tmp_path):
+    """bin/libFM -save_state after 3 iterations, then -resume for 3 more: the appended
+    test_rmse / free_energy files and the #Iter lines continue the 6-iteration run's."""
+    d = os.path.join(GOLDEN, "tiny")
+    t, _ = load_case("tiny/vb")
+    m = t["meta"]
+    import subprocess
+
+    def run(cwd, iters, extra):
+        os.makedirs(cwd, exist_ok=True)
+        out = subprocess.run([CLI, "-task", "r", "-train", os.path.join(d, "train.libfm"), "-test",
+                              os.path.join(d, "test.libfm"), "-method", "vb", "-dim", m["dim"], "-iter", str(iters),
+                              "-seed", str(m["seed"]), "-init_stdev", str(m["init_stdev"])] + extra,
+                             cwd=str(cwd), capture_output=True, text=True, timeout=300)
+        assert "ERROR" not in out.stderr, out.stderr
+        return out.stdout
+
+    one = tmp_path / "one"
+    s_one = run(one, 6, [])
+    two = tmp_path / "two"
+    run(two, 3, ["-save_state", "vb.state"])
+    s_two = run(two, 3, ["-resume", "vb.state"])
+    tag = m["dim"].replace(",", "")
+    for fn in ("test_rmse_%s_vb" % tag, "free_energy_%s_vb" % tag):
+        assert open(one / fn).read() == open(two / fn).read(), fn
+    it_one = re.findall(r"#Iter=\s*(\d+)\tTrain=(\S+)\tTest=(\S+)", s_one)
+    it_two = re.findall(r"#Iter=\s*(\d+)\tTrain=(\S+)\tTest=(\S+)", s_two)
+    assert it_two == it_one[3:]
