@@ -317,11 +317,12 @@ hipError_t mc_lord_defer_flush(const McArgs &a, int is_w, uint32_t n, hipStream_
 hipError_t mc_row_sums(const RowRec *rows, uint32_t n, int mode, double w0, double *out, uint32_t nblocks,
                        hipStream_t s);
 // the end of the fused train re-prediction: the last factor's and the w terms from the rows'
-// entries, yhat = E + Q2 (+ w0), then as mc_train_update (e = yhat - y, per block the clipped
-// squared error); pk_done: the v sweeps accumulated factors 0..k-2 into the records
+// entries, yhat[row] = E + Q2 (+ w0) (mc_train_update follows); pk_done: the v sweeps
+// accumulated factors 0..k-2 into the records; scratch [2 * D] receives compact copies of the
+// last factor's v and of w
 hipError_t mc_pred_final(const uint64_t *row_ptr, const uint2 *csr, const double2 *ms_v, const double2 *ms_w, int k,
-                         int k1, int k0, double w0, int pk_done, RowRec *rows, const uint32_t *pos, const float *target,
-                         uint32_t n, double mn, double mx, double *out, uint32_t nblocks, hipStream_t s);
+                         int k1, int k0, double w0, int pk_done, const RowRec *rows, const uint32_t *pos, uint32_t n,
+                         uint32_t D, double *scratch, double *yhat, hipStream_t s);
 hipError_t mc_e_shift(RowRec *rows, uint32_t n, double d, hipStream_t s);
 hipError_t mc_train_update(RowRec *rows, const double *yhat, const float *target, uint32_t n, double mn, double mx,
                            double *out, uint32_t nblocks, const uint32_t *pos, hipStream_t s);

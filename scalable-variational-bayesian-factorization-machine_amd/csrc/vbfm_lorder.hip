@@ -62,6 +62,8 @@ template <bool IS_W, int P, bool NEXT>
 struct McOp {
 	double vo, v, vn;
 	bool go;
+	double vp = 0.0;   // v_{f-1}[j] for the fused train re-prediction (McArgs::pk), pk 0: off
+	int pk = 0;
 	DEVI void stat(Rec &r, float x, double &s1, double &s2) const
 	{
 		if constexpr (IS_W) {
@@ -89,6 +91,9 @@ struct McOp {
 			const double a = vn * x;
 			double &q = IS_W ? Q<0>(r) : Q<1 - P>(r);
 			q = first ? 0.0 + a : q + a;
+		}
+		if constexpr (!IS_W) {
+			if (pk) mc_pred_acc(TQ<0>(r), TZ<0>(r), T(r), x, first, vp, pk);   // MCMC leaves tq, tz, t free
 		}
 	}
 };
@@ -454,6 +459,8 @@ __global__ __launch_bounds__(BLOCK) void k_mc_level_lord(McArgs a)
 	McOp<IS_W, P, NEXT> op;
 	op.vo = a.par[(size_t)j * a.stride].x;
 	op.vn = NEXT ? a.par_next[(size_t)j * a.next_stride].x : 0.0;
+	op.pk = IS_W ? 0 : a.pk;
+	op.vp = op.pk ? a.par_prev[(size_t)j * a.next_stride].x : 0.0;
 	double sm = 0.0, ss = 0.0;
 	if constexpr (MODE == 0) {
 		if (n <= CAP) {   // resident run, x / next positions prefetched (as k_level_lord)
@@ -846,6 +853,8 @@ __global__ __launch_bounds__(BLOCK) void k_mc_lord_defer(McArgs a)
 	McOp<IS_W, P, false> op;
 	op.vo = a.par[(size_t)j * a.stride].x;
 	const double vn = NEXT ? a.par_next[(size_t)j * a.next_stride].x : 0.0;
+	const int pk = IS_W ? 0 : a.pk;
+	const double vp = pk ? a.par_prev[(size_t)j * a.next_stride].x : 0.0;
 	const bool first = a.first_level != 0;
 	const bool pending = (a.pending & 1) != 0;
 	double sm = 0.0, ss = 0.0;
@@ -878,7 +887,8 @@ __global__ __launch_bounds__(BLOCK) void k_mc_lord_defer(McArgs a)
 			const float x = __uint_as_float(q[u].x);
 			if (pending) mc_apply_pending<IS_W, P>(v, t[u], __uint_as_float(q[u].w));
 			if constexpr (NEXT) mc_add_next_q<IS_W, P>(v, x, first, vn);
-			if (pending || NEXT) lds_put(recs, i, v);
+			if (pk) mc_pred_acc(TQ<0>(v), TZ<0>(v), T(v), x, first, vp, pk);
+			if (pending || NEXT || pk) lds_put(recs, i, v);
 			op.stat(v, x, sm, ss);
 			dsts[i] = q[u].y;
 		}

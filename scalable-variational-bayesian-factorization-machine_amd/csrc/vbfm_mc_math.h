@@ -67,4 +67,31 @@ DEVI bool mc_draw(double mean_sum, double ss, double cur, double lambda, double 
 	return true;
 }
 
+// One entry's terms of the train re-prediction (predict_data_and_write_to_eterms,
+// fm_learn_mcmc.h:117-348) for the factor f-1 whose values are final while factor f is swept,
+// with the reference's operations in the row's ascending feature order: s1 = that factor's
+// q (step 1: q = 0.0, q += v*x), ev = the e accumulator (e = 0.0, e += 0.5*q*q per factor),
+// q2 = the q accumulator of step 2 (q = 0.0, q -= 0.5*v*v*x*x over every factor and entry).
+// At a row's first entry of a sweep the previous factor's complete s1 is folded into ev
+// (pk 2), or the accumulators start (pk 1, the sweep of factor 1).
+DEVI void mc_pred_acc(double &s1, double &ev, double &q2, float x, bool first, double vp, int pk)
+{
+	const double xd = x;
+	const double a = vp * xd;
+	const double b = 0.5 * vp * vp * xd * xd;
+	if (first) {
+		if (pk == 1) {
+			ev = 0.0;
+			q2 = 0.0 - b;
+		} else {
+			ev = ev + 0.5 * s1 * s1;
+			q2 = q2 - b;
+		}
+		s1 = 0.0 + a;
+	} else {
+		s1 = s1 + a;
+		q2 = q2 - b;
+	}
+}
+
 }  // namespace

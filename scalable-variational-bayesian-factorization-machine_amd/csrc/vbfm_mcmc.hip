@@ -98,39 +98,32 @@ __global__ __launch_bounds__(BLOCK) void k_mc_v_level(McArgs a)
 		ss = st.y;
 	}
 	const double vn = NEXT ? a.par_next[(size_t)j * a.next_stride].x : 0.0;
+	const double vp = a.pk ? a.par_prev[(size_t)j * a.next_stride].x : 0.0;   // fused re-prediction
 	const uint32_t g = a.attr_group[j];
 	double v;
 	const bool go = mc_draw(sm, ss, vo, a.lambda[(size_t)g * a.hstride], a.mu[(size_t)g * a.hstride], a.alpha,
 	                        mc_z(a, j), a.z != nullptr, a.sample, true, v, a.counters, threadIdx.x == 0);
 	if (threadIdx.x == 0) a.par[(size_t)j * a.stride].x = v;
-	if (!go && !NEXT) return;
-	if (a.dup[j]) {   // a column listing a row twice: sequential, as the reference
-		__syncthreads();
-		if (threadIdx.x == 0)
-			for (uint32_t i = 0; i < n; ++i) {
-				const uint2 ent = col[i];
-				RowRec &r = a.rows[ent.x & ROW_MASK];
-				const float x = ent_x(ent);
-				if (go) {
-					const double h = x * (mc_q<P>(r) - x * vo);
-					mc_qref<P>(r) -= x * (vo - v);
-					r.e -= h * (vo - v);
-				}
-				if constexpr (NEXT) mc_qacc<1 - P>(r, x, (ent.x & ROW_FIRST) != 0, vn);
-			}
-		return;
-	}
-	for (uint32_t i = threadIdx.x; i < n; i += BLOCK) {        // :826-834
-		const uint2 ent = col[i];
+	if (!go && !NEXT && !a.pk) return;
+	auto entry = [&](uint2 ent) {
 		RowRec &r = a.rows[ent.x & ROW_MASK];
 		const float x = ent_x(ent);
+		const bool first = (ent.x & ROW_FIRST) != 0;
 		if (go) {
 			const double h = x * (mc_q<P>(r) - x * vo);
 			mc_qref<P>(r) -= x * (vo - v);
 			r.e -= h * (vo - v);
 		}
-		if constexpr (NEXT) mc_qacc<1 - P>(r, x, (ent.x & ROW_FIRST) != 0, vn);
+		if constexpr (NEXT) mc_qacc<1 - P>(r, x, first, vn);
+		if (a.pk) mc_pred_acc(r.tq, r.tz, r.t, x, first, vp, a.pk);   // MCMC leaves tq, tz, t free
+	};
+	if (a.dup[j]) {   // a column listing a row twice: sequential, as the reference
+		__syncthreads();
+		if (threadIdx.x == 0)
+			for (uint32_t i = 0; i < n; ++i) entry(col[i]);
+		return;
 	}
+	for (uint32_t i = threadIdx.x; i < n; i += BLOCK) entry(col[i]);   // :826-834
 }
 
 // ---- draw_w over one level (+ q-cache of factor 0 into slot 0) ---------------------------
@@ -263,6 +256,56 @@ __global__ __launch_bounds__(BLOCK) void k_mc_train_update(RowRec *rows, const d
 	}
 	s = block_sum1<BLOCK>(s, lds);
 	if (threadIdx.x == 0) out[blockIdx.x] = s;
+}
+
+// the end of the fused train re-prediction (fm_learn_mcmc.h:117-348; the v sweeps of factors
+// 1..k-1 accumulated factors 0..k-2 into each record's tq / tz / t, mc_pred_acc): the last
+// factor's q and its squared terms, then the w terms, from the row's entries in ascending
+// feature order, yhat = e + q (+ w0) into yhat[row] (k_mc_train_update follows). The last
+// factor's v and the w are read from compact copies (vlast[j],
+// wc[j]: 8 B per attribute, MALL-resident at the bench scale). The q of step 1 and the squared
+// terms of step 2 go to separate accumulators, each in the reference's order, so one pass over
+// the entries serves both; the w terms follow every squared term (step 3). A row without
+// entries predicts w0.
+__global__ __launch_bounds__(256) void k_mc_pred_final(const uint64_t *row_ptr, const uint2 *csr, const double *vlast,
+                                                       const double *wc, int k, int k1, int k0, double w0, int pk_done,
+                                                       const RowRec *rows, const uint32_t *pos, uint32_t n, double *yhat)
+{
+	const uint32_t c = blockIdx.x * 256u + threadIdx.x;   // one row per thread: every gather chain in flight
+	if (c >= n) return;
+	const uint64_t b = row_ptr[c], e = row_ptr[c + 1];
+	double ev = 0.0, q2 = 0.0;
+	if (pk_done && e > b) {
+		const RowRec &rec = rows[pos ? pos[c] : c];
+		ev = rec.tz + 0.5 * rec.tq * rec.tq;   // fold factor k-2
+		q2 = rec.t;
+	}
+	if (k > 0) {
+		double q = 0.0;
+		for (uint64_t p = b; p < e; ++p) {
+			const uint2 ent = csr[p];
+			const double v = vlast[ent.x];
+			const float x = ent_x(ent);
+			q += v * x;
+			q2 -= 0.5 * v * v * x * x;
+		}
+		ev += 0.5 * q * q;
+	}
+	if (k1)
+		for (uint64_t p = b; p < e; ++p) {
+			const uint2 ent = csr[p];
+			q2 += wc[ent.x] * ent_x(ent);
+		}
+	double yh = ev + q2;
+	if (k0) yh += w0;
+	yhat[c] = yh;
+}
+
+// out[j] = p[j * stride].x: one factor's (or w's) values as a compact array
+__global__ void k_mc_extract(const double2 *p, uint32_t stride, uint32_t D, double *out)
+{
+	const uint32_t j = blockIdx.x * 256u + threadIdx.x;
+	if (j < D) out[j] = p[(size_t)j * stride].x;
 }
 
 // test side (:143-151 and _evaluate :261-279): pred_this = yhat, pred_sum_all += clip(yhat);
@@ -398,6 +441,17 @@ hipError_t mc_train_update(RowRec *rows, const double *yhat, const float *target
                            double *out, uint32_t nblocks, const uint32_t *pos, hipStream_t s)
 {
 	k_mc_train_update<256><<<nblocks, 256, 0, s>>>(rows, yhat, target, n, mn, mx, out, pos);
+	return hipGetLastError();
+}
+
+hipError_t mc_pred_final(const uint64_t *row_ptr, const uint2 *csr, const double2 *ms_v, const double2 *ms_w, int k,
+                         int k1, int k0, double w0, int pk_done, const RowRec *rows, const uint32_t *pos, uint32_t n,
+                         uint32_t D, double *scratch, double *yhat, hipStream_t s)
+{
+	double *vlast = scratch, *wc = scratch + D;
+	if (D && k > 0) k_mc_extract<<<grid_for(D), 256, 0, s>>>(ms_v + (k - 1), (uint32_t)k, D, vlast);
+	if (D && k1) k_mc_extract<<<grid_for(D), 256, 0, s>>>(ms_w, 1, D, wc);
+	if (n) k_mc_pred_final<<<grid_for(n), 256, 0, s>>>(row_ptr, csr, vlast, wc, k, k1, k0, w0, pk_done, rows, pos, n, yhat);
 	return hipGetLastError();
 }
 

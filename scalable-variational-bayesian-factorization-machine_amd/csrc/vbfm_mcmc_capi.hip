@@ -44,10 +44,12 @@ struct McState {
 	std::vector<uint8_t> col_nonempty;                    // [train nf] over all shards
 	double *pred_this = nullptr, *pred_sum = nullptr;     // [test rows]
 	double *vc = nullptr;                                 // [k*D] compact v for the re-prediction
+	double *pc = nullptr;                                 // [2*D] last factor's v and w (fused re-prediction)
 	double *red_d = nullptr;                              // [4 * MC_RED_BLOCKS]
 	std::vector<double> red_h;
 	uint32_t iter = 0;
 	bool caches = false;
+	bool pred_acc = false;                                // v sweeps accumulate the train re-prediction
 	uint32_t hc[HC_N] = {};
 	hipEvent_t ev[MEV_N] = {};
 };
@@ -58,7 +60,7 @@ void mc_free(vbfm_ctx *c)
 {
 	McState *m = c->mc;
 	if (!m) return;
-	dfree(m->hyp_d); dfree(m->z_d); dfree(m->pred_this); dfree(m->pred_sum); dfree(m->red_d); dfree(m->vc);
+	dfree(m->hyp_d); dfree(m->z_d); dfree(m->pred_this); dfree(m->pred_sum); dfree(m->red_d); dfree(m->vc); dfree(m->pc);
 	for (int i = 0; i < MEV_N; i++)
 		if (m->ev[i]) (void)hipEventDestroy(m->ev[i]);
 	delete m;
@@ -282,7 +284,21 @@ McArgs mc_args(vbfm_ctx *c, uint32_t l, bool is_w, int f)
 	a.counters = c->counters;
 	a.stats = c->stats;
 	a.slot = is_w ? 0 : (f & 1);
+	if (m.pred_acc && !is_w && f >= 1) {   // factor f-1 is final: its re-prediction terms ride along
+		a.par_prev = c->ms_v + (f - 1);
+		a.pk = f == 1 ? 1 : 2;
+	}
 	return a;
+}
+
+// The train re-prediction after draw_all fused into the v sweeps (McArgs::pk) and one final
+// row pass (k_mc_pred_final) instead of a separate prediction of every entry's k factors:
+// the same operations in the same order, so e is bit-identical (VBFM_MC_FUSED_PREDICT=0: the
+// separate prediction)
+bool fused_predict()
+{
+	const char *e = getenv("VBFM_MC_FUSED_PREDICT");
+	return !(e && e[0] == '0');
 }
 
 void mc_sweep(vbfm_ctx *c, bool is_w, int f)
@@ -367,8 +383,8 @@ void mc_step_v(vbfm_ctx *c, int f)
 	c->q_ready[(f + 1) & 1] = f + 1 < c->k ? f + 1 : -1;
 }
 
-// full prediction of train (into scratch) and test (fm_learn_mcmc.h:117-348)
-void mc_predict(vbfm_ctx *c)
+// full prediction of train (into scratch; unless train = false) and test (fm_learn_mcmc.h:117-348)
+void mc_predict(vbfm_ctx *c, bool train = true)
 {
 	McState &m = *c->mc;
 	// the parameters are {v, 0} pairs: the wave-form prediction reads a compact copy of v
@@ -377,9 +393,11 @@ void mc_predict(vbfm_ctx *c)
 	const int btr = blocked_predict(c, c->tr), bte = c->e_test ? blocked_predict(c, c->te) : 0;
 	if ((btr == 2 || bte == 2) && c->k <= 256 && kd && !m.vc) m.vc = dalloc<double>(kd);
 	bool fresh = false;
-	HIPCHK(vbk::predict_e_compact(c->tr.row_ptr, c->tr.csr, c->ms_v, c->ms_w, c->k, c->k1, c->k0, m.w0, c->scratch_n,
-	                              c->tr.n, btr, m.vc, kd, !fresh, c->s));
-	fresh = fresh || (btr == 2 && m.vc);
+	if (train) {
+		HIPCHK(vbk::predict_e_compact(c->tr.row_ptr, c->tr.csr, c->ms_v, c->ms_w, c->k, c->k1, c->k0, m.w0,
+		                              c->scratch_n, c->tr.n, btr, m.vc, kd, !fresh, c->s));
+		fresh = fresh || (btr == 2 && m.vc);
+	}
 	if (c->e_test)
 		HIPCHK(vbk::predict_e_compact(c->te.row_ptr, c->te.csr, c->ms_v, c->ms_w, c->k, c->k1, c->k0, m.w0, c->e_test,
 		                              c->te.n, bte, m.vc, kd, !fresh, c->s));
@@ -574,13 +592,19 @@ int vbfm_mcmc_iterate(vbfm_ctx *c, vbfm_mcmc_stats *o)
 		HIPCHK(hipEventRecord(m.ev[MEV_HYPER], c->s));
 		if (c->k1) mc_step_w(c);
 		HIPCHK(hipEventRecord(m.ev[MEV_W], c->s));
+		const bool fused = fused_predict();
 		if (c->k > 0) {
 			draw_v_hyper(c);
+			struct Acc {
+				McState &m;
+				Acc(McState &m_, bool on) : m(m_) { m.pred_acc = on; }
+				~Acc() { m.pred_acc = false; }
+			} acc(m, fused);
 			for (int f = 0; f < c->k; f++) mc_step_v(c, f);
 		}
 		HIPCHK(hipEventRecord(m.ev[MEV_V], c->s));
 		// re-predict and evaluate (fm_learn_mcmc_simultaneous.h:134-175, 238-245)
-		mc_predict(c);
+		mc_predict(c, !fused);
 		const double mn = c->min_target, mx = c->max_target;
 		HIPCHK(vbk::mc_test_update(c->e_test, c->te.target, c->te.n, mn, mx, 1.0 / (m.iter + 1), m.pred_this,
 		                           m.pred_sum, m.red_d, MC_RED_BLOCKS, c->s));
@@ -589,6 +613,12 @@ int vbfm_mcmc_iterate(vbfm_ctx *c, vbfm_mcmc_stats *o)
 		double tm[5] = {0, 0, 0, 0, 0};
 		for (uint32_t b = 0; b < MC_RED_BLOCKS; b++)
 			for (int q = 0; q < 4; q++) tm[q] += m.red_h[4 * b + q];
+		if (fused) {   // yhat of train from the sweeps' accumulators + the last factor and w
+			if (!m.pc) m.pc = dalloc<double>(2 * (size_t)c->D);
+			HIPCHK(vbk::mc_pred_final(c->tr.row_ptr, c->tr.csr, c->ms_v, c->ms_w, c->k, c->k1, c->k0, m.w0, c->k >= 2,
+			                          c->rows, c->rows_lorder ? c->lpos0 : nullptr, c->tr.n, c->D, m.pc, c->scratch_n,
+			                          c->s));
+		}
 		HIPCHK(vbk::mc_train_update(c->rows, c->scratch_n, c->tr.target, c->tr.n, mn, mx, c->red_d, c->RED_BLOCKS,
 		                            c->rows_lorder ? c->lpos0 : nullptr, c->s));
 		tm[4] = finish_sum(c, c->RED_BLOCKS);

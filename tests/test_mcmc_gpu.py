@@ -173,3 +173,64 @@ def test_wave_prediction_compact_chain_vs_reference(case, synth_files, sa_split,
     p = fml.get_params()
     if "final_fm_v" in a:
         assert rel_err(p["v"], a["final_fm_v"]) <= REL
+
+
+def _fused_pair(run, monkeypatch):
+    """run() twice: the train re-prediction as its own pass (VBFM_MC_FUSED_PREDICT=0, exact
+    reference order) and fused into the v sweeps + the final row pass (default)."""
+    monkeypatch.setenv("VBFM_PREDICT", "exact")
+    out = []
+    for fused in ("0", "1"):
+        monkeypatch.setenv("VBFM_MC_FUSED_PREDICT", fused)
+        out.append(run())
+    return out
+
+
+@pytest.mark.parametrize("split", ["0", "1"])
+@pytest.mark.parametrize("case", ["synth_als", "sa_mcmc", "tiny_dup/mcmc", "tiny/mcmc_meta"])
+def test_fused_train_prediction_is_bit_identical(case, split, synth_files, sa_split, monkeypatch):
+    """The train re-prediction of draw_all's end (fm_learn_mcmc.h:117-348) accumulated inside
+    the v sweeps (factor f-1's terms while factor f is swept) + one final row pass: the same
+    operations in the reference's order, so every iteration's Train= / Test= values, the final
+    parameters and the rows' e equal the separate exact-order prediction's bit for bit (level
+    store and column layout, fused and row-sharded split kernels, a repeated feature)."""
+    monkeypatch.setenv("VBFM_FORCE_SPLIT", split)
+
+    def run():
+        _, _, fml, stats = run_case(case, synth_files, sa_split)
+        r = ([(s.rmse_all, s.rmse_this, s.train_rmse, s.alpha, s.w0) for s in stats], fml.get_params()["v"],
+             fml.rows()["e"])
+        fml.close()
+        return r
+
+    a, b = _fused_pair(run, monkeypatch)
+    assert a[0] == b[0]
+    np.testing.assert_array_equal(a[1], b[1])
+    np.testing.assert_array_equal(a[2], b[2])
+
+
+@pytest.mark.parametrize("layout", ["level", "column"])
+@pytest.mark.parametrize("k", [0, 1, 2, 3])
+def test_fused_train_prediction_few_factors(k, layout, monkeypatch):
+    """k = 0 (w terms only), 1 (no accumulating sweep), 2 (one), 3: the fused re-prediction
+    against the separate one, device-RNG MCMC on synthetic field data, bit for bit."""
+    import synth
+
+    rp, f, v, y = synth.generate(20000, 5, 150, 3, 1)
+    rpt, ft, vt, yt = synth.generate(500, 5, 150, 4, 1)
+    nf = 5 * 150
+
+    def run():
+        fml = vbfm.FMLearnMCMC(1, 1, k, nf + 1, min_target=float(y.min()), max_target=float(y.max()), method="mcmc",
+                               layout=layout)
+        fml.init_device(9)
+        stats = list(fml.learn(vbfm.DataSubset.from_csr(rp, f, v, y, nf),
+                               vbfm.DataSubset.from_csr(rpt, ft, vt, yt, nf), 3))
+        assert fml.layout() == layout
+        r = ([(s.rmse_all, s.train_rmse, s.alpha, s.w0) for s in stats], fml.rows()["e"])
+        fml.close()
+        return r
+
+    a, b = _fused_pair(run, monkeypatch)
+    assert a[0] == b[0]
+    np.testing.assert_array_equal(a[1], b[1])
