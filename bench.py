@@ -351,7 +351,7 @@ def main():
     elif mc:
         kernel = "k_mc_level_lord" if layout == "level" else "k_mc_v_level"
     else:
-        kernel = "k_level_lord" if layout == "level" else "k_v_level_fused"
+        kernel = {"level": "k_level_lord", "entry": "k_level_lord<ENT> (entry store)"}.get(layout, "k_v_level_fused")
     # row shards (N > 1, or the multi-rank kernels forced on one GPU): a level is the split
     # form -- statistics kernel, RCCL all-reduce, posterior / correction -- and its time (the
     # per-level events bracket all of it) is what avg_launch_ms reports

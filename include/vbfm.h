@@ -173,11 +173,17 @@ int vbfm_get_test_e(vbfm_ctx *ctx, double *e /*[test rows]*/);
  *                      (vbfm_set_layout fails at the first sweep when the data does not
  *                      allow it). Results are identical up to the summation order of the
  *                      data-set sums (w0, alpha, free energy).
- * Set before vbfm_set_train; VBFM_LAYOUT=auto|column|level in the environment overrides.
- * vbfm_get_layout reports the layout in use (COLUMN or LEVEL) once the train set is known. */
+ *   VBFM_LAYOUT_ENTRY  for levels that miss rows (multi-hot rows without fields): one slot per
+ *                      train entry in the level order, a row's record in the slot of the entry
+ *                      its next level sweeps; levels stream their runs and move each record to
+ *                      its row's next slot (nnz x 64 B of HBM; VB, one rank). AUTO picks it
+ *                      where LEVEL does not apply and it fits (VBFM_ESTORE=0: COLUMN instead).
+ * Set before vbfm_set_train; VBFM_LAYOUT=auto|column|level|entry in the environment overrides.
+ * vbfm_get_layout reports the layout in use (COLUMN, LEVEL or ENTRY) once the train set is known. */
 #define VBFM_LAYOUT_AUTO 0
 #define VBFM_LAYOUT_COLUMN 1
 #define VBFM_LAYOUT_LEVEL 2
+#define VBFM_LAYOUT_ENTRY 3
 int vbfm_set_layout(vbfm_ctx *ctx, int32_t layout);
 int vbfm_get_layout(vbfm_ctx *ctx, int32_t *layout);
 

@@ -120,11 +120,7 @@ LevelArgs level_args(vbfm_ctx *c, uint32_t l, bool is_w, int f);
 // ---- level-ordered row store (vbfm_lorder.hip) ------------------------------------------
 void lord_release(vbfm_ctx *c, bool keep_rows)
 {
-	if (keep_rows && c->rows_lorder) {
-		HIPCHK(vbk::rows_scatter(c->rows_alt, c->rows, c->lrow0, c->tr.n, c->s));
-		std::swap(c->rows, c->rows_alt);
-		c->rows_lorder = false;
-	}
+	if (keep_rows) rows_row_order(c);   // (without keep_rows the records are discarded)
 	sync(c);
 	dfree(c->rows_alt); dfree(c->lcp); dfree(c->lx); dfree(c->lnext); dfree(c->lrow0); dfree(c->lpos0);
 	dfree(c->lpidx); dfree(c->lpx); dfree(c->post_tab); dfree(c->lpay); dfree(c->lpay2);
@@ -132,6 +128,7 @@ void lord_release(vbfm_ctx *c, bool keep_rows)
 	c->seg_ptr.clear();
 	c->long_min = 0;
 	c->lord = false;
+	c->estore = false;
 	c->rows_lorder = false;
 }
 
@@ -140,6 +137,7 @@ static int layout_request(const vbfm_ctx *c)
 	const char *env = getenv("VBFM_LAYOUT");
 	if (env && !strcmp(env, "column")) return VBFM_LAYOUT_COLUMN;
 	if (env && !strcmp(env, "level")) return VBFM_LAYOUT_LEVEL;
+	if (env && !strcmp(env, "entry")) return VBFM_LAYOUT_ENTRY;
 	if (env && !strcmp(env, "auto")) return VBFM_LAYOUT_AUTO;
 	return c->layout_req;
 }
@@ -180,6 +178,66 @@ static void build_long_segs(vbfm_ctx *c, const std::vector<uint64_t> &lcp, const
 	sync(c);
 }
 
+// The entry store, for levels that miss rows (multi-hot rows without fields): one slot per
+// train entry in the field store's order (level by level, the level's columns in ascending
+// feature order, rows ascending in a column), nnz x 64 B; a row's record waits in the slot of
+// the entry its next level sweeps, so a level streams its columns' runs and scatters each
+// record to the row's next slot (k_level_lord<..., ENT>) instead of gathering and writing back
+// rows in place (the column-gather layout: two random touches per entry).
+// Single rank, fused sweeps, no row listing a feature twice, the VB learner; the store must
+// fit in half the free memory. A row without entries parks its record in slot nnz + r.
+// Returns false when it does not apply (force: throw instead).
+bool build_estore(vbfm_ctx *c, const std::vector<uint64_t> &lcp, const std::vector<uint8_t> &dup,
+                  const std::vector<uint32_t> &feats, bool force)
+{
+	DevData &d = c->tr;
+	const uint32_t n = d.n, nf = d.nf;
+	std::string why;
+	const char *env = getenv("VBFM_ESTORE");
+	size_t fr = 0, tot = 0;
+	HIPCHK(hipMemGetInfo(&fr, &tot));
+	if (!force && env && env[0] == '0') why = "VBFM_ESTORE=0";
+	else if (c->mc) why = "the MCMC / ALS sweeps";
+	else if (c->row_comm() || c->force_split) why = "row shards (split sweeps)";
+	else if (n == 0 || d.nnz == 0) why = "no train entries";
+	else if (d.nnz + n >= 0x80000000ull) why = "more than 2^31 entries and rows";
+	else if ((double)(d.nnz + n) * sizeof(RowRec) > 0.5 * (double)fr) why = "the store does not fit in half the free memory";
+	for (uint32_t i = 0; i < nf && why.empty(); i++)
+		if (dup[feats[i]]) why = "a row lists feature " + std::to_string(feats[i]) + " twice";
+	if (!why.empty()) {
+		if (force) throw std::string("entry store not possible: ") + why;
+		return false;
+	}
+	std::vector<uint32_t> lvpos(nf);
+	for (uint32_t i = 0; i < nf; i++) lvpos[feats[i]] = i;
+	c->lcp = dalloc<uint64_t>(lcp.size());
+	HIPCHK(hipMemcpyAsync(c->lcp, lcp.data(), lcp.size() * 8, hipMemcpyHostToDevice, c->s));
+	uint32_t *lv = dalloc<uint32_t>(nf);
+	HIPCHK(hipMemcpyAsync(lv, lvpos.data(), (size_t)nf * 4, hipMemcpyHostToDevice, c->s));
+	{
+		uint32_t *cnt = dalloc<uint32_t>(1), h = 1;
+		HIPCHK(vbk::count_x_ne1(d.csc, d.nnz, cnt, c->s));
+		HIPCHK(hipMemcpyAsync(&h, cnt, 4, hipMemcpyDeviceToHost, c->s));
+		sync(c);
+		dfree(cnt);
+		const char *kx = getenv("VBFM_LX");
+		if (h != 0 || (kx && kx[0] == '1')) c->lx = dalloc<float>(d.nnz);
+	}
+	c->lnext = dalloc<uint32_t>(d.nnz);
+	c->lpos0 = dalloc<uint32_t>(n);
+	// slots: the entries, then one parking slot per row (used by rows without entries)
+	c->rows_alt = dalloc<RowRec>(d.nnz + n);
+	HIPCHK(hipMemsetAsync(c->rows_alt, 0, (d.nnz + n) * sizeof(RowRec), c->s));
+	HIPCHK(vbk::estore_build(d.row_ptr, d.csr, d.col_ptr, d.csc, lv, c->lcp, n, d.nnz, c->lnext, c->lx, c->lpos0,
+	                         c->s));
+	sync(c);
+	dfree(lv);
+	c->lord = true;
+	c->estore = true;
+	c->rows_lorder = false;
+	return true;
+}
+
 // Level-ordered store of the train set when every level holds each row exactly once (no
 // repeated feature in a row): per level l, positions [l*n, (l+1)*n) list the level's
 // columns in ascending feature order, rows ascending within a column.
@@ -212,7 +270,12 @@ void build_lorder(vbfm_ctx *c, const std::vector<uint64_t> &cp, const std::vecto
 	}
 	if (!why.empty()) {
 		if (req == VBFM_LAYOUT_LEVEL) throw std::string("level-ordered row layout not possible: ") + why;
+		if (build_estore(c, lcp, dup, feats, req == VBFM_LAYOUT_ENTRY)) return;
 		build_long_segs(c, lcp, dup, feats);   // the column-gather layout
+		return;
+	}
+	if (req == VBFM_LAYOUT_ENTRY) {   // forced on complete levels too (tests)
+		build_estore(c, lcp, dup, feats, true);
 		return;
 	}
 	c->lcp = dalloc<uint64_t>(lcp.size());
@@ -293,7 +356,8 @@ void build_lorder(vbfm_ctx *c, const std::vector<uint64_t> &cp, const std::vecto
 void rows_level_order(vbfm_ctx *c)
 {
 	if (!c->lord || c->rows_lorder) return;
-	HIPCHK(vbk::rows_gather(c->rows_alt, c->rows, c->lrow0, c->tr.n, c->s));
+	if (c->estore) HIPCHK(vbk::rows_scatter(c->rows_alt, c->rows, c->lpos0, c->tr.n, c->s));   // row r -> its slot
+	else HIPCHK(vbk::rows_gather(c->rows_alt, c->rows, c->lrow0, c->tr.n, c->s));
 	std::swap(c->rows, c->rows_alt);
 	c->rows_lorder = true;
 }
@@ -301,9 +365,17 @@ void rows_level_order(vbfm_ctx *c)
 void rows_row_order(vbfm_ctx *c)
 {
 	if (!c->rows_lorder) return;
-	HIPCHK(vbk::rows_scatter(c->rows_alt, c->rows, c->lrow0, c->tr.n, c->s));
+	if (c->estore) HIPCHK(vbk::rows_gather(c->rows_alt, c->rows, c->lpos0, c->tr.n, c->s));
+	else HIPCHK(vbk::rows_scatter(c->rows_alt, c->rows, c->lrow0, c->tr.n, c->s));
 	std::swap(c->rows, c->rows_alt);
 	c->rows_lorder = false;
+}
+
+// the data-set sums (w0, alpha / free energy, train quirk) read N consecutive records: the
+// field store's level-0 order is such a permutation, the entry store's slots are not
+void rows_dense(vbfm_ctx *c)
+{
+	if (c->estore) rows_row_order(c);
 }
 
 // ---- feature shards (vbfm_set_shard_mode) ------------------------------------------------
@@ -637,6 +709,14 @@ void sweep_level(vbfm_ctx *c, uint32_t l, bool is_w, int f)
 		a.src = c->rows;
 		a.dst = c->rows_alt;
 		a.first_level = l == 0;
+		if (c->estore) {   // one store, global slots: records move to their rows' next slots in place
+			a.lbase = 0;
+			a.dst = c->rows;
+			a.ent = 1;
+			HIPCHK(vbk::lord_level(a, is_w, c->s));
+			prof_end(c, p);
+			return;
+		}
 		if (!c->row_comm() && !c->force_split) {
 			if (c->long_min) {
 				a.long_min = c->long_min;
@@ -714,6 +794,7 @@ void step_w0(vbfm_ctx *c)
 	// update_w0 (fm_learn_vb.h:504-525)
 	const double sigma_old = c->s0d;
 	c->s0d = 1.0 / (c->sigma_0 + (double)c->n_global * c->alpha);
+	rows_dense(c);
 	HIPCHK(vbk::row_sums(c->rows, c->tr.n, 0, c->mu0, c->red_d, c->RED_BLOCKS, c->s));
 	double w0_temp = finish_sum(c, c->RED_BLOCKS);
 	allreduce_host(c, &w0_temp, 1);
@@ -763,6 +844,7 @@ void step_v(vbfm_ctx *c, int f)
 
 double rows_energy(vbfm_ctx *c)
 {
+	rows_dense(c);
 	HIPCHK(vbk::row_sums(c->rows, c->tr.n, 1, 0.0, c->red_d, c->RED_BLOCKS, c->s));
 	double s = finish_sum(c, c->RED_BLOCKS);
 	allreduce_host(c, &s, 1);
@@ -1609,6 +1691,7 @@ int vbfm_iterate(vbfm_ctx *c, vbfm_iter_stats *o)
 		sync(c);
 		double tm[3] = {0.0, 0.0, 0.0};
 		for (uint32_t i = 0; i < c->RED_BLOCKS; i++) { tm[0] += c->red_h[2 * i]; tm[1] += c->red_h[2 * i + 1]; }
+		rows_dense(c);
 		HIPCHK(vbk::train_quirk(c->rows, c->tr.n, mn, mx, c->red_d, c->RED_BLOCKS, c->s));
 		tm[2] = finish_sum(c, c->RED_BLOCKS);
 		allreduce_host(c, tm, 3);
@@ -1656,7 +1739,7 @@ int vbfm_set_shard_mode(vbfm_ctx *c, int32_t mode, int32_t num_shards)
 int vbfm_set_layout(vbfm_ctx *c, int32_t layout)
 {
 	if (!c) return fail(nullptr, "null context");
-	if (layout < VBFM_LAYOUT_AUTO || layout > VBFM_LAYOUT_LEVEL) return fail(c, "unknown row layout");
+	if (layout < VBFM_LAYOUT_AUTO || layout > VBFM_LAYOUT_ENTRY) return fail(c, "unknown row layout");
 	if (c->rows) return fail(c, "vbfm_set_layout must precede vbfm_set_train");
 	c->layout_req = layout;
 	return 0;
@@ -1667,7 +1750,7 @@ int vbfm_get_layout(vbfm_ctx *c, int32_t *layout)
 	if (!c || !layout) return fail(c, "null argument");
 	return guarded(c, [&] {
 		require_train(c);
-		*layout = c->lord ? VBFM_LAYOUT_LEVEL : VBFM_LAYOUT_COLUMN;
+		*layout = c->estore ? VBFM_LAYOUT_ENTRY : c->lord ? VBFM_LAYOUT_LEVEL : VBFM_LAYOUT_COLUMN;
 	});
 }
 

@@ -136,6 +136,8 @@ struct vbfm_ctx {
 	// level-ordered row store (vbfm_lorder.hip)
 	int layout_req = VBFM_LAYOUT_AUTO;
 	bool lord = false;             // built for the current train set and in use
+	bool estore = false;           // ... as the entry store (levels that miss rows: build_estore);
+	                               // lpos0 then holds each row's slot between sweeps, lrow0 is unused
 	bool rows_lorder = false;      // rows currently hold level-0 order (else row order)
 	RowRec *rows_alt = nullptr;    // second record buffer (each level moves rows -> rows_alt)
 	uint64_t *lcp = nullptr;       // [nf+1] global position of each level feature's run
@@ -239,6 +241,7 @@ void read_counters(vbfm_ctx *c, vbfm_iter_stats *o);
 void upload_hyp(vbfm_ctx *c);
 void lord_release(vbfm_ctx *c, bool keep_rows);
 void rows_level_order(vbfm_ctx *c);   // records in level-0 order before a sweep (no-op without the store)
+void rows_dense(vbfm_ctx *c);         // records N-dense for the data-set sums (row order from the entry store)
 void rows_row_order(vbfm_ctx *c);     // records back in row order (row-indexed kernels, readback)   // level-ordered store freed (rows back to row order)
 
 }  // namespace vbi

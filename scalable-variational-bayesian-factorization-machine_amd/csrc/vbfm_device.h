@@ -83,6 +83,7 @@ struct LevelArgs {
 	const RowRec *src;         // records in this level's order
 	RowRec *dst;               // records in the next level's order
 	int first_level;           // level 0: every row's smallest feature (q-cache restart)
+	int ent;                   // the entry store: src == dst, lnext bit 31 = the row's first entry
 	// deferred correction (row-sharded split on the level-ordered store)
 	const uint32_t *lpidx;     // the entry's row: index of its previous-level feature in that level
 	const float *lpx;          // ... and that entry's x
@@ -203,6 +204,12 @@ hipError_t count_x_ne1(const uint2 *csc, uint64_t nnz, uint32_t *cnt, hipStream_
 hipError_t lord_pack2(const uint32_t *lnext, const uint32_t *lpidx, uint2 *lpay2, uint64_t nnz, hipStream_t s);
 hipError_t lord_pack(const float *lx, const uint32_t *lnext, const uint32_t *lpidx, const float *lpx, uint4 *lpay,
                      uint64_t nnz, hipStream_t s);
+// the entry store (levels that miss rows): per train row its entries' slots -> lnext [nnz] (bit 31:
+// the row's first entry), lx [nnz] (or null), lfirst [n] (a row without entries: nnz + r);
+// lvpos[j] = level position of feature j
+hipError_t estore_build(const uint64_t *row_ptr, const uint2 *csr, const uint64_t *col_ptr, const uint2 *csc,
+                        const uint32_t *lvpos, const uint64_t *lcp, uint32_t n, uint64_t nnz, uint32_t *lnext,
+                        float *lx, uint32_t *lfirst, hipStream_t s);
 hipError_t rows_scatter(RowRec *dst, const RowRec *src, const uint32_t *idx, uint32_t n, hipStream_t s);
 hipError_t mark_first(const uint64_t *row_ptr, const uint2 *csr, const uint64_t *col_ptr, uint2 *csc,
                       uint32_t n, hipStream_t s);

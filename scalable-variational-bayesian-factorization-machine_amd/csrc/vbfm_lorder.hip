@@ -202,7 +202,11 @@ DEVI void lord_stats(double2 *recs, const RowRec *src, const float *lx, uint32_t
 // correction of every record of the run and its move to the next level's order. resident:
 // the run (n <= CAP) is still in LDS from lord_stats. Every record is written even when the
 // guards skip the correction: the write IS the move.
-template <int BLOCK, uint32_t CAP, class Op>
+// ENT (the entry store, build_estore): bit 31 of a next position marks the row's first entry
+// (the q-cache restart), which the level-uniform `first` gives in the field store
+constexpr uint32_t ENT_FIRST = 0x80000000u;
+
+template <int BLOCK, uint32_t CAP, class Op, bool ENT = false>
 DEVI void lord_move(double2 *recs, uint32_t *dsts, const RowRec *src, const float *lx, const uint32_t *nxt, uint32_t n,
                     bool resident, RowRec *dst, bool first, const Op &op)
 {
@@ -231,9 +235,9 @@ DEVI void lord_move(double2 *recs, uint32_t *dsts, const RowRec *src, const floa
 			if (i < m) {
 				Rec v;
 				lds_get(recs, i, v);
-				op.apply(v, xr[u], first);
+				op.apply(v, xr[u], ENT ? (nr[u] & ENT_FIRST) != 0 : first);
 				lds_put(recs, i, v);
-				dsts[i] = nr[u];
+				dsts[i] = ENT ? nr[u] & ~ENT_FIRST : nr[u];
 			}
 		}
 		__syncthreads();
@@ -278,7 +282,7 @@ DEVI void res_stats(const double2 *recs, uint32_t n, const float (&xr)[R], const
 	}
 }
 
-template <int BLOCK, int R, class Op>
+template <int BLOCK, int R, class Op, bool ENT = false>
 DEVI void res_move(double2 *recs, uint32_t *dsts, uint32_t n, const float (&xr)[R], const uint32_t (&nr)[R],
                    RowRec *dst, bool first, const Op &op)
 {
@@ -288,9 +292,9 @@ DEVI void res_move(double2 *recs, uint32_t *dsts, uint32_t n, const float (&xr)[
 		if (i < n) {
 			Rec v;
 			lds_get(recs, i, v);
-			op.apply(v, xr[u], first);
+			op.apply(v, xr[u], ENT ? (nr[u] & ENT_FIRST) != 0 : first);
 			lds_put(recs, i, v);
-			dsts[i] = nr[u];
+			dsts[i] = ENT ? nr[u] & ~ENT_FIRST : nr[u];
 		}
 	}
 	__syncthreads();
@@ -305,7 +309,7 @@ DEVI void res_move(double2 *recs, uint32_t *dsts, uint32_t n, const float (&xr)[
 // reduce its statistics (update_v :587-596 / update_w :534-539), posterior + guards, then
 // correct and move every record. Runs longer than CAP = BLOCK*R records are streamed twice
 // (contiguous, L2-warm).
-template <int BLOCK, int R, bool IS_W, int P, bool NEXT>
+template <int BLOCK, int R, bool IS_W, int P, bool NEXT, bool ENT>
 __global__ __launch_bounds__(BLOCK) void k_level_lord(LevelArgs a)
 {
 	constexpr uint32_t CAP = BLOCK * R;
@@ -335,14 +339,15 @@ __global__ __launch_bounds__(BLOCK) void k_level_lord(LevelArgs a)
 		block_sum2<BLOCK>(s1, s2, lds);
 		op.go = vb_post<IS_W>(s1, s2, hyp, a.alpha, op.mo, op.so, op.mu, op.sig, a.counters, threadIdx.x == 0);
 		if (threadIdx.x == 0) a.ms[(size_t)j * a.ms_stride] = make_double2(op.mu, op.sig);
-		res_move<BLOCK, R>(recs, dsts, n, xr, nr, a.dst, a.first_level != 0, op);
+		res_move<BLOCK, R, VbOp<IS_W, P, NEXT>, ENT>(recs, dsts, n, xr, nr, a.dst, a.first_level != 0, op);
 		return;
 	}
 	lord_stats<BLOCK, CAP>(recs, src, lx, n, op, s1, s2);
 	block_sum2<BLOCK>(s1, s2, lds);
 	op.go = vb_post<IS_W>(s1, s2, hyp, a.alpha, op.mo, op.so, op.mu, op.sig, a.counters, threadIdx.x == 0);
 	if (threadIdx.x == 0) a.ms[(size_t)j * a.ms_stride] = make_double2(op.mu, op.sig);
-	lord_move<BLOCK, CAP>(recs, dsts, src, lx, a.lnext + sb, n, false, a.dst, a.first_level != 0, op);
+	lord_move<BLOCK, CAP, VbOp<IS_W, P, NEXT>, ENT>(recs, dsts, src, lx, a.lnext + sb, n, false, a.dst,
+	                                                a.first_level != 0, op);
 }
 
 // Long columns (skewed data: a popular item): one workgroup would stream the whole run while
@@ -574,13 +579,63 @@ __global__ __launch_bounds__(256) void k_rows_scatter(RowRec *__restrict__ dst, 
 	reinterpret_cast<double2 *>(dst + idx[p])[c] = reinterpret_cast<const double2 *>(src + p)[c];
 }
 
+// The entry store (data whose levels miss rows: multi-hot rows without fields): slot s of the
+// store is the s-th entry of the train set taken level by level (the level's columns in
+// ascending feature order, rows ascending in a column: the field store's order), and a row's
+// record waits in the slot of the entry its next level will sweep. A row's features ascend
+// with their levels (the schedule's definition), so its CSR entries come in level order: per
+// row, each entry's slot (its rank in its column by binary search), then for every slot the
+// slot of the row's next entry (the last entry -> the first: the next sweep), bit 31 on the
+// row's first entry (the q-cache restart), the entry's x, and the row's first slot. A row
+// without entries is never swept: its record waits in a parking slot past the entries, nnz + r.
+__global__ __launch_bounds__(256) void k_estore_build(const uint64_t *row_ptr, const uint2 *csr, const uint64_t *col_ptr,
+                                                      const uint2 *csc, const uint32_t *lvpos, const uint64_t *lcp,
+                                                      uint32_t n, uint64_t nnz, uint32_t *lnext, float *lx,
+                                                      uint32_t *lfirst)
+{
+	const uint32_t r = blockIdx.x * 256u + threadIdx.x;
+	if (r >= n) return;
+	const uint64_t b = row_ptr[r], e = row_ptr[r + 1];
+	if (e == b) {
+		lfirst[r] = (uint32_t)(nnz + r);
+		return;
+	}
+	auto slot_of = [&](uint2 ent) -> uint32_t {
+		const uint32_t j = ent.x;
+		uint64_t lo = col_ptr[j], hi = col_ptr[j + 1];   // rows ascending: first entry with row >= r
+		const uint64_t c0 = lo;
+		while (lo < hi) {
+			const uint64_t mid = (lo + hi) >> 1;
+			if ((csc[mid].x & ROW_MASK) < r) lo = mid + 1;
+			else hi = mid;
+		}
+		return (uint32_t)(lcp[lvpos[j]] + (lo - c0));
+	};
+	const uint32_t s0 = slot_of(csr[b]);
+	uint32_t s = s0;
+	for (uint64_t p = b; p < e; ++p) {
+		const uint32_t sn = p + 1 < e ? slot_of(csr[p + 1]) : s0;
+		lnext[s] = sn | (p == b ? ENT_FIRST : 0u);
+		if (lx) lx[s] = ent_x(csr[p]);
+		s = sn;
+	}
+	lfirst[r] = s0;
+}
+
 template <bool IS_W, int P, bool NEXT>
 void launch_lord(const LevelArgs &a, hipStream_t s)
 {
-	if (a.avg_len <= 96) k_level_lord<64, 2, IS_W, P, NEXT><<<a.nfeat, 64, 0, s>>>(a);
-	else if (a.avg_len <= 320) k_level_lord<256, 1, IS_W, P, NEXT><<<a.nfeat, 256, 0, s>>>(a);
-	else if (a.avg_len <= 640) k_level_lord<256, 2, IS_W, P, NEXT><<<a.nfeat, 256, 0, s>>>(a);
-	else k_level_lord<512, 2, IS_W, P, NEXT><<<a.nfeat, 512, 0, s>>>(a);
+	if (a.ent) {
+		if (a.avg_len <= 96) k_level_lord<64, 2, IS_W, P, NEXT, true><<<a.nfeat, 64, 0, s>>>(a);
+		else if (a.avg_len <= 320) k_level_lord<256, 1, IS_W, P, NEXT, true><<<a.nfeat, 256, 0, s>>>(a);
+		else if (a.avg_len <= 640) k_level_lord<256, 2, IS_W, P, NEXT, true><<<a.nfeat, 256, 0, s>>>(a);
+		else k_level_lord<512, 2, IS_W, P, NEXT, true><<<a.nfeat, 512, 0, s>>>(a);
+		return;
+	}
+	if (a.avg_len <= 96) k_level_lord<64, 2, IS_W, P, NEXT, false><<<a.nfeat, 64, 0, s>>>(a);
+	else if (a.avg_len <= 320) k_level_lord<256, 1, IS_W, P, NEXT, false><<<a.nfeat, 256, 0, s>>>(a);
+	else if (a.avg_len <= 640) k_level_lord<256, 2, IS_W, P, NEXT, false><<<a.nfeat, 256, 0, s>>>(a);
+	else k_level_lord<512, 2, IS_W, P, NEXT, false><<<a.nfeat, 512, 0, s>>>(a);
 }
 
 template <bool IS_W, int P>
@@ -1165,6 +1220,15 @@ hipError_t rows_gather(RowRec *dst, const RowRec *src, const uint32_t *idx, uint
 {
 	if (n == 0) return hipSuccess;
 	k_rows_gather<<<(unsigned)(((uint64_t)n * 4 + 255) / 256), 256, 0, s>>>(dst, src, idx, n);
+	return hipGetLastError();
+}
+
+hipError_t estore_build(const uint64_t *row_ptr, const uint2 *csr, const uint64_t *col_ptr, const uint2 *csc,
+                        const uint32_t *lvpos, const uint64_t *lcp, uint32_t n, uint64_t nnz, uint32_t *lnext,
+                        float *lx, uint32_t *lfirst, hipStream_t s)
+{
+	if (n == 0) return hipSuccess;
+	k_estore_build<<<(n + 255) / 256, 256, 0, s>>>(row_ptr, csr, col_ptr, csc, lvpos, lcp, n, nnz, lnext, lx, lfirst);
 	return hipGetLastError();
 }
 

@@ -447,6 +447,7 @@ int vbfm_mcmc_init(vbfm_ctx *c, const vbfm_mcmc_config *cfg)
 		if (c->shard_mode == VBFM_SHARD_FEATURES)
 			throw std::string("feature shards are implemented for the VB learner only");
 		mc_free(c);
+		if (c->estore) lord_release(c, true);   // the MCMC sweeps run on the field store or the columns
 		c->mc = new McState();
 		McState &m = *c->mc;
 		for (int i = 0; i < MEV_N; i++) HIPCHK(hipEventCreate(&m.ev[i]));

@@ -30,7 +30,7 @@ P_u32, P_u64, P_f32, P_f64, P_u8 = (C.POINTER(C.c_uint32), C.POINTER(C.c_uint64)
                                     C.POINTER(C.c_double), C.POINTER(C.c_uint8))
 
 
-LAYOUTS = {"auto": 0, "column": 1, "level": 2}   # VBFM_LAYOUT_* (include/vbfm.h)
+LAYOUTS = {"auto": 0, "column": 1, "level": 2, "entry": 3}   # VBFM_LAYOUT_* (include/vbfm.h)
 SYNTH_MODEL_SEED = 7   # tests/synth.py MODEL_SEED: the planted model shared by train, test and all shards
 
 
@@ -351,11 +351,12 @@ class FMLearnVB:
         _check(lib().vbfm_set_shard_mode(self._ctx, {"rows": 0, "features": 1}[mode], int(num_shards)), self._ctx)
 
     def layout(self):
-        """Row layout in use for the sweeps: "column" (row order, gather) or "level"
-        (records kept in the current level's column order, streamed)."""
+        """Row layout in use for the sweeps: "column" (row order, gather), "level" (records
+        kept in the current level's column order, streamed) or "entry" (one slot per train
+        entry, for levels that miss rows)."""
         v = C.c_int32()
         _check(lib().vbfm_get_layout(self._ctx, C.byref(v)), self._ctx)
-        return {1: "column", 2: "level"}[v.value]
+        return {1: "column", 2: "level", 3: "entry"}[v.value]
 
     # -- parameters ---------------------------------------------------------------------
     def _params_struct(self, arrs):

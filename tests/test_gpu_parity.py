@@ -494,12 +494,13 @@ def test_long_column_segments_edge_cases(case, monkeypatch):
 
 def test_level_layout_refused_when_levels_incomplete():
     """tiny has rows of different lengths: a level misses rows, the level layout cannot
-    apply -- auto falls back to the column layout, an explicit request fails loudly."""
+    apply -- auto takes the entry store, an explicit level request fails loudly."""
     d = os.path.join(GOLDEN, "tiny")
     train = vbfm.DataSubset.load(os.path.join(d, "train.libfm"))
     test = vbfm.DataSubset.load(os.path.join(d, "test.libfm"))
     g = gpu_learner(train, test, "1,1,3", 5, 0.1)
-    assert g.layout() == "column"
+    g.init_caches()
+    assert g.layout() == "entry"
     D = vbfm.num_all_attribute(train, test)
     g2 = vbfm.FMLearnVB(1, 1, 3, D, min_target=train.min_target, max_target=train.max_target, layout="level")
     g2.init(5, 0.1)

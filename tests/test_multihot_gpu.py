@@ -35,15 +35,18 @@ def test_device_multihot_generator_matches_spec(row_offset):
     np.testing.assert_array_equal(tg, y)
 
 
+@pytest.mark.parametrize("layout", ["auto", "column"])
 @pytest.mark.parametrize("k", [1, 6])
-def test_multihot_two_iterations_vs_oracle(k):
+def test_multihot_two_iterations_vs_oracle(k, layout):
+    """layout auto = the entry store (the levels miss rows: one slot per entry, records moved
+    to their rows' next slots), column = the column-gather layout."""
     n, D, lo, hi = 30_000, 4000, 5, 60
-    g = vbfm.FMLearnVB(1, 1, k, D + 1, min_target=1.0, max_target=5.0)
+    g = vbfm.FMLearnVB(1, 1, k, D + 1, min_target=1.0, max_target=5.0, layout=layout)
     g.init(7, 0.1)
     g.synth_multihot(0, n, D, lo, hi, 1000, 1)
     g.synth_multihot(1, 3000, D, lo, hi, 500000, 1)
     g.init_caches()
-    assert g.layout() == "column"
+    assert g.layout() == ("entry" if layout == "auto" else "column")
     tr = synth.generate_multihot(n, D, lo, hi, 1000, 1)
     te = synth.generate_multihot(3000, D, lo, hi, 500000, 1)
     o = oc.VB(1, 1, k, D + 1)
@@ -57,3 +60,56 @@ def test_multihot_two_iterations_vs_oracle(k):
         assert abs(st.free_energy - o.s.last_free_energy) <= REL * abs(o.s.last_free_energy)
     assert st.num_levels > 100                  # long dependency chains: many small levels
     assert rel_err(g.get_params()["mu_v"], o.params()["mu_v"]) <= REL
+
+
+@pytest.mark.parametrize("xmode", [0, 1])
+def test_entry_store_equals_column_layout(xmode):
+    """The entry store sweeps every column's entries in the column layout's order with the same
+    per-thread assignment and reduction tree, and the data-set sums (w0, alpha, free energy,
+    train quirk) add the rows in row order on both: the two layouts agree bit for bit over three
+    iterations (x = 1 without a stored x array, and x ~ U(0.5, 1.5))."""
+    n, D, lo, hi, k = 20_000, 3000, 3, 40, 4
+    res = {}
+    for layout in ("entry", "column"):
+        g = vbfm.FMLearnVB(1, 1, k, D + 1, min_target=1.0, max_target=5.0, layout=layout)
+        g.init(7, 0.1)
+        g.synth_multihot(0, n, D, lo, hi, 1000, xmode)
+        g.synth_multihot(1, 2000, D, lo, hi, 500000, xmode)
+        g.init_caches()
+        assert g.layout() == layout
+        st = [g.iterate() for _ in range(3)]
+        res[layout] = ([(s.rmse, s.free_energy, s.alpha, s.mu_0_dash, s.train_quirk) for s in st],
+                       g.get_params()["mu_v"], g.rows()["e"])
+        g.close()
+    assert res["entry"][0] == res["column"][0]
+    np.testing.assert_array_equal(res["entry"][1], res["column"][1])
+    np.testing.assert_array_equal(res["entry"][2], res["column"][2])
+
+
+def test_entry_store_refused_where_it_cannot_apply(monkeypatch):
+    """A row listing a feature twice puts it twice in one level: auto falls back to the column
+    layout, an explicit entry request fails loudly; VBFM_ESTORE=0 keeps the column layout."""
+    import os
+    from conftest import GOLDEN
+    d = os.path.join(GOLDEN, "tiny_dup")
+    train = vbfm.DataSubset.load(os.path.join(d, "train.libfm"))
+    test = vbfm.DataSubset.load(os.path.join(d, "test.libfm"))
+    D = vbfm.num_all_attribute(train, test)
+    for layout, expect in (("auto", "column"), ("entry", None)):
+        g = vbfm.FMLearnVB(1, 1, 3, D, min_target=train.min_target, max_target=train.max_target, layout=layout)
+        g.init(5, 0.1)
+        g.set_data(train, test)
+        if expect is None:
+            with pytest.raises(vbfm.VbfmError, match="entry store not possible"):
+                g.init_caches()
+        else:
+            g.init_caches()
+            assert g.layout() == expect
+        g.close()
+    monkeypatch.setenv("VBFM_ESTORE", "0")
+    g = vbfm.FMLearnVB(1, 1, 3, 3001, min_target=1.0, max_target=5.0)
+    g.init(5, 0.1)
+    g.synth_multihot(0, 5000, 3000, 3, 20, 1, 0)
+    g.synth_multihot(1, 500, 3000, 3, 20, 2, 0)
+    g.init_caches()
+    assert g.layout() == "column"

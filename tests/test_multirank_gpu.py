@@ -176,9 +176,10 @@ def test_vb_row_shards_match_one_rank(world, kind, layout):
     column layout) vs the un-sharded data set: RMSE, free energy, alpha per iteration and the
     final parameters within 1e-9."""
     s, r = _launch(world, kind, "vb", layout)
-    assert s["layout"] == r["layout"]
-    if kind == "ragged":
-        assert s["layout"] == "column"
+    if kind == "ragged":   # row shards: the column layout; one rank: the entry store (auto)
+        assert s["layout"] == "column" and r["layout"] in ("column", "entry")
+    else:
+        assert s["layout"] == r["layout"]
     assert s["levels"] == r["levels"]
     for key in ("rmse", "fe", "alpha"):
         for a, b in zip(s[key], r[key]):
