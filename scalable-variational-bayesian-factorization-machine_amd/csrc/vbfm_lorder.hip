@@ -837,17 +837,30 @@ __global__ __launch_bounds__(256) void k_lord_prev_fill(const uint32_t *feats, c
 	}
 }
 
+// the longest mean column the deferred kernels run with the 64 x 2 shape: 128 (a run still
+// fits its 128 slots); at C4's per-rank shape on 8 GPUs (1.25e7 rows, ~100 per column) the
+// level takes 0.467 ms against 0.475 with 256 x 1 (profiles/probes/ab_defer_small_shape.txt).
+// VBFM_SMALL_MAX overrides.
+inline uint32_t small_max()
+{
+	static const uint32_t v = [] {
+		const char *e = getenv("VBFM_SMALL_MAX");
+		return e ? (uint32_t)atoi(e) : 128u;
+	}();
+	return v;
+}
+
 template <bool IS_W, int P, bool NEXT, int PK>
 void launch_defer_pk(const LevelArgs &a, hipStream_t s)
 {
 	if (a.lpay2) {   // every x 1: 8-B payloads
-		if (a.avg_len <= 96) k_lord_defer<64, 2, IS_W, P, NEXT, PK, true><<<a.nfeat, 64, 0, s>>>(a);
+		if (a.avg_len <= small_max()) k_lord_defer<64, 2, IS_W, P, NEXT, PK, true><<<a.nfeat, 64, 0, s>>>(a);
 		else if (a.avg_len <= 320) k_lord_defer<256, 1, IS_W, P, NEXT, PK, true><<<a.nfeat, 256, 0, s>>>(a);
 		else if (a.avg_len <= 640) k_lord_defer<256, 2, IS_W, P, NEXT, PK, true><<<a.nfeat, 256, 0, s>>>(a);
 		else k_lord_defer<512, 2, IS_W, P, NEXT, PK, true><<<a.nfeat, 512, 0, s>>>(a);
 		return;
 	}
-	if (a.avg_len <= 96) k_lord_defer<64, 2, IS_W, P, NEXT, PK, false><<<a.nfeat, 64, 0, s>>>(a);
+	if (a.avg_len <= small_max()) k_lord_defer<64, 2, IS_W, P, NEXT, PK, false><<<a.nfeat, 64, 0, s>>>(a);
 	else if (a.avg_len <= 320) k_lord_defer<256, 1, IS_W, P, NEXT, PK, false><<<a.nfeat, 256, 0, s>>>(a);
 	else if (a.avg_len <= 640) k_lord_defer<256, 2, IS_W, P, NEXT, PK, false><<<a.nfeat, 256, 0, s>>>(a);
 	else k_lord_defer<512, 2, IS_W, P, NEXT, PK, false><<<a.nfeat, 512, 0, s>>>(a);
@@ -1000,13 +1013,13 @@ template <bool IS_W, int P, bool NEXT>
 void launch_mc_defer(const McArgs &a, hipStream_t s)
 {
 	if (a.lpay2) {   // every x 1: 8-B payloads
-		if (a.avg_len <= 96) k_mc_lord_defer<64, 2, IS_W, P, NEXT, true><<<a.nfeat, 64, 0, s>>>(a);
+		if (a.avg_len <= small_max()) k_mc_lord_defer<64, 2, IS_W, P, NEXT, true><<<a.nfeat, 64, 0, s>>>(a);
 		else if (a.avg_len <= 320) k_mc_lord_defer<256, 1, IS_W, P, NEXT, true><<<a.nfeat, 256, 0, s>>>(a);
 		else if (a.avg_len <= 640) k_mc_lord_defer<256, 2, IS_W, P, NEXT, true><<<a.nfeat, 256, 0, s>>>(a);
 		else k_mc_lord_defer<512, 2, IS_W, P, NEXT, true><<<a.nfeat, 512, 0, s>>>(a);
 		return;
 	}
-	if (a.avg_len <= 96) k_mc_lord_defer<64, 2, IS_W, P, NEXT, false><<<a.nfeat, 64, 0, s>>>(a);
+	if (a.avg_len <= small_max()) k_mc_lord_defer<64, 2, IS_W, P, NEXT, false><<<a.nfeat, 64, 0, s>>>(a);
 	else if (a.avg_len <= 320) k_mc_lord_defer<256, 1, IS_W, P, NEXT, false><<<a.nfeat, 256, 0, s>>>(a);
 	else if (a.avg_len <= 640) k_mc_lord_defer<256, 2, IS_W, P, NEXT, false><<<a.nfeat, 256, 0, s>>>(a);
 	else k_mc_lord_defer<512, 2, IS_W, P, NEXT, false><<<a.nfeat, 512, 0, s>>>(a);
