@@ -165,7 +165,7 @@ def main():
                     help="rows: exact row shards, each rank its own rows (weak scaling, default); "
                          "features: the north star's column partition, every rank all rows (strong "
                          "scaling, Jacobi across shards)")
-    ap.add_argument("--layout", default="auto", choices=["auto", "column", "level"],
+    ap.add_argument("--layout", default="auto", choices=["auto", "column", "level", "entry"],
                     help="row-cache layout of the sweeps (include/vbfm.h VBFM_LAYOUT_*)")
     ap.add_argument("--scaling", default="strong", choices=["strong", "weak"],
                     help="row shards: strong = the config's rows in total (default), weak = per rank")
