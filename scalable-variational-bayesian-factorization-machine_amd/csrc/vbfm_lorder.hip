@@ -837,15 +837,16 @@ __global__ __launch_bounds__(256) void k_lord_prev_fill(const uint32_t *feats, c
 	}
 }
 
-// the longest mean column the deferred kernels run with the 64 x 2 shape: 128 (a run still
-// fits its 128 slots); at C4's per-rank shape on 8 GPUs (1.25e7 rows, ~100 per column) the
-// level takes 0.467 ms against 0.475 with 256 x 1 (profiles/probes/ab_defer_small_shape.txt).
-// VBFM_SMALL_MAX overrides.
+// the longest mean column the deferred kernels run with the 64 x 2 shape: 96, the fused and
+// column kernels' threshold -- the same workgroup shape gives the same reduction tree, which
+// keeps the split sweeps bit-identical to the fused ones. (128 would make C4's per-rank level on
+// 8 GPUs 1.7 % faster, profiles/probes/ab_defer_small_shape.txt, at the price of that identity.)
+// VBFM_SMALL_MAX overrides (A/B only).
 inline uint32_t small_max()
 {
 	static const uint32_t v = [] {
 		const char *e = getenv("VBFM_SMALL_MAX");
-		return e ? (uint32_t)atoi(e) : 128u;
+		return e ? (uint32_t)atoi(e) : 96u;
 	}();
 	return v;
 }

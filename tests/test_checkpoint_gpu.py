@@ -39,13 +39,19 @@ def _trace(stats):
     return [(s.rmse, s.mae, s.train_quirk, s.free_energy, s.alpha, s.mu_0_dash) for s in stats]
 
 
-@pytest.mark.parametrize("split", ["0", "1"])
-@pytest.mark.parametrize("layout", ["level", "column"])
+@pytest.mark.parametrize("split,layout", [("0", "level"), ("0", "column"), ("1", "level"), ("1", "column"),
+                                          ("0", "entry")])
 def test_resume_continues_bit_for_bit(layout, split, tmp_path, monkeypatch):
     """4 iterations in one go against 2 + save, then load into a fresh context + 2: equal
-    bit for bit (level-ordered store and column layout, fused and deferred-split sweeps)."""
+    bit for bit (level-ordered store, column layout and entry store; fused and deferred-split
+    sweeps). The entry store runs on multi-hot rows (its levels miss rows)."""
     monkeypatch.setenv("VBFM_FORCE_SPLIT", split)
-    tr, te, nf = _data()
+    if layout == "entry":
+        tr = synth.generate_multihot(8000, 1500, 3, 30, 41, 1)
+        te = synth.generate_multihot(800, 1500, 3, 30, 42, 1)
+        nf = 1500
+    else:
+        tr, te, nf = _data()
     k = 5
     a = _learner(tr, te, nf, k, layout)
     a.init_caches()
