@@ -53,3 +53,20 @@ def test_two_rank_bench_matches_one_rank(scaling):
     _close(two["free_energy"], one["free_energy"])
     assert one["test_rmse_trace"][-1] < one["test_rmse_trace"][0]
     assert len(one["rccl_libs"]) <= 1 and len(two["rccl_libs"]) <= 1
+
+
+def test_eight_rank_bench_matches_one_rank():
+    """The driver's N = 8 launch rehearsed on one GPU: `--gpus 8` spawns eight rank processes
+    (one per GPU on a node; here they share the card through the host exchange), each owning
+    1/8 of the rows (strong scaling), the level schedule max-reduced over the ranks, the
+    deferred split sweeps with a per-level all-reduce of 8 shards' statistics -- the same run
+    as one rank over all rows."""
+    eight = _bench("--gpus", "8", "--transport", "host")
+    assert eight["n_gpus"] == 8 and eight["n_ranks_seen"] == 8 and eight["transport"] == "host"
+    assert eight["config"]["rows_total"] == 200_000 and eight["config"]["rows_per_gpu"] == 25_000
+    assert eight["config"]["parallelism"] == "row-sharded dp8"
+    one = _bench("--rows", "200000")
+    for a, b in zip(eight["test_rmse_trace"], one["test_rmse_trace"]):
+        assert abs(a - b) <= 1e-8 * b, (eight["test_rmse_trace"], one["test_rmse_trace"])
+    _close(eight["test_rmse"], one["test_rmse"])
+    _close(eight["free_energy"], one["free_energy"])
