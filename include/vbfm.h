@@ -176,7 +176,7 @@ int vbfm_get_test_e(vbfm_ctx *ctx, double *e /*[test rows]*/);
  *   VBFM_LAYOUT_ENTRY  for levels that miss rows (multi-hot rows without fields): one slot per
  *                      train entry in the level order, a row's record in the slot of the entry
  *                      its next level sweeps; levels stream their runs and move each record to
- *                      its row's next slot (nnz x 64 B of HBM; VB, one rank). AUTO picks it
+ *                      its row's next slot (nnz x 64 B of HBM; one rank). AUTO picks it
  *                      where LEVEL does not apply and it fits (VBFM_ESTORE=0: COLUMN instead).
  * Set before vbfm_set_train; VBFM_LAYOUT=auto|column|level|entry in the environment overrides.
  * vbfm_get_layout reports the layout in use (COLUMN, LEVEL or ENTRY) once the train set is known. */

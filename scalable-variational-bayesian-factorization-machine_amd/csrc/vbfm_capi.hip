@@ -184,7 +184,7 @@ static void build_long_segs(vbfm_ctx *c, const std::vector<uint64_t> &lcp, const
 // the entry its next level sweeps, so a level streams its columns' runs and scatters each
 // record to the row's next slot (k_level_lord<..., ENT>) instead of gathering and writing back
 // rows in place (the column-gather layout: two random touches per entry).
-// Single rank, fused sweeps, no row listing a feature twice, the VB learner; the store must
+// Single rank, fused sweeps, no row listing a feature twice (VB and MCMC / ALS); the store must
 // fit in half the free memory. A row without entries parks its record in slot nnz + r.
 // Returns false when it does not apply (force: throw instead).
 bool build_estore(vbfm_ctx *c, const std::vector<uint64_t> &lcp, const std::vector<uint8_t> &dup,
@@ -197,7 +197,6 @@ bool build_estore(vbfm_ctx *c, const std::vector<uint64_t> &lcp, const std::vect
 	size_t fr = 0, tot = 0;
 	HIPCHK(hipMemGetInfo(&fr, &tot));
 	if (!force && env && env[0] == '0') why = "VBFM_ESTORE=0";
-	else if (c->mc) why = "the MCMC / ALS sweeps";
 	else if (c->row_comm() || c->force_split) why = "row shards (split sweeps)";
 	else if (n == 0 || d.nnz == 0) why = "no train entries";
 	else if (d.nnz + n >= 0x80000000ull) why = "more than 2^31 entries and rows";

@@ -159,6 +159,7 @@ struct McArgs {
 	// (the accumulators start), 2 a later factor; par_prev = v_{f-1} (stride next_stride)
 	const double2 *par_prev;
 	int pk;
+	int ent;                   // the entry store (as LevelArgs::ent; fused sweeps only)
 };
 
 // kernels launched from the C-ABI layer (vbfm_kernels.hip)

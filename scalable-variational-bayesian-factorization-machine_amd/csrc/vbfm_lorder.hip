@@ -449,7 +449,7 @@ __global__ __launch_bounds__(BLOCK) void k_level_lord_move(LevelArgs a)
 // MODE 0: fused; 1: statistics of this shard's rows into a.stats; 2: draw from the
 // all-reduced a.stats, correct and move. Launch shape (BLOCK) as the column-gather MCMC
 // kernel so that both reduce a column in the same order.
-template <int BLOCK, int R, bool IS_W, int P, bool NEXT, int MODE>
+template <int BLOCK, int R, bool IS_W, int P, bool NEXT, int MODE, bool ENT = false>
 __global__ __launch_bounds__(BLOCK) void k_mc_level_lord(McArgs a)
 {
 	constexpr uint32_t CAP = BLOCK * R;
@@ -480,7 +480,7 @@ __global__ __launch_bounds__(BLOCK) void k_mc_level_lord(McArgs a)
 			op.go = mc_draw(sm, ss, op.vo, a.lambda[(size_t)g * a.hstride], a.mu[(size_t)g * a.hstride], a.alpha,
 			                mc_z(a, j), a.z != nullptr, a.sample, !IS_W, op.v, a.counters, threadIdx.x == 0);
 			if (threadIdx.x == 0) a.par[(size_t)j * a.stride].x = op.v;
-			res_move<BLOCK, R>(recs, dsts, n, xr, nr, a.dst, a.first_level != 0, op);
+			res_move<BLOCK, R, McOp<IS_W, P, NEXT>, ENT>(recs, dsts, n, xr, nr, a.dst, a.first_level != 0, op);
 			return;
 		}
 	}
@@ -501,7 +501,8 @@ __global__ __launch_bounds__(BLOCK) void k_mc_level_lord(McArgs a)
 		op.go = mc_draw(sm, ss, op.vo, a.lambda[(size_t)g * a.hstride], a.mu[(size_t)g * a.hstride], a.alpha,
 		                mc_z(a, j), a.z != nullptr, a.sample, !IS_W, op.v, a.counters, threadIdx.x == 0);
 		if (threadIdx.x == 0) a.par[(size_t)j * a.stride].x = op.v;
-		lord_move<BLOCK, CAP>(recs, dsts, src, lx, a.lnext + sb, n, false, a.dst, a.first_level != 0, op);
+		lord_move<BLOCK, CAP, McOp<IS_W, P, NEXT>, ENT>(recs, dsts, src, lx, a.lnext + sb, n, false, a.dst,
+		                                                a.first_level != 0, op);
 	}
 }
 
@@ -1026,20 +1027,30 @@ void launch_mc_defer(const McArgs &a, hipStream_t s)
 	else k_mc_lord_defer<512, 2, IS_W, P, NEXT, false><<<a.nfeat, 512, 0, s>>>(a);
 }
 
-template <int BLOCK, int R, int MODE>
-void launch_mc_lord(const McArgs &a, int is_w, hipStream_t s)
+template <int BLOCK, int R, int MODE, bool ENT>
+void launch_mc_lord_ent(const McArgs &a, int is_w, hipStream_t s)
 {
 	const bool nx = a.par_next != nullptr;
 	if (is_w) {
-		if (nx) k_mc_level_lord<BLOCK, R, true, 0, true, MODE><<<a.nfeat, BLOCK, 0, s>>>(a);
-		else k_mc_level_lord<BLOCK, R, true, 0, false, MODE><<<a.nfeat, BLOCK, 0, s>>>(a);
+		if (nx) k_mc_level_lord<BLOCK, R, true, 0, true, MODE, ENT><<<a.nfeat, BLOCK, 0, s>>>(a);
+		else k_mc_level_lord<BLOCK, R, true, 0, false, MODE, ENT><<<a.nfeat, BLOCK, 0, s>>>(a);
 	} else if (a.slot == 0) {
-		if (nx) k_mc_level_lord<BLOCK, R, false, 0, true, MODE><<<a.nfeat, BLOCK, 0, s>>>(a);
-		else k_mc_level_lord<BLOCK, R, false, 0, false, MODE><<<a.nfeat, BLOCK, 0, s>>>(a);
+		if (nx) k_mc_level_lord<BLOCK, R, false, 0, true, MODE, ENT><<<a.nfeat, BLOCK, 0, s>>>(a);
+		else k_mc_level_lord<BLOCK, R, false, 0, false, MODE, ENT><<<a.nfeat, BLOCK, 0, s>>>(a);
 	} else {
-		if (nx) k_mc_level_lord<BLOCK, R, false, 1, true, MODE><<<a.nfeat, BLOCK, 0, s>>>(a);
-		else k_mc_level_lord<BLOCK, R, false, 1, false, MODE><<<a.nfeat, BLOCK, 0, s>>>(a);
+		if (nx) k_mc_level_lord<BLOCK, R, false, 1, true, MODE, ENT><<<a.nfeat, BLOCK, 0, s>>>(a);
+		else k_mc_level_lord<BLOCK, R, false, 1, false, MODE, ENT><<<a.nfeat, BLOCK, 0, s>>>(a);
 	}
+}
+
+// the entry store runs the fused form only (one rank)
+template <int BLOCK, int R, int MODE>
+void launch_mc_lord(const McArgs &a, int is_w, hipStream_t s)
+{
+	if constexpr (MODE == 0) {
+		if (a.ent) return launch_mc_lord_ent<BLOCK, R, MODE, true>(a, is_w, s);
+	}
+	launch_mc_lord_ent<BLOCK, R, MODE, false>(a, is_w, s);
 }
 
 template <int MODE>

@@ -127,6 +127,7 @@ std::vector<double> mc_param_sums(vbfm_ctx *c, int mode, bool is_v)
 
 double mc_row_sum(vbfm_ctx *c, int mode, double w0)
 {
+	rows_dense(c);
 	HIPCHK(vbk::mc_row_sums(c->rows, c->tr.n, mode, w0, c->red_d, c->RED_BLOCKS, c->s));
 	double s = finish_sum(c, c->RED_BLOCKS);
 	allreduce_host(c, &s, 1);
@@ -156,6 +157,7 @@ void draw_w0(vbfm_ctx *c)   // :628-668 (w0_mean_0 = 0)
 	m.w0 = m.sample ? m.stream.gaussian(mean, std::sqrt(s2)) : mean;
 	if (std::isnan(m.w0)) { m.hc[HC_NAN_W0]++; m.w0 = old; return; }
 	if (std::isinf(m.w0)) { m.hc[HC_INF_W0]++; m.w0 = old; return; }
+	rows_dense(c);
 	HIPCHK(vbk::mc_e_shift(c->rows, c->tr.n, old - m.w0, c->s));
 }
 
@@ -316,6 +318,14 @@ void mc_sweep(vbfm_ctx *c, bool is_w, int f)
 			a.src = c->rows;
 			a.dst = c->rows_alt;
 			a.first_level = l == 0;
+			if (c->estore) {   // one store, global slots: each record to its row's next slot
+				a.lbase = 0;
+				a.dst = c->rows;
+				a.ent = 1;
+				HIPCHK(vbk::mc_lord_level(a, 0, is_w, c->s));
+				prof_end(c, p);
+				continue;
+			}
 			if (!c->row_comm() && !c->force_split) {
 				HIPCHK(vbk::mc_lord_level(a, 0, is_w, c->s));
 			} else if (c->deferred()) {
@@ -447,7 +457,6 @@ int vbfm_mcmc_init(vbfm_ctx *c, const vbfm_mcmc_config *cfg)
 		if (c->shard_mode == VBFM_SHARD_FEATURES)
 			throw std::string("feature shards are implemented for the VB learner only");
 		mc_free(c);
-		if (c->estore) lord_release(c, true);   // the MCMC sweeps run on the field store or the columns
 		c->mc = new McState();
 		McState &m = *c->mc;
 		for (int i = 0; i < MEV_N; i++) HIPCHK(hipEventCreate(&m.ev[i]));
