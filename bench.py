@@ -23,6 +23,7 @@ model (tests/synth.py), so test RMSE falls as the model fits.
 """
 import argparse
 import json
+import math
 import os
 import subprocess
 import sys
@@ -267,7 +268,16 @@ def main():
         fml.init_caches()
     launch_events = not online and not args.no_launch_events
     if launch_events:   # per-launch event pairs: the online epoch has num_batch * k * levels launches
-        fml.set_profiling(True)
+        # short level launches (many levels): an event pair costs up to ~4.5 us of device time
+        # on some boxes, so time a sample -- every stride-th launch, stride coprime with the
+        # level count so that every level is sampled alike
+        n_lev = fml.levels()[1]
+        stride = 1
+        if n_lev * k > 8000:
+            stride = 16
+            while math.gcd(stride, n_lev) != 1:
+                stride += 1
+        fml.set_profiling(True, stride)
     layout = fml.layout()
     nnz = fml.shape(0)[2]                # this rank's train entries
     log("rank %d: setup %.1f s (N=%d F=%d S=%d features=%d nnz=%d k=%d, %s layout)" % (

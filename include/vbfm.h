@@ -188,7 +188,7 @@ int vbfm_set_layout(vbfm_ctx *ctx, int32_t layout);
 int vbfm_get_layout(vbfm_ctx *ctx, int32_t *layout);
 
 /* per-launch event timing of the sweep kernels inside vbfm_iterate (off by default) */
-int vbfm_set_profiling(vbfm_ctx *ctx, int32_t on);
+int vbfm_set_profiling(vbfm_ctx *ctx, int32_t on);   /* on > 1: time every on-th launch of a kind */
 
 /* ---- checkpoint / resume ----------------------------------------------------------------
  * No reference counterpart: the reference always starts from its initial draws

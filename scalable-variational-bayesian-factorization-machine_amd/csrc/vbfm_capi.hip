@@ -484,6 +484,38 @@ void check_schedule(vbfm_ctx *c)
 	if (nb) throw std::string("VBFM_CHECK: dependency schedule violated (") + std::to_string(nb) + " row claims)";
 }
 
+// The levels in Kahn's order (vbfm_kernels.hip k_kahn_*): rounds are queued 32 at a time; one
+// read of the append counter per batch tells when every feature has its level.
+static void kahn_levels(vbfm_ctx *c, uint32_t *level)
+{
+	DevData &d = c->tr;
+	const uint32_t nf = d.nf;
+	c->sched_kahn = true;
+	if (nf == 0) return;
+	const int batch = 32;
+	const size_t nb = (size_t)nf + 2 * batch + 3;
+	uint32_t *indeg = dalloc<uint32_t>(nf), *order = dalloc<uint32_t>(nf), *tail = dalloc<uint32_t>(1);
+	uint32_t *bounds = dalloc<uint32_t>(nb);
+	HIPCHK(vbk::kahn_init(d.row_ptr, d.csr, d.n, nf, indeg, level, order, tail, bounds, c->s));
+	uint32_t prev = 0xFFFFFFFFu;
+	for (int t = 0;; t += batch) {
+		if ((size_t)t + batch + 2 >= nb) throw std::string("level schedule did not converge");
+		for (int u = t; u < t + batch; u++)
+			HIPCHK(vbk::kahn_round(d.col_ptr, d.csc, d.row_ptr, d.csr, bounds, u, indeg, level, order, tail, c->s));
+		uint32_t tl = 0;
+		HIPCHK(hipMemcpyAsync(&tl, tail, 4, hipMemcpyDeviceToHost, c->s));
+		sync(c);
+		c->sched_rounds += batch;
+		if (tl == nf) break;
+		if (tl == prev || tl > nf) throw std::string("level schedule did not converge (a feature cycle)");
+		prev = tl;
+	}
+	dfree(indeg);
+	dfree(order);
+	dfree(tail);
+	dfree(bounds);
+}
+
 // Dependency levels of the train features (see vbfm_kernels.hip header). With several
 // row shards every round's levels are max-reduced over the shards, so all ranks share one
 // schedule: the one the un-sharded data set defines.
@@ -499,7 +531,19 @@ void build_schedule(vbfm_ctx *c)
 	HIPCHK(vbk::level_init(level, nf, c->s));
 	HIPCHK(vbk::mark_dups(d.row_ptr, d.csr, d.n, c->dup, c->s));
 	if (c->multi() && nf) allreduce_dev(c, c->dup, nf, ncclUint8, ncclMax);
-	for (int round = 0;; round++) {
+	// VBFM_SCHEDULE: "relax" (rounds to the fixed point), "kahn" (one pass in Kahn's order), default:
+	// relaxation rounds while they are cheap (field-structured data converges in two), then
+	// Kahn's order; row shards relax (every round is max-reduced over the shards)
+	const char *sm = getenv("VBFM_SCHEDULE");
+	const int mode = c->multi() ? 0 : (sm && !strcmp(sm, "relax")) ? 0 : (sm && !strcmp(sm, "kahn")) ? 2 : 1;
+	c->sched_rounds = 0;
+	c->sched_kahn = false;
+	for (int round = 0; mode != 2; round++) {
+		if (mode == 1 && round == 3) {
+			kahn_levels(c, level);
+			break;
+		}
+		c->sched_rounds++;
 		uint32_t ch = 0;
 		HIPCHK(hipMemsetAsync(changed, 0, 4, c->s));
 		HIPCHK(vbk::level_relax(d.row_ptr, d.csr, d.n, nf, level, changed, c->s));
@@ -512,6 +556,7 @@ void build_schedule(vbfm_ctx *c)
 		if (!ch) break;
 		if (round > (int)nf + 2) throw std::string("level schedule did not converge");
 	}
+	if (mode == 2) kahn_levels(c, level);
 	c->level_h.assign(nf, 0);
 	if (nf) HIPCHK(hipMemcpy(c->level_h.data(), level, nf * 4, hipMemcpyDeviceToHost));
 	dfree(level);
@@ -663,7 +708,8 @@ LevelArgs level_args(vbfm_ctx *c, uint32_t l, bool is_w, int f)
 // event pair around one launch when profiling (the pool grows on first use)
 size_t prof_begin(vbfm_ctx *c, int kind)
 {
-	if (!c->profiling) return 0;
+	if (!c->profiling) return NO_SPAN;
+	if (c->prof_stride > 1 && c->prof_tick[kind]++ % (uint64_t)c->prof_stride != 0) return NO_SPAN;
 	if (c->pev_used + 2 > c->pev.size()) {
 		const size_t add = std::max<size_t>(256, c->pev.size());
 		for (size_t i = 0; i < add; i++) {
@@ -683,7 +729,7 @@ size_t prof_begin(vbfm_ctx *c, int kind)
 
 void prof_end(vbfm_ctx *c, size_t a)
 {
-	if (c->profiling) HIPCHK(hipEventRecord(c->pev[a + 1], c->s));
+	if (c->profiling && a != NO_SPAN) HIPCHK(hipEventRecord(c->pev[a + 1], c->s));
 }
 
 void sweep_level(vbfm_ctx *c, uint32_t l, bool is_w, int f)
@@ -1757,6 +1803,8 @@ int vbfm_set_profiling(vbfm_ctx *c, int32_t on)
 {
 	if (!c) return fail(nullptr, "null context");
 	c->profiling = on != 0;
+	c->prof_stride = on > 1 ? on : 1;
+	for (auto &t : c->prof_tick) t = 0;
 	return 0;
 }
 

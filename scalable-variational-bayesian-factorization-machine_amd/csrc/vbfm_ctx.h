@@ -106,6 +106,8 @@ struct vbfm_ctx {
 	uint32_t *level_feats = nullptr;
 	uint8_t *dup = nullptr;
 	bool sched_ready = false;
+	int sched_rounds = 0;          // relaxation rounds (+ Kahn rounds queued) of the last schedule
+	bool sched_kahn = false;       // the last schedule came from Kahn's order
 	// reductions
 	static constexpr uint32_t RED_BLOCKS = 512;
 	double *red_d = nullptr;
@@ -129,6 +131,8 @@ struct vbfm_ctx {
 	hipEvent_t ev[vbi::EV_N] = {};
 	// per-launch profiling (vbfm_set_profiling)
 	bool profiling = false;
+	int prof_stride = 1;             // event pair around every prof_stride-th launch of a kind
+	uint64_t prof_tick[3] = {0, 0, 0};
 	std::vector<hipEvent_t> pev;
 	size_t pev_used = 0;
 	struct Span { size_t a; int kind; };   // kind 0 = v level, 1 = w level, 2 = qcache
@@ -214,6 +218,7 @@ void allreduce_dev(vbfm_ctx *c, void *buf, size_t n, ncclDataType_t t, ncclRedOp
 double finish_sum(vbfm_ctx *c, uint32_t nblocks);
 void require_train(vbfm_ctx *c);
 uint32_t nlevels(vbfm_ctx *c);
+constexpr size_t NO_SPAN = ~(size_t)0;   // prof_begin: this launch is not timed
 size_t prof_begin(vbfm_ctx *c, int kind);
 void prof_end(vbfm_ctx *c, size_t a);
 int blocked_predict(const vbfm_ctx *c, const DevData &d);

@@ -262,6 +262,13 @@ hipError_t level_init(uint32_t *level, uint32_t nf, hipStream_t s);
 hipError_t level_relax(const uint64_t *row_ptr, const uint2 *csr, uint32_t n, uint32_t nf, uint32_t *level,
                        uint32_t *changed, hipStream_t s);
 hipError_t mark_dups(const uint64_t *row_ptr, const uint2 *csr, uint32_t n, uint8_t *dup, hipStream_t s);
+// the same levels in Kahn's order: edge counts + the level-1 frontier (bounds[0..1]), then one
+// frontier per round (round t: level t+1 in order[bounds[t]..bounds[t+1]), closes bounds[t+2])
+hipError_t kahn_init(const uint64_t *row_ptr, const uint2 *csr, uint32_t n, uint32_t nf, uint32_t *indeg,
+                     uint32_t *level, uint32_t *order, uint32_t *tail, uint32_t *bounds, hipStream_t s);
+hipError_t kahn_round(const uint64_t *col_ptr, const uint2 *csc, const uint64_t *row_ptr, const uint2 *csr,
+                      uint32_t *bounds, int t, uint32_t *indeg, uint32_t *level, uint32_t *order, uint32_t *tail,
+                      hipStream_t s);
 // feature-sharded passes (vbfm_capi.hip fs_pass): save e/t and zero the next q-cache slot;
 // pack (or add) the shard's changes; unpack the summed changes; parameter exchange
 hipError_t fs_begin(RowRec *rows, uint32_t n, double *base, int next_slot, hipStream_t s);

@@ -979,6 +979,95 @@ __global__ void k_level_relax(const uint64_t *row_ptr, const uint2 *csr, uint32_
 	if (ch) atomicOr(changed, 1u);
 }
 
+// The same levels in one pass over the edges (Kahn's order, level-synchronous): the relaxation
+// needs one round per row switch on the longest path (365 rounds of the whole CSR for the
+// multi-hot bench's 785 levels); here a feature's level is fixed in the round its last
+// predecessor is processed. Edges are counted per entry: every entry (r, j) has the edge to the
+// next distinct feature of row r, counted once per entry by k_kahn_indeg and consumed once per
+// entry by k_kahn_round, whatever the order of a column's rows or repeated ids.
+__global__ void k_kahn_indeg(const uint64_t *row_ptr, const uint2 *csr, uint32_t n, uint32_t *indeg)
+{
+	const uint32_t r = blockIdx.x * 256u + threadIdx.x;
+	if (r >= n) return;
+	const uint64_t b = row_ptr[r], e = row_ptr[r + 1];
+	if (e - b < 2) return;
+	uint32_t nx = csr[e - 1].x, cnt = 0;   // next distinct feature after the current run
+	for (uint64_t q = e - 1; q > b; --q) {
+		const uint32_t cur = csr[q - 1].x;
+		if (cur != csr[q].x) {
+			if (cnt) atomicAdd(&indeg[nx], cnt);
+			nx = csr[q].x;
+			cnt = 0;
+		}
+		if (cur != nx) cnt++;
+	}
+	if (cnt) atomicAdd(&indeg[nx], cnt);
+}
+
+// lanes with want append val to order[] (one atomic per wave); every lane of the wave calls
+DEVI void wave_append(bool want, uint32_t val, uint32_t *tail, uint32_t *order)
+{
+	const uint64_t m = __ballot(want);
+	if (!m) return;
+	const int lane = threadIdx.x & 63;
+	const int leader = __ffsll((unsigned long long)m) - 1;
+	uint32_t base = 0;
+	if (lane == leader) base = atomicAdd(tail, (uint32_t)__popcll(m));
+	base = __shfl(base, leader);
+	if (want) order[base + __popcll(m & ((1ull << lane) - 1ull))] = val;
+}
+
+__global__ __launch_bounds__(256) void k_kahn_seed(const uint32_t *indeg, uint32_t nf, uint32_t *level,
+                                                   uint32_t *order, uint32_t *tail)
+{
+	const uint32_t j = blockIdx.x * 256u + threadIdx.x;
+	const bool src = j < nf && indeg[j] == 0;
+	if (src) level[j] = 1;
+	wave_append(src, j, tail, order);
+}
+
+// frontier bounds: the features of level t+1 are order[bounds[t] .. bounds[t+1])
+__global__ void k_kahn_close(const uint32_t *tail, uint32_t *bounds, int slot)
+{
+	if (threadIdx.x == 0) bounds[slot] = *tail;
+}
+
+// round t: every entry of a frontier column consumes its edge; a feature whose last edge
+// goes gets level t+2 and joins the next frontier. One wave per column (lanes over entries).
+__global__ __launch_bounds__(256) void k_kahn_round(const uint64_t *col_ptr, const uint2 *csc, const uint64_t *row_ptr,
+                                                    const uint2 *csr, const uint32_t *bounds, int t, uint32_t *indeg,
+                                                    uint32_t *level, uint32_t *order, uint32_t *tail)
+{
+	const uint32_t s = bounds[t], e = bounds[t + 1];
+	const uint32_t lane = threadIdx.x & 63u;
+	const uint32_t nw = gridDim.x * 4u;
+	for (uint32_t i = s + ((blockIdx.x * 256u + threadIdx.x) >> 6); i < e; i += nw) {
+		const uint32_t j = order[i];
+		const uint64_t cb = col_ptr[j], ce = col_ptr[j + 1];
+		for (uint64_t p0 = cb; p0 < ce; p0 += 64) {
+			const uint64_t p = p0 + lane;
+			bool ready = false;
+			uint32_t nxt = 0;
+			if (p < ce) {
+				const uint32_t r = csc[p].x & ROW_MASK;
+				uint64_t lo = row_ptr[r], hi = row_ptr[r + 1];
+				const uint64_t end = hi;
+				while (lo < hi) {   // first entry of the row past feature j
+					const uint64_t mid = (lo + hi) >> 1;
+					if (csr[mid].x <= j) lo = mid + 1;
+					else hi = mid;
+				}
+				if (lo < end) {
+					nxt = csr[lo].x;
+					ready = atomicSub(&indeg[nxt], 1u) == 1u;
+				}
+			}
+			if (ready) level[nxt] = (uint32_t)t + 2u;
+			wave_append(ready, nxt, tail, order);
+		}
+	}
+}
+
 __global__ void k_mark_dups(const uint64_t *row_ptr, const uint2 *csr, uint32_t n, uint8_t *dup)
 {
 	const uint32_t r = blockIdx.x * 256u + threadIdx.x;
@@ -1515,6 +1604,29 @@ hipError_t level_relax(const uint64_t *row_ptr, const uint2 *csr, uint32_t n, ui
 	(void)nf;
 	if (n == 0) return hipSuccess;
 	k_level_relax<<<grid_for(n), 256, 0, s>>>(row_ptr, csr, n, level, changed);
+	return hipGetLastError();
+}
+
+hipError_t kahn_init(const uint64_t *row_ptr, const uint2 *csr, uint32_t n, uint32_t nf, uint32_t *indeg,
+                     uint32_t *level, uint32_t *order, uint32_t *tail, uint32_t *bounds, hipStream_t s)
+{
+	if (nf == 0) return hipSuccess;
+	hipError_t err = hipMemsetAsync(indeg, 0, (size_t)nf * 4, s);
+	if (err == hipSuccess) err = hipMemsetAsync(tail, 0, 4, s);
+	if (err == hipSuccess) err = hipMemsetAsync(bounds, 0, 4, s);
+	if (err != hipSuccess) return err;
+	if (n) k_kahn_indeg<<<grid_for(n), 256, 0, s>>>(row_ptr, csr, n, indeg);
+	k_kahn_seed<<<grid_for(nf), 256, 0, s>>>(indeg, nf, level, order, tail);
+	k_kahn_close<<<1, 64, 0, s>>>(tail, bounds, 1);
+	return hipGetLastError();
+}
+
+hipError_t kahn_round(const uint64_t *col_ptr, const uint2 *csc, const uint64_t *row_ptr, const uint2 *csr,
+                      uint32_t *bounds, int t, uint32_t *indeg, uint32_t *level, uint32_t *order, uint32_t *tail,
+                      hipStream_t s)
+{
+	k_kahn_round<<<1024, 256, 0, s>>>(col_ptr, csc, row_ptr, csr, bounds, t, indeg, level, order, tail);
+	k_kahn_close<<<1, 64, 0, s>>>(tail, bounds, t + 2);
 	return hipGetLastError();
 }
 

@@ -522,8 +522,9 @@ class FMLearnVB:
         _check(lib().vbfm_free_energy(self._ctx, C.byref(F)), self._ctx)
         return F.value
 
-    def set_profiling(self, on=True):
-        _check(lib().vbfm_set_profiling(self._ctx, 1 if on else 0), self._ctx)
+    def set_profiling(self, on=True, stride=1):
+        """Event pairs around the sweep launches; stride > 1 times every stride-th launch of a kind."""
+        _check(lib().vbfm_set_profiling(self._ctx, max(1, int(stride)) if on else 0), self._ctx)
 
     def factor_sweep(self):
         ms = C.c_double()
