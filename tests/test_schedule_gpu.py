@@ -94,3 +94,29 @@ def test_sampled_launch_events(stride):
     a_full = full.ms_vlevel_kernels / full.n_vlevel_launches
     a = st.ms_vlevel_kernels / st.n_vlevel_launches
     assert 0.5 * a_full < a < 2.0 * a_full
+
+
+@pytest.mark.parametrize("shape", ["c3_fields", "multihot_bench"])
+def test_kahn_equals_relaxation_at_bench_size(shape, monkeypatch):
+    """At the bench sizes: C3's 1e7 rows x 40 fields (level = field + 1, 25k columns of ~400
+    entries per frontier) and the multi-hot bench's 1e7 rows x U(5,60) ids of 1e6 features
+    (785 levels): Kahn's order gives the relaxation's levels."""
+    got = {}
+    for mode in ("relax", "kahn"):
+        monkeypatch.setenv("VBFM_SCHEDULE", mode)
+        if shape == "c3_fields":
+            F, S = 40, 25_000
+            g = vbfm.FMLearnVB(1, 1, 2, F * S + 1)
+            g.synth(0, 10_000_000, F, S, 1000, 0)
+        else:
+            g = vbfm.FMLearnVB(1, 1, 2, 1_000_001)
+            g.synth_multihot(0, 10_000_000, 1_000_000, 5, 60, 1000, 0)
+        got[mode] = g.levels()
+        g.close()
+    np.testing.assert_array_equal(got["relax"][0], got["kahn"][0])
+    assert got["relax"][1] == got["kahn"][1]
+    if shape == "c3_fields":
+        assert got["kahn"][1] == 40
+        np.testing.assert_array_equal(got["kahn"][0][:40 * 25_000], np.arange(40 * 25_000) // 25_000 + 1)
+    else:
+        assert got["kahn"][1] == 785
