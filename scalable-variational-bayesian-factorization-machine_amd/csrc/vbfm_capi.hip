@@ -494,8 +494,12 @@ static void kahn_levels(vbfm_ctx *c, uint32_t *level)
 	if (nf == 0) return;
 	const int batch = 32;
 	const size_t nb = (size_t)nf + 2 * batch + 3;
-	uint32_t *indeg = dalloc<uint32_t>(nf), *order = dalloc<uint32_t>(nf), *tail = dalloc<uint32_t>(1);
-	uint32_t *bounds = dalloc<uint32_t>(nb);
+	struct Bufs {   // freed on every exit, the error ones included
+		uint32_t *indeg = nullptr, *order = nullptr, *tail = nullptr, *bounds = nullptr;
+		~Bufs() { dfree(indeg); dfree(order); dfree(tail); dfree(bounds); }
+	} b;
+	uint32_t *indeg = b.indeg = dalloc<uint32_t>(nf), *order = b.order = dalloc<uint32_t>(nf);
+	uint32_t *tail = b.tail = dalloc<uint32_t>(1), *bounds = b.bounds = dalloc<uint32_t>(nb);
 	HIPCHK(vbk::kahn_init(d.row_ptr, d.csr, d.n, nf, indeg, level, order, tail, bounds, c->s));
 	uint32_t prev = 0xFFFFFFFFu;
 	for (int t = 0;; t += batch) {
@@ -510,10 +514,6 @@ static void kahn_levels(vbfm_ctx *c, uint32_t *level)
 		if (tl == prev || tl > nf) throw std::string("level schedule did not converge (a feature cycle)");
 		prev = tl;
 	}
-	dfree(indeg);
-	dfree(order);
-	dfree(tail);
-	dfree(bounds);
 }
 
 // Dependency levels of the train features (see vbfm_kernels.hip header). With several

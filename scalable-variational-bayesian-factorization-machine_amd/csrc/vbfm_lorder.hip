@@ -206,6 +206,24 @@ DEVI void lord_stats(double2 *recs, const RowRec *src, const float *lx, uint32_t
 // (the q-cache restart), which the level-uniform `first` gives in the field store
 constexpr uint32_t ENT_FIRST = 0x80000000u;
 
+// one 16-B piece of a moved record. NT (the entry store): a non-temporal store -- a slot is read
+// by a later level of the row, rarely the next one, so the moved records are not kept in L2 and
+// the launch boundary has no dirty lines to write back (multi-hot bench: v sweep 799 -> 706 ms,
+// profiles/probes/ab_entry_nt_store.txt; the field store, whose next level reads every record,
+// gains nothing from it)
+template <bool NT>
+DEVI void put_piece(double2 *d, size_t idx, const double2 &v)
+{
+	if constexpr (NT) {
+		ntv2 w;
+		w.x = v.x;
+		w.y = v.y;
+		__builtin_nontemporal_store(w, reinterpret_cast<ntv2 *>(d) + idx);
+	} else {
+		d[idx] = v;
+	}
+}
+
 template <int BLOCK, uint32_t CAP, class Op, bool ENT = false>
 DEVI void lord_move(double2 *recs, uint32_t *dsts, const RowRec *src, const float *lx, const uint32_t *nxt, uint32_t n,
                     bool resident, RowRec *dst, bool first, const Op &op)
@@ -243,7 +261,7 @@ DEVI void lord_move(double2 *recs, uint32_t *dsts, const RowRec *src, const floa
 		__syncthreads();
 		for (uint32_t t = threadIdx.x; t < m * 4; t += BLOCK) {
 			const uint32_t i = t >> 2, c = t & 3;
-			d[(size_t)dsts[i] * 4 + c] = recs[lslot(i, c)];
+			put_piece<ENT>(d, (size_t)dsts[i] * 4 + c, recs[lslot(i, c)]);
 		}
 	}
 }
@@ -301,7 +319,7 @@ DEVI void res_move(double2 *recs, uint32_t *dsts, uint32_t n, const float (&xr)[
 	double2 *d = reinterpret_cast<double2 *>(dst);
 	for (uint32_t t = threadIdx.x; t < n * 4; t += BLOCK) {
 		const uint32_t i = t >> 2, c = t & 3;
-		d[(size_t)dsts[i] * 4 + c] = recs[lslot(i, c)];
+		put_piece<ENT>(d, (size_t)dsts[i] * 4 + c, recs[lslot(i, c)]);
 	}
 }
 

@@ -30,6 +30,7 @@
 #include <cmath>
 #include <cstring>
 #include <string>
+#include <thread>
 #include <vector>
 
 using namespace vbi;
@@ -575,9 +576,17 @@ __global__ __launch_bounds__(256) void k_ov_lord(LevelArgs a)
 		}
 	}
 	__syncthreads();
-	double2 *d = reinterpret_cast<double2 *>(a.dst);
-	for (uint32_t t = threadIdx.x; t < m * 4; t += 256)
-		d[(size_t)dsts[t >> 2] * 4 + (t & 3)] = stage[ov_slot(t >> 2, t & 3)];
+	// non-temporal stores: v sweep 1129 -> 1086 ms per C3 epoch (profiles/probes/ab_online_nt_store.txt;
+	// write-through stores were 8 % slower, ab_write_through.txt)
+	typedef double ntv2 __attribute__((ext_vector_type(2)));
+	ntv2 *d = reinterpret_cast<ntv2 *>(a.dst);
+	for (uint32_t t = threadIdx.x; t < m * 4; t += 256) {
+		const double2 v = stage[ov_slot(t >> 2, t & 3)];
+		ntv2 w;
+		w.x = v.x;
+		w.y = v.y;
+		__builtin_nontemporal_store(w, d + (size_t)dsts[t >> 2] * 4 + (t & 3));
+	}
 }
 
 inline unsigned grid_of(uint64_t n, unsigned block = 256) { return (unsigned)((n + block - 1) / block); }
@@ -656,6 +665,16 @@ struct OvState {
 	uint32_t size = 0;             // size_except_last = ceil(N / num_batch)
 	vbrng::Glibc stream;           // the reference's rand() after the initial draws
 	std::vector<uint32_t> shuffle; // kept across epochs (:58-62)
+	// the next epoch's shuffle, drawn on a host thread while the GPU sweeps this epoch's batches
+	// (the permutation depends on the rand() stream and the last permutation only)
+	std::vector<uint32_t> sh_next;
+	vbrng::Glibc stream_next;
+	std::thread pre;
+	void pre_join()
+	{
+		if (pre.joinable()) pre.join();
+	}
+	~OvState() { pre_join(); }
 	double2 *nat_w = nullptr, *nat_v = nullptr;   // natural_{mu,sigma}_{w,v}_dash; nat_v factor-major [f][j]
 	                                              // (the reference's layout): a level's columns are
 	                                              // consecutive ids, so their natural parameters are one
@@ -768,16 +787,39 @@ void *ov_tmp(OvState &o, size_t bytes)
 	return o.tmp;
 }
 
+// std::random_shuffle(sh, sh + N) (libstdc++: i from 1, j = rand() % (i + 1))
+void ov_shuffle(std::vector<uint32_t> &sh, vbrng::Glibc &stream)
+{
+	const uint32_t N = (uint32_t)sh.size();
+	for (uint32_t i = 1; i < N; i++) {
+		const uint32_t j = (uint32_t)(stream.next() % (int32_t)(i + 1));
+		if (j != i) std::swap(sh[i], sh[j]);
+	}
+}
+
+// the next epoch's permutation on a host thread; called once this epoch's has reached the device
+void ov_prefetch_shuffle(OvState &o)
+{
+	o.pre_join();
+	o.pre = std::thread([&o] {
+		o.sh_next = o.shuffle;
+		o.stream_next = o.stream;
+		ov_shuffle(o.sh_next, o.stream_next);
+	});
+}
+
 // steps 1-3 of the file header: the epoch's batches
 void ov_regroup(vbfm_ctx *c)
 {
 	OvState &o = *c->ov;
 	const uint32_t N = o.n_total, nf = c->tr.nf, nb = o.num_batch;
 	const uint64_t nnz = c->tr.nnz;
-	// std::random_shuffle(shuffle, shuffle + N) (libstdc++: i from 1, j = rand() % (i + 1))
-	for (uint32_t i = 1; i < N; i++) {
-		const uint32_t j = (uint32_t)(o.stream.next() % (int32_t)(i + 1));
-		if (j != i) std::swap(o.shuffle[i], o.shuffle[j]);
+	if (o.pre.joinable()) {   // drawn during the last epoch
+		o.pre_join();
+		std::swap(o.shuffle, o.sh_next);
+		o.stream = o.stream_next;
+	} else {
+		ov_shuffle(o.shuffle, o.stream);
 	}
 	HIPCHK(hipMemcpyAsync(o.sh_d, o.shuffle.data(), (size_t)N * 4, hipMemcpyHostToDevice, c->s));
 	k_ov_batch<<<grid_of(N), 256, 0, c->s>>>(o.sh_d, N, o.size, o.bat_d, o.iota_d);
@@ -1082,7 +1124,8 @@ int vbfm_online_epoch(vbfm_ctx *c, vbfm_online_stats *out)
 		std::vector<uint64_t> eoff((size_t)nb + 1);
 		for (uint32_t b = 0; b <= nb; b++)
 			HIPCHK(hipMemcpyAsync(&eoff[b], o.gptr + (size_t)b * nf, 8, hipMemcpyDeviceToHost, c->s));
-		sync(c);
+		sync(c);   // the permutation's copy to the device is done: draw the next one meanwhile
+		ov_prefetch_shuffle(o);
 		const DevData full = c->tr;
 		RowRec *const rows_full = c->rows;
 		const uint64_t n_global_full = c->n_global;
