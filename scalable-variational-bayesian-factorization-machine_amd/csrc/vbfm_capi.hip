@@ -781,7 +781,8 @@ void sweep_level(vbfm_ctx *c, uint32_t l, bool is_w, int f)
 			const bool carried = l == 0 && c->carry != 0 && !is_w;
 			a.pend_kind = carried ? (c->carry == 3 ? 2 : 1) : 0;
 			c->carry = 0;
-			a.pending = (l > 0 || carried) ? 1 : 0;   // the kernels stream the records non-temporally
+			a.pending = (l > 0 || carried) ? 1 : 0;
+			if (c->tr.n > 50000000u) a.pending |= 2;     // non-temporal record loads (large shards)
 			a.first_prev = l == 1;
 			HIPCHK(vbk::lord_defer_level(a, is_w, c->s));
 			if (c->row_comm())

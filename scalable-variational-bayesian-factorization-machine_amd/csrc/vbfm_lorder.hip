@@ -754,7 +754,11 @@ __global__ __launch_bounds__(BLOCK) void k_lord_defer(LevelArgs a)
 			q[u] = pay_load<PAY8>(a, sb + base + min(i, m - 1));
 		}
 		double2 sv[4 * R];
-		stage_load<BLOCK, R, true>(sv, s + (size_t)base * 4, m);   // records read once: non-temporal
+		// records read once: non-temporal loads on large shards (pending bit 1); on a shard the
+		// size of C4's on 8 GPUs (1.25e7 rows) plain loads are 1.5 % faster
+		// (profiles/probes/ab_defer_loads.txt)
+		if (a.pending & 2) stage_load<BLOCK, R, true>(sv, s + (size_t)base * 4, m);
+		else stage_load<BLOCK, R, false>(sv, s + (size_t)base * 4, m);
 		// unconditional (a.tab always holds a previous level's width; unused unless pending):
 		// a branch here lets the compiler sink half of each payload load after the records'
 #pragma unroll
