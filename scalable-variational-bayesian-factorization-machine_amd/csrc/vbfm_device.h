@@ -21,6 +21,23 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
+
+// The longest mean column of a level swept with the 64-thread x 2 workgroup shape (longer: 256 x
+// 1, 256 x 2, 512 x 2). Every level kernel -- fused, deferred split, column-gather, entry store,
+// MCMC -- takes its shape from the same thresholds: the same shape gives the same reduction tree,
+// so the layouts and the fused / split forms stay bit-identical to each other. 96: at 128 a level
+// of C4's per-rank shard on 8 GPUs (columns of ~100 entries) runs ~1 % faster in the deferred
+// split form but ~2 % slower fused (profiles/probes/ab_defer_small_shape.txt). VBFM_SMALL_MAX
+// overrides (A/B).
+inline uint32_t shape_small_max()
+{
+	static const uint32_t v = [] {
+		const char *e = getenv("VBFM_SMALL_MAX");
+		return e ? (uint32_t)atoi(e) : 96u;
+	}();
+	return v;
+}
 
 struct __attribute__((aligned(64))) RowRec {
 	double e;    // cache[i].e      residual y - yhat (fm_learn_vb_simultaneous.h:42-44)

@@ -1363,7 +1363,7 @@ namespace vbk {
 template <int P, bool NEXT>
 hipError_t launch_v_fused(const LevelArgs &a, hipStream_t s)
 {
-	if (a.avg_len <= 96) k_v_level_fused<64, 2, P, NEXT><<<a.nfeat, 64, 0, s>>>(a);
+	if (a.avg_len <= shape_small_max()) k_v_level_fused<64, 2, P, NEXT><<<a.nfeat, 64, 0, s>>>(a);
 	else if (a.avg_len <= 320) k_v_level_fused<256, 1, P, NEXT><<<a.nfeat, 256, 0, s>>>(a);
 	else if (a.avg_len <= 640) k_v_level_fused<256, 2, P, NEXT><<<a.nfeat, 256, 0, s>>>(a);
 	else k_v_level_fused<512, 2, P, NEXT><<<a.nfeat, 512, 0, s>>>(a);
@@ -1373,7 +1373,7 @@ hipError_t launch_v_fused(const LevelArgs &a, hipStream_t s)
 template <bool NEXT>
 hipError_t launch_w_fused(const LevelArgs &a, hipStream_t s)
 {
-	if (a.avg_len <= 96) k_w_level_fused<64, 2, NEXT><<<a.nfeat, 64, 0, s>>>(a);
+	if (a.avg_len <= shape_small_max()) k_w_level_fused<64, 2, NEXT><<<a.nfeat, 64, 0, s>>>(a);
 	else if (a.avg_len <= 320) k_w_level_fused<256, 1, NEXT><<<a.nfeat, 256, 0, s>>>(a);
 	else if (a.avg_len <= 640) k_w_level_fused<256, 2, NEXT><<<a.nfeat, 256, 0, s>>>(a);
 	else k_w_level_fused<512, 2, NEXT><<<a.nfeat, 512, 0, s>>>(a);

@@ -645,13 +645,13 @@ template <bool IS_W, int P, bool NEXT>
 void launch_lord(const LevelArgs &a, hipStream_t s)
 {
 	if (a.ent) {
-		if (a.avg_len <= 96) k_level_lord<64, 2, IS_W, P, NEXT, true><<<a.nfeat, 64, 0, s>>>(a);
+		if (a.avg_len <= shape_small_max()) k_level_lord<64, 2, IS_W, P, NEXT, true><<<a.nfeat, 64, 0, s>>>(a);
 		else if (a.avg_len <= 320) k_level_lord<256, 1, IS_W, P, NEXT, true><<<a.nfeat, 256, 0, s>>>(a);
 		else if (a.avg_len <= 640) k_level_lord<256, 2, IS_W, P, NEXT, true><<<a.nfeat, 256, 0, s>>>(a);
 		else k_level_lord<512, 2, IS_W, P, NEXT, true><<<a.nfeat, 512, 0, s>>>(a);
 		return;
 	}
-	if (a.avg_len <= 96) k_level_lord<64, 2, IS_W, P, NEXT, false><<<a.nfeat, 64, 0, s>>>(a);
+	if (a.avg_len <= shape_small_max()) k_level_lord<64, 2, IS_W, P, NEXT, false><<<a.nfeat, 64, 0, s>>>(a);
 	else if (a.avg_len <= 320) k_level_lord<256, 1, IS_W, P, NEXT, false><<<a.nfeat, 256, 0, s>>>(a);
 	else if (a.avg_len <= 640) k_level_lord<256, 2, IS_W, P, NEXT, false><<<a.nfeat, 256, 0, s>>>(a);
 	else k_level_lord<512, 2, IS_W, P, NEXT, false><<<a.nfeat, 512, 0, s>>>(a);
@@ -860,31 +860,18 @@ __global__ __launch_bounds__(256) void k_lord_prev_fill(const uint32_t *feats, c
 	}
 }
 
-// the longest mean column the deferred kernels run with the 64 x 2 shape: 96, the fused and
-// column kernels' threshold -- the same workgroup shape gives the same reduction tree, which
-// keeps the split sweeps bit-identical to the fused ones. (128 would make C4's per-rank level on
-// 8 GPUs 1.7 % faster, profiles/probes/ab_defer_small_shape.txt, at the price of that identity.)
-// VBFM_SMALL_MAX overrides (A/B only).
-inline uint32_t small_max()
-{
-	static const uint32_t v = [] {
-		const char *e = getenv("VBFM_SMALL_MAX");
-		return e ? (uint32_t)atoi(e) : 96u;
-	}();
-	return v;
-}
 
 template <bool IS_W, int P, bool NEXT, int PK>
 void launch_defer_pk(const LevelArgs &a, hipStream_t s)
 {
 	if (a.lpay2) {   // every x 1: 8-B payloads
-		if (a.avg_len <= small_max()) k_lord_defer<64, 2, IS_W, P, NEXT, PK, true><<<a.nfeat, 64, 0, s>>>(a);
+		if (a.avg_len <= shape_small_max()) k_lord_defer<64, 2, IS_W, P, NEXT, PK, true><<<a.nfeat, 64, 0, s>>>(a);
 		else if (a.avg_len <= 320) k_lord_defer<256, 1, IS_W, P, NEXT, PK, true><<<a.nfeat, 256, 0, s>>>(a);
 		else if (a.avg_len <= 640) k_lord_defer<256, 2, IS_W, P, NEXT, PK, true><<<a.nfeat, 256, 0, s>>>(a);
 		else k_lord_defer<512, 2, IS_W, P, NEXT, PK, true><<<a.nfeat, 512, 0, s>>>(a);
 		return;
 	}
-	if (a.avg_len <= small_max()) k_lord_defer<64, 2, IS_W, P, NEXT, PK, false><<<a.nfeat, 64, 0, s>>>(a);
+	if (a.avg_len <= shape_small_max()) k_lord_defer<64, 2, IS_W, P, NEXT, PK, false><<<a.nfeat, 64, 0, s>>>(a);
 	else if (a.avg_len <= 320) k_lord_defer<256, 1, IS_W, P, NEXT, PK, false><<<a.nfeat, 256, 0, s>>>(a);
 	else if (a.avg_len <= 640) k_lord_defer<256, 2, IS_W, P, NEXT, PK, false><<<a.nfeat, 256, 0, s>>>(a);
 	else k_lord_defer<512, 2, IS_W, P, NEXT, PK, false><<<a.nfeat, 512, 0, s>>>(a);
@@ -1037,13 +1024,13 @@ template <bool IS_W, int P, bool NEXT>
 void launch_mc_defer(const McArgs &a, hipStream_t s)
 {
 	if (a.lpay2) {   // every x 1: 8-B payloads
-		if (a.avg_len <= small_max()) k_mc_lord_defer<64, 2, IS_W, P, NEXT, true><<<a.nfeat, 64, 0, s>>>(a);
+		if (a.avg_len <= shape_small_max()) k_mc_lord_defer<64, 2, IS_W, P, NEXT, true><<<a.nfeat, 64, 0, s>>>(a);
 		else if (a.avg_len <= 320) k_mc_lord_defer<256, 1, IS_W, P, NEXT, true><<<a.nfeat, 256, 0, s>>>(a);
 		else if (a.avg_len <= 640) k_mc_lord_defer<256, 2, IS_W, P, NEXT, true><<<a.nfeat, 256, 0, s>>>(a);
 		else k_mc_lord_defer<512, 2, IS_W, P, NEXT, true><<<a.nfeat, 512, 0, s>>>(a);
 		return;
 	}
-	if (a.avg_len <= small_max()) k_mc_lord_defer<64, 2, IS_W, P, NEXT, false><<<a.nfeat, 64, 0, s>>>(a);
+	if (a.avg_len <= shape_small_max()) k_mc_lord_defer<64, 2, IS_W, P, NEXT, false><<<a.nfeat, 64, 0, s>>>(a);
 	else if (a.avg_len <= 320) k_mc_lord_defer<256, 1, IS_W, P, NEXT, false><<<a.nfeat, 256, 0, s>>>(a);
 	else if (a.avg_len <= 640) k_mc_lord_defer<256, 2, IS_W, P, NEXT, false><<<a.nfeat, 256, 0, s>>>(a);
 	else k_mc_lord_defer<512, 2, IS_W, P, NEXT, false><<<a.nfeat, 512, 0, s>>>(a);
@@ -1080,7 +1067,7 @@ void launch_mc_lord_shape(const McArgs &a, int is_w, hipStream_t s)
 {
 	// the column-gather MCMC kernel's BLOCK (vbfm_mcmc.hip launch_level), records per thread
 	// as the VB level kernel
-	if (a.avg_len <= 96) launch_mc_lord<64, 2, MODE>(a, is_w, s);
+	if (a.avg_len <= shape_small_max()) launch_mc_lord<64, 2, MODE>(a, is_w, s);
 	else if (a.avg_len <= 320) launch_mc_lord<256, 1, MODE>(a, is_w, s);
 	else if (a.avg_len <= 640) launch_mc_lord<256, 2, MODE>(a, is_w, s);
 	else launch_mc_lord<512, 2, MODE>(a, is_w, s);
