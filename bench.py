@@ -115,6 +115,17 @@ def shard_plan(rows, world, rank, mode):
     return {"rows": hi - lo, "row_offset": lo, "rows_total": rows}
 
 
+def launch_event_stride(levels, k, limit=8000):
+    """Time every stride-th level launch: 1 up to `limit` launches per iteration, else the
+    smallest stride >= 16 coprime with the level count (every level sampled alike)."""
+    if levels * k <= limit:
+        return 1
+    stride = 16
+    while math.gcd(stride, levels) != 1:
+        stride += 1
+    return stride
+
+
 def spawn_ranks(n):
     """Start n rank processes of this script (one per GPU) and wait for them. This process
     never touches a GPU; each child gets the torchrun environment."""
@@ -271,13 +282,7 @@ def main():
         # short level launches (many levels): an event pair costs up to ~4.5 us of device time
         # on some boxes, so time a sample -- every stride-th launch, stride coprime with the
         # level count so that every level is sampled alike
-        n_lev = fml.levels()[1]
-        stride = 1
-        if n_lev * k > 8000:
-            stride = 16
-            while math.gcd(stride, n_lev) != 1:
-                stride += 1
-        fml.set_profiling(True, stride)
+        fml.set_profiling(True, launch_event_stride(fml.levels()[1], k))
     layout = fml.layout()
     nnz = fml.shape(0)[2]                # this rank's train entries
     log("rank %d: setup %.1f s (N=%d F=%d S=%d features=%d nnz=%d k=%d, %s layout)" % (
