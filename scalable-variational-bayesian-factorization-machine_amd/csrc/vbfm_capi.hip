@@ -688,6 +688,10 @@ LevelArgs level_args(vbfm_ctx *c, uint32_t l, bool is_w, int f)
 	a.ms_stride_next = (uint32_t)c->k;
 	a.hyp = is_w ? c->hyp_w_d : c->hyp_v_d + f;
 	a.hyp_stride = is_w ? 1 : (uint32_t)c->k;
+	// one attribute group: the level kernels take the prior by value (hyp_w / hyp_v on the host
+	// are the values last pushed to hyp_w_d / hyp_v_d)
+	a.hyp_uniform = c->G == 1;
+	a.hyp0 = c->G == 1 ? (is_w ? c->hyp_w[0] : c->hyp_v[f]) : 0.0;
 	a.attr_group = c->group_d;
 	a.dup = c->dup;
 	a.alpha = c->alpha;

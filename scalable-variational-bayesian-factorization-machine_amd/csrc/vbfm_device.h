@@ -144,6 +144,8 @@ struct McArgs {
 	const double *lambda;      // prior precision of (group g): lambda[g*hstride]
 	const double *mu;          // prior mean of (group g): mu[g*hstride]
 	uint32_t hstride;
+	int hyp_uniform;           // one attribute group: the prior is {lambda0, mu0} by value
+	double lambda0, mu0;
 	const uint32_t *attr_group;
 	const uint8_t *dup;
 	double alpha;

@@ -82,7 +82,7 @@ __global__ __launch_bounds__(BLOCK) void k_v_level_fused(LevelArgs a)
 	block_sum2<BLOCK>(vm, vs, lds);
 
 	double mu, sig;
-	const double sv_g = a.hyp[(size_t)a.attr_group[j] * a.hyp_stride];
+	const double sv_g = (a.hyp_uniform ? a.hyp0 : a.hyp[(size_t)a.attr_group[j] * a.hyp_stride]);
 	const bool go = v_post(vm, vs, sv_g, a.alpha, mo, so, mu, sig, a.counters, threadIdx.x == 0);
 	if (threadIdx.x == 0) a.ms[(size_t)j * a.ms_stride] = make_double2(mu, sig);
 	if (!go && !NEXT) return;
@@ -149,7 +149,7 @@ __global__ __launch_bounds__(256) void k_col_long_correct(LevelArgs a)
 	const double2 msj = a.seg_part[2 * g.seg0 + 1];
 	const double mo = msj.x, so = msj.y;
 	const double2 nx = NEXT ? a.ms_next[(size_t)j * a.ms_stride_next] : make_double2(0.0, 0.0);
-	const double hyp = a.hyp[(size_t)a.attr_group[j] * a.hyp_stride];
+	const double hyp = (a.hyp_uniform ? a.hyp0 : a.hyp[(size_t)a.attr_group[j] * a.hyp_stride]);
 	const bool lead = threadIdx.x == 0 && blockIdx.x == g.seg0;
 	double mu, sig;
 	const bool go = IS_W ? w_post(s1, s2, hyp, a.alpha, mo, so, mu, sig, a.counters, lead)
@@ -199,7 +199,7 @@ __global__ __launch_bounds__(BLOCK) void k_v_level_correct(LevelArgs a)
 	double2 nx = make_double2(0.0, 0.0);
 	if constexpr (NEXT) nx = a.ms_next[(size_t)j * a.ms_stride_next];
 	double mu, sig;
-	const double sv_g = a.hyp[(size_t)a.attr_group[j] * a.hyp_stride];
+	const double sv_g = (a.hyp_uniform ? a.hyp0 : a.hyp[(size_t)a.attr_group[j] * a.hyp_stride]);
 	const bool go = v_post(st.x, st.y, sv_g, a.alpha, msj.x, msj.y, mu, sig, a.counters, threadIdx.x == 0);
 	if (threadIdx.x == 0) a.ms[(size_t)j * a.ms_stride] = make_double2(mu, sig);
 	if (!go && !NEXT) return;
@@ -270,7 +270,7 @@ __global__ __launch_bounds__(BLOCK) void k_w_level_fused(LevelArgs a)
 	}
 	block_sum2<BLOCK>(wm, ws, lds);
 	double mu, sig;
-	const double sw_g = a.hyp[(size_t)a.attr_group[j] * a.hyp_stride];
+	const double sw_g = (a.hyp_uniform ? a.hyp0 : a.hyp[(size_t)a.attr_group[j] * a.hyp_stride]);
 	const bool go = w_post(wm, ws, sw_g, a.alpha, mo, so, mu, sig, a.counters, threadIdx.x == 0);
 	if (threadIdx.x == 0) a.ms[(size_t)j * a.ms_stride] = make_double2(mu, sig);
 	if (!go && !NEXT) return;
@@ -324,7 +324,7 @@ __global__ __launch_bounds__(BLOCK) void k_w_level_correct(LevelArgs a)
 	double2 nx = make_double2(0.0, 0.0);
 	if constexpr (NEXT) nx = a.ms_next[(size_t)j * a.ms_stride_next];
 	double mu, sig;
-	const double sw_g = a.hyp[(size_t)a.attr_group[j] * a.hyp_stride];
+	const double sw_g = (a.hyp_uniform ? a.hyp0 : a.hyp[(size_t)a.attr_group[j] * a.hyp_stride]);
 	const bool go = w_post(st.x, st.y, sw_g, a.alpha, msj.x, msj.y, mu, sig, a.counters, threadIdx.x == 0);
 	if (threadIdx.x == 0) a.ms[(size_t)j * a.ms_stride] = make_double2(mu, sig);
 	if (!go && !NEXT) return;

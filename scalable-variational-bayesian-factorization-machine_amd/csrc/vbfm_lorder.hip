@@ -346,7 +346,8 @@ __global__ __launch_bounds__(BLOCK) void k_level_lord(LevelArgs a)
 	op.nx = NEXT ? a.ms_next[(size_t)j * a.ms_stride_next] : make_double2(0.0, 0.0);
 
 	double s1 = 0.0, s2 = 0.0;
-	const double hyp = a.hyp[(size_t)a.attr_group[j] * a.hyp_stride];
+	// one attribute group: the prior by value (no attr_group -> hyp load chain)
+	const double hyp = a.hyp_uniform ? a.hyp0 : a.hyp[(size_t)a.attr_group[j] * a.hyp_stride];
 	if (n <= CAP) {   // the run stays in LDS from the statistics to the move
 		float xr[R];
 		uint32_t nr[R];
@@ -415,7 +416,7 @@ __global__ __launch_bounds__(LONG_BLOCK) void k_lord_long_move(LevelArgs a)
 	VbOp<IS_W, P, NEXT> op;
 	op.mo = msj.x; op.so = msj.y;
 	op.nx = NEXT ? a.ms_next[(size_t)j * a.ms_stride_next] : make_double2(0.0, 0.0);
-	const double hyp = a.hyp[(size_t)a.attr_group[j] * a.hyp_stride];
+	const double hyp = (a.hyp_uniform ? a.hyp0 : a.hyp[(size_t)a.attr_group[j] * a.hyp_stride]);
 	const bool lead = threadIdx.x == 0 && blockIdx.x == g.seg0;
 	op.go = vb_post<IS_W>(s1, s2, hyp, a.alpha, op.mo, op.so, op.mu, op.sig, a.counters, lead);
 	if (lead) a.ms[(size_t)j * a.ms_stride] = make_double2(op.mu, op.sig);
@@ -456,7 +457,7 @@ __global__ __launch_bounds__(BLOCK) void k_level_lord_move(LevelArgs a)
 	VbOp<IS_W, P, NEXT> op;
 	op.mo = msj.x; op.so = msj.y;
 	op.nx = NEXT ? a.ms_next[(size_t)j * a.ms_stride_next] : make_double2(0.0, 0.0);
-	const double hyp = a.hyp[(size_t)a.attr_group[j] * a.hyp_stride];
+	const double hyp = (a.hyp_uniform ? a.hyp0 : a.hyp[(size_t)a.attr_group[j] * a.hyp_stride]);
 	op.go = vb_post<IS_W>(st.x, st.y, hyp, a.alpha, op.mo, op.so, op.mu, op.sig, a.counters, threadIdx.x == 0);
 	if (threadIdx.x == 0) a.ms[(size_t)j * a.ms_stride] = make_double2(op.mu, op.sig);
 	lord_move<BLOCK, CAP>(recs, dsts, a.src + (sb - a.lbase), a.lx ? a.lx + sb : nullptr, a.lnext + sb, n, false, a.dst,
@@ -494,8 +495,8 @@ __global__ __launch_bounds__(BLOCK) void k_mc_level_lord(McArgs a)
 			__syncthreads();
 			res_stats<BLOCK, R>(recs, n, xr, op, sm, ss);
 			block_sum2<BLOCK>(sm, ss, lds);
-			const uint32_t g = a.attr_group[j];
-			op.go = mc_draw(sm, ss, op.vo, a.lambda[(size_t)g * a.hstride], a.mu[(size_t)g * a.hstride], a.alpha,
+			const uint32_t g = mc_group(a, j);
+			op.go = mc_draw(sm, ss, op.vo, mc_lambda(a, g), mc_mu(a, g), a.alpha,
 			                mc_z(a, j), a.z != nullptr, a.sample, !IS_W, op.v, a.counters, threadIdx.x == 0);
 			if (threadIdx.x == 0) a.par[(size_t)j * a.stride].x = op.v;
 			res_move<BLOCK, R, McOp<IS_W, P, NEXT>, ENT>(recs, dsts, n, xr, nr, a.dst, a.first_level != 0, op);
@@ -515,8 +516,8 @@ __global__ __launch_bounds__(BLOCK) void k_mc_level_lord(McArgs a)
 		ss = st.y;
 	}
 	if constexpr (MODE != 1) {
-		const uint32_t g = a.attr_group[j];
-		op.go = mc_draw(sm, ss, op.vo, a.lambda[(size_t)g * a.hstride], a.mu[(size_t)g * a.hstride], a.alpha,
+		const uint32_t g = mc_group(a, j);
+		op.go = mc_draw(sm, ss, op.vo, mc_lambda(a, g), mc_mu(a, g), a.alpha,
 		                mc_z(a, j), a.z != nullptr, a.sample, !IS_W, op.v, a.counters, threadIdx.x == 0);
 		if (threadIdx.x == 0) a.par[(size_t)j * a.stride].x = op.v;
 		lord_move<BLOCK, CAP, McOp<IS_W, P, NEXT>, ENT>(recs, dsts, src, lx, a.lnext + sb, n, false, a.dst,
@@ -802,7 +803,7 @@ __global__ __launch_bounds__(256) void k_lord_defer_post(LevelArgs a)
 	const uint32_t j = a.feats[i];
 	const double2 msj = a.ms[(size_t)j * a.ms_stride];
 	const double2 st = a.stats[i];
-	const double hyp = a.hyp[(size_t)a.attr_group[j] * a.hyp_stride];
+	const double hyp = a.hyp_uniform ? a.hyp0 : a.hyp[(size_t)a.attr_group[j] * a.hyp_stride];
 	double mu, sig;
 	const bool go = vb_post<IS_W>(st.x, st.y, hyp, a.alpha, msj.x, msj.y, mu, sig, a.counters, true);
 	a.ms[(size_t)j * a.ms_stride] = make_double2(mu, sig);
@@ -989,9 +990,9 @@ __global__ __launch_bounds__(256) void k_mc_lord_defer_post(McArgs a)
 	const uint32_t j = a.feats[i];
 	const double vo = a.par[(size_t)j * a.stride].x;
 	const double2 st = a.stats[i];
-	const uint32_t g = a.attr_group[j];
+	const uint32_t g = mc_group(a, j);
 	double v = vo;
-	const bool go = mc_draw(st.x, st.y, vo, a.lambda[(size_t)g * a.hstride], a.mu[(size_t)g * a.hstride], a.alpha,
+	const bool go = mc_draw(st.x, st.y, vo, mc_lambda(a, g), mc_mu(a, g), a.alpha,
 	                        mc_z(a, j), a.z != nullptr, a.sample, !IS_W, v, a.counters, true);
 	a.par[(size_t)j * a.stride].x = v;
 	PostT t;

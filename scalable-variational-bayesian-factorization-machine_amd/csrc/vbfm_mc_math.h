@@ -29,6 +29,11 @@ DEVI double device_normal(uint64_t seed, uint64_t stream, uint64_t j)
 	return sqrt(-2.0 * log(u1)) * cos(6.283185307179586 * u2);
 }
 
+// the feature's prior (group of attribute j); by value when there is one group
+DEVI uint32_t mc_group(const McArgs &a, uint32_t j) { return a.hyp_uniform ? 0u : a.attr_group[j]; }
+DEVI double mc_lambda(const McArgs &a, uint32_t g) { return a.hyp_uniform ? a.lambda0 : a.lambda[(size_t)g * a.hstride]; }
+DEVI double mc_mu(const McArgs &a, uint32_t g) { return a.hyp_uniform ? a.mu0 : a.mu[(size_t)g * a.hstride]; }
+
 DEVI double mc_z(const McArgs &a, uint32_t j)
 {
 	if (!a.sample) return 0.0;

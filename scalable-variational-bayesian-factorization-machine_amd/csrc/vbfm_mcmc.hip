@@ -99,9 +99,9 @@ __global__ __launch_bounds__(BLOCK) void k_mc_v_level(McArgs a)
 	}
 	const double vn = NEXT ? a.par_next[(size_t)j * a.next_stride].x : 0.0;
 	const double vp = a.pk ? a.par_prev[(size_t)j * a.next_stride].x : 0.0;   // fused re-prediction
-	const uint32_t g = a.attr_group[j];
+	const uint32_t g = mc_group(a, j);
 	double v;
-	const bool go = mc_draw(sm, ss, vo, a.lambda[(size_t)g * a.hstride], a.mu[(size_t)g * a.hstride], a.alpha,
+	const bool go = mc_draw(sm, ss, vo, mc_lambda(a, g), mc_mu(a, g), a.alpha,
 	                        mc_z(a, j), a.z != nullptr, a.sample, true, v, a.counters, threadIdx.x == 0);
 	if (threadIdx.x == 0) a.par[(size_t)j * a.stride].x = v;
 	if (!go && !NEXT && !a.pk) return;
@@ -155,9 +155,9 @@ __global__ __launch_bounds__(BLOCK) void k_mc_w_level(McArgs a)
 		ss = st.y;
 	}
 	const double vn = NEXT ? a.par_next[(size_t)j * a.next_stride].x : 0.0;
-	const uint32_t g = a.attr_group[j];
+	const uint32_t g = mc_group(a, j);
 	double w;
-	const bool go = mc_draw(sm, ss, wo, a.lambda[(size_t)g * a.hstride], a.mu[(size_t)g * a.hstride], a.alpha,
+	const bool go = mc_draw(sm, ss, wo, mc_lambda(a, g), mc_mu(a, g), a.alpha,
 	                        mc_z(a, j), a.z != nullptr, a.sample, false, w, a.counters, threadIdx.x == 0);
 	if (threadIdx.x == 0) a.par[(size_t)j * a.stride].x = w;
 	if (!go && !NEXT) return;
@@ -188,10 +188,10 @@ __global__ void k_mc_prior(McArgs a, uint32_t j0, uint32_t j1, int is_v)
 {
 	const uint32_t j = j0 + blockIdx.x * 256u + threadIdx.x;
 	if (j >= j1) return;
-	const uint32_t g = a.attr_group[j];
+	const uint32_t g = mc_group(a, j);
 	const double cur = a.par[(size_t)j * a.stride].x;
 	double out;
-	mc_draw(0.0, 0.0, cur, a.lambda[(size_t)g * a.hstride], a.mu[(size_t)g * a.hstride], a.alpha, mc_z(a, j),
+	mc_draw(0.0, 0.0, cur, mc_lambda(a, g), mc_mu(a, g), a.alpha, mc_z(a, j),
 	        a.z != nullptr, a.sample, is_v != 0, out, a.counters, true);
 	a.par[(size_t)j * a.stride].x = out;
 }

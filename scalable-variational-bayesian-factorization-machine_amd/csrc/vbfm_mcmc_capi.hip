@@ -276,6 +276,12 @@ McArgs mc_args(vbfm_ctx *c, uint32_t l, bool is_w, int f)
 	a.lambda = is_w ? d_w_lambda(c) : d_v_lambda(c) + f;
 	a.mu = is_w ? d_w_mu(c) : d_v_mu(c) + f;
 	a.hstride = is_w ? 1 : (uint32_t)c->k;
+	// one attribute group: the prior by value (the host copies are what was pushed to hyp_d)
+	a.hyp_uniform = c->G == 1;
+	if (c->G == 1) {
+		a.lambda0 = is_w ? m.w_lambda[0] : m.v_lambda[f];
+		a.mu0 = is_w ? m.w_mu[0] : m.v_mu[f];
+	}
 	a.attr_group = c->group_d;
 	a.dup = c->dup;
 	a.alpha = m.alpha;
