@@ -426,6 +426,7 @@ void sweep_level_shard(vbfm_ctx *c, uint32_t l, bool is_w, int f, int s)
 	const uint32_t lo = c->fs_lo[l * P1 + s], hi = c->fs_lo[l * P1 + s + 1];
 	a.feats = c->level_feats + lo;
 	a.nfeat = hi - lo;
+	a.feat_base += lo - c->level_ptr[l];   // (used only when the level is consecutive ids)
 	a.first_mask = 0;
 	if (a.nfeat == 0) return;
 	const size_t p = prof_begin(c, is_w ? 1 : 0);
@@ -574,6 +575,11 @@ void build_schedule(vbfm_ctx *c)
 	std::vector<uint64_t> cp((size_t)nf + 1, 0);
 	HIPCHK(hipMemcpy(cp.data(), d.col_ptr, ((size_t)nf + 1) * 8, hipMemcpyDeviceToHost));
 	c->level_avg.assign(L, 0);
+	c->level_base.assign(L, ~0u);
+	for (uint32_t l = 0; l < L; l++) {
+		const uint32_t lo = c->level_ptr[l], hi = c->level_ptr[l + 1];   // ascending, distinct ids
+		if (hi > lo && feats[hi - 1] - feats[lo] == hi - lo - 1) c->level_base[l] = feats[lo];
+	}
 	for (uint32_t l = 0; l < L; l++) {
 		uint64_t z = 0;
 		for (uint32_t i = c->level_ptr[l]; i < c->level_ptr[l + 1]; i++) z += cp[feats[i] + 1] - cp[feats[i]];
@@ -681,6 +687,8 @@ LevelArgs level_args(vbfm_ctx *c, uint32_t l, bool is_w, int f)
 	a.col_ptr = c->tr.col_ptr;
 	a.csc = c->tr.csc;
 	a.feats = c->level_feats + c->level_ptr[l];
+	a.feat_contig = l < c->level_base.size() && c->level_base[l] != ~0u;
+	a.feat_base = a.feat_contig ? c->level_base[l] : 0u;
 	a.nfeat = c->level_ptr[l + 1] - c->level_ptr[l];
 	a.rows = c->rows;
 	a.ms = is_w ? c->ms_w : c->ms_v + f;

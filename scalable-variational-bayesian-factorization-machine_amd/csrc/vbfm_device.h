@@ -76,6 +76,8 @@ struct LevelArgs {
 	const uint2 *csc;
 	const uint32_t *feats;     // features of this level (ascending id)
 	uint32_t nfeat;
+	int feat_contig;           // the level's features are consecutive ids: feature i = feat_base + i
+	uint32_t feat_base;        // (no feats[] load on the workgroup's path; field-structured data)
 	RowRec *rows;
 	double2 *ms;               // ms_v + f (stride k), or ms_w (stride 1)
 	uint32_t ms_stride;
@@ -136,6 +138,8 @@ struct McArgs {
 	const uint2 *csc;
 	const uint32_t *feats;
 	uint32_t nfeat;
+	int feat_contig;           // as LevelArgs
+	uint32_t feat_base;
 	RowRec *rows;
 	double2 *par;              // v_f (at f, stride k) or w (stride 1)
 	uint32_t stride;
@@ -369,3 +373,9 @@ hipError_t mc_param_sums(const double2 *pw, const double2 *pv, const uint32_t *p
                          uint32_t nchunks, int mode, const double *cw, const double *cv, int k, double *out,
                          hipStream_t s);
 }  // namespace vbk
+
+// feature id of the i-th feature of a level
+template <class A> __device__ __forceinline__ uint32_t level_feat(const A &a, uint32_t i)
+{
+	return a.feat_contig ? a.feat_base + i : a.feats[i];
+}

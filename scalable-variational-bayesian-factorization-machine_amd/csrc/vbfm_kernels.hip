@@ -44,7 +44,7 @@ template <int BLOCK, int R, int P, bool NEXT>
 __global__ __launch_bounds__(BLOCK) void k_v_level_fused(LevelArgs a)
 {
 	__shared__ double lds[2 * (BLOCK / 64)];
-	const uint32_t j = a.feats[blockIdx.x];
+	const uint32_t j = level_feat(a, blockIdx.x);
 	const uint64_t cb = a.col_ptr[j];
 	const uint32_t n = (uint32_t)(a.col_ptr[j + 1] - cb);
 	if (a.long_min && n > a.long_min && !a.dup[j]) return;   // segment kernels (col_long)
@@ -116,7 +116,7 @@ __global__ __launch_bounds__(256) void k_col_long_stats(LevelArgs a)
 {
 	__shared__ double lds[2 * (256 / 64)];
 	const LongSeg g = a.segs[blockIdx.x];
-	const uint32_t j = a.feats[g.col];
+	const uint32_t j = level_feat(a, g.col);
 	const uint2 *col = a.csc + a.col_ptr[j] + g.start;
 	const double2 msj = a.ms[(size_t)j * a.ms_stride];
 	double s1 = 0.0, s2 = 0.0;
@@ -138,7 +138,7 @@ template <bool IS_W, int P, bool NEXT>
 __global__ __launch_bounds__(256) void k_col_long_correct(LevelArgs a)
 {
 	const LongSeg g = a.segs[blockIdx.x];
-	const uint32_t j = a.feats[g.col];
+	const uint32_t j = level_feat(a, g.col);
 	const uint2 *col = a.csc + a.col_ptr[j] + g.start;
 	double s1 = 0.0, s2 = 0.0;
 	for (uint32_t q = 0; q < g.nseg; ++q) {
@@ -171,7 +171,7 @@ template <int BLOCK, int P>
 __global__ __launch_bounds__(BLOCK) void k_v_level_stats(LevelArgs a)
 {
 	__shared__ double lds[2 * (BLOCK / 64)];
-	const uint32_t j = a.feats[blockIdx.x];
+	const uint32_t j = level_feat(a, blockIdx.x);
 	const uint64_t cb = a.col_ptr[j];
 	const uint32_t n = (uint32_t)(a.col_ptr[j + 1] - cb);
 	const uint2 *col = a.csc + cb;
@@ -190,7 +190,7 @@ __global__ __launch_bounds__(BLOCK) void k_v_level_stats(LevelArgs a)
 template <int BLOCK, int P, bool NEXT>
 __global__ __launch_bounds__(BLOCK) void k_v_level_correct(LevelArgs a)
 {
-	const uint32_t j = a.feats[blockIdx.x];
+	const uint32_t j = level_feat(a, blockIdx.x);
 	const uint64_t cb = a.col_ptr[j];
 	const uint32_t n = (uint32_t)(a.col_ptr[j + 1] - cb);
 	const uint2 *col = a.csc + cb;
@@ -236,7 +236,7 @@ template <int BLOCK, int R, bool NEXT>
 __global__ __launch_bounds__(BLOCK) void k_w_level_fused(LevelArgs a)
 {
 	__shared__ double lds[2 * (BLOCK / 64)];
-	const uint32_t j = a.feats[blockIdx.x];
+	const uint32_t j = level_feat(a, blockIdx.x);
 	const uint64_t cb = a.col_ptr[j];
 	const uint32_t n = (uint32_t)(a.col_ptr[j + 1] - cb);
 	if (a.long_min && n > a.long_min && !a.dup[j]) return;   // segment kernels (col_long)
@@ -298,7 +298,7 @@ template <int BLOCK>
 __global__ __launch_bounds__(BLOCK) void k_w_level_stats(LevelArgs a)
 {
 	__shared__ double lds[2 * (BLOCK / 64)];
-	const uint32_t j = a.feats[blockIdx.x];
+	const uint32_t j = level_feat(a, blockIdx.x);
 	const uint64_t cb = a.col_ptr[j];
 	const uint32_t n = (uint32_t)(a.col_ptr[j + 1] - cb);
 	const uint2 *col = a.csc + cb;
@@ -315,7 +315,7 @@ __global__ __launch_bounds__(BLOCK) void k_w_level_stats(LevelArgs a)
 template <int BLOCK, bool NEXT>
 __global__ __launch_bounds__(BLOCK) void k_w_level_correct(LevelArgs a)
 {
-	const uint32_t j = a.feats[blockIdx.x];
+	const uint32_t j = level_feat(a, blockIdx.x);
 	const uint64_t cb = a.col_ptr[j];
 	const uint32_t n = (uint32_t)(a.col_ptr[j + 1] - cb);
 	const uint2 *col = a.csc + cb;

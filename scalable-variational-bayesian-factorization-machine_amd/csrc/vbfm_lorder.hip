@@ -334,7 +334,7 @@ __global__ __launch_bounds__(BLOCK) void k_level_lord(LevelArgs a)
 	__shared__ double2 recs[CAP * 4];
 	__shared__ uint32_t dsts[CAP];
 	__shared__ double lds[2 * (BLOCK / 64)];
-	const uint32_t j = a.feats[blockIdx.x];
+	const uint32_t j = level_feat(a, blockIdx.x);
 	const uint64_t sb = a.lcp[blockIdx.x];
 	const uint32_t n = (uint32_t)(a.lcp[blockIdx.x + 1] - sb);
 	if (a.long_min && n > a.long_min) return;      // a long column: the segment kernels' (lord_long)
@@ -384,7 +384,7 @@ __global__ __launch_bounds__(LONG_BLOCK) void k_lord_long_stats(LevelArgs a)
 	__shared__ double2 recs[LONG_CAP * 4];
 	__shared__ double lds[2 * (LONG_BLOCK / 64)];
 	const LongSeg g = a.segs[blockIdx.x];
-	const uint32_t j = a.feats[g.col];
+	const uint32_t j = level_feat(a, g.col);
 	const uint64_t sb = a.lcp[g.col] + g.start;
 	const double2 msj = a.ms[(size_t)j * a.ms_stride];
 	VbOp<IS_W, P, false> op;
@@ -404,7 +404,7 @@ __global__ __launch_bounds__(LONG_BLOCK) void k_lord_long_move(LevelArgs a)
 	__shared__ double2 recs[LONG_CAP * 4];
 	__shared__ uint32_t dsts[LONG_CAP];
 	const LongSeg g = a.segs[blockIdx.x];
-	const uint32_t j = a.feats[g.col];
+	const uint32_t j = level_feat(a, g.col);
 	const uint64_t sb = a.lcp[g.col] + g.start;
 	double s1 = 0.0, s2 = 0.0;
 	for (uint32_t q = 0; q < g.nseg; ++q) {
@@ -431,7 +431,7 @@ __global__ __launch_bounds__(BLOCK) void k_level_lord_stats(LevelArgs a)
 	constexpr uint32_t CAP = BLOCK * 2;
 	__shared__ double2 recs[CAP * 4];
 	__shared__ double lds[2 * (BLOCK / 64)];
-	const uint32_t j = a.feats[blockIdx.x];
+	const uint32_t j = level_feat(a, blockIdx.x);
 	const uint64_t sb = a.lcp[blockIdx.x];
 	const uint32_t n = (uint32_t)(a.lcp[blockIdx.x + 1] - sb);
 	const double2 msj = a.ms[(size_t)j * a.ms_stride];
@@ -449,7 +449,7 @@ __global__ __launch_bounds__(BLOCK) void k_level_lord_move(LevelArgs a)
 	constexpr uint32_t CAP = BLOCK * 2;
 	__shared__ double2 recs[CAP * 4];
 	__shared__ uint32_t dsts[CAP];
-	const uint32_t j = a.feats[blockIdx.x];
+	const uint32_t j = level_feat(a, blockIdx.x);
 	const uint64_t sb = a.lcp[blockIdx.x];
 	const uint32_t n = (uint32_t)(a.lcp[blockIdx.x + 1] - sb);
 	const double2 msj = a.ms[(size_t)j * a.ms_stride];
@@ -475,7 +475,7 @@ __global__ __launch_bounds__(BLOCK) void k_mc_level_lord(McArgs a)
 	__shared__ double2 recs[CAP * 4];
 	__shared__ uint32_t dsts[MODE == 1 ? 1 : CAP];
 	__shared__ double lds[2 * (BLOCK / 64)];
-	const uint32_t j = a.feats[blockIdx.x];
+	const uint32_t j = level_feat(a, blockIdx.x);
 	const uint64_t sb = a.lcp[blockIdx.x];
 	const uint32_t n = (uint32_t)(a.lcp[blockIdx.x + 1] - sb);
 	const RowRec *src = a.src + (sb - a.lbase);
@@ -726,7 +726,7 @@ __global__ __launch_bounds__(BLOCK) void k_lord_defer(LevelArgs a)
 	__shared__ double2 recs[CAP * 4];
 	__shared__ uint32_t dsts[CAP];
 	__shared__ double lds[2 * (BLOCK / 64)];
-	const uint32_t j = a.feats[blockIdx.x];
+	const uint32_t j = level_feat(a, blockIdx.x);
 	const uint64_t sb = a.lcp[blockIdx.x];
 	const uint32_t n = (uint32_t)(a.lcp[blockIdx.x + 1] - sb);
 	const RowRec *src = a.src + (sb - a.lbase);
@@ -800,7 +800,7 @@ __global__ __launch_bounds__(256) void k_lord_defer_post(LevelArgs a)
 {
 	const uint32_t i = blockIdx.x * 256u + threadIdx.x;
 	if (i >= a.nfeat) return;
-	const uint32_t j = a.feats[i];
+	const uint32_t j = level_feat(a, i);
 	const double2 msj = a.ms[(size_t)j * a.ms_stride];
 	const double2 st = a.stats[i];
 	const double hyp = a.hyp_uniform ? a.hyp0 : a.hyp[(size_t)a.attr_group[j] * a.hyp_stride];
@@ -925,7 +925,7 @@ __global__ __launch_bounds__(BLOCK) void k_mc_lord_defer(McArgs a)
 	__shared__ double2 recs[CAP * 4];
 	__shared__ uint32_t dsts[CAP];
 	__shared__ double lds[2 * (BLOCK / 64)];
-	const uint32_t j = a.feats[blockIdx.x];
+	const uint32_t j = level_feat(a, blockIdx.x);
 	const uint64_t sb = a.lcp[blockIdx.x];
 	const uint32_t n = (uint32_t)(a.lcp[blockIdx.x + 1] - sb);
 	const double2 *s = reinterpret_cast<const double2 *>(a.src + (sb - a.lbase));
@@ -987,7 +987,7 @@ __global__ __launch_bounds__(256) void k_mc_lord_defer_post(McArgs a)
 {
 	const uint32_t i = blockIdx.x * 256u + threadIdx.x;
 	if (i >= a.nfeat) return;
-	const uint32_t j = a.feats[i];
+	const uint32_t j = level_feat(a, i);
 	const double vo = a.par[(size_t)j * a.stride].x;
 	const double2 st = a.stats[i];
 	const uint32_t g = mc_group(a, j);

@@ -72,7 +72,7 @@ template <int BLOCK, int P, bool NEXT, int MODE>
 __global__ __launch_bounds__(BLOCK) void k_mc_v_level(McArgs a)
 {
 	__shared__ double lds[2 * (BLOCK / 64)];
-	const uint32_t j = a.feats[blockIdx.x];
+	const uint32_t j = level_feat(a, blockIdx.x);
 	const uint64_t cb = a.col_ptr[j];
 	const uint32_t n = (uint32_t)(a.col_ptr[j + 1] - cb);
 	const uint2 *col = a.csc + cb;
@@ -131,7 +131,7 @@ template <int BLOCK, bool NEXT, int MODE>
 __global__ __launch_bounds__(BLOCK) void k_mc_w_level(McArgs a)
 {
 	__shared__ double lds[2 * (BLOCK / 64)];
-	const uint32_t j = a.feats[blockIdx.x];
+	const uint32_t j = level_feat(a, blockIdx.x);
 	const uint64_t cb = a.col_ptr[j];
 	const uint32_t n = (uint32_t)(a.col_ptr[j + 1] - cb);
 	const uint2 *col = a.csc + cb;

@@ -264,6 +264,8 @@ McArgs mc_args(vbfm_ctx *c, uint32_t l, bool is_w, int f)
 	a.csc = c->tr.csc;
 	if (l < nlevels(c)) {
 		a.feats = c->level_feats + c->level_ptr[l];
+		a.feat_contig = c->level_base[l] != ~0u;
+		a.feat_base = c->level_base[l];
 		a.nfeat = c->level_ptr[l + 1] - c->level_ptr[l];
 		a.avg_len = c->level_avg[l];
 	}

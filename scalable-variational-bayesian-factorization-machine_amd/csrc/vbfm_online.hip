@@ -199,7 +199,7 @@ __global__ __launch_bounds__(256) void k_ov_v_level(LevelArgs a)
 	// the batch's col_ptr is indexed by level position (ov_regroup): coalesced, and the
 	// column's entries can be fetched in parallel with its parameters (the feature id is
 	// loaded with the bounds, before the branch on the column length)
-	const uint32_t j = a.feats[col_i];
+	const uint32_t j = level_feat(a, col_i);
 	const uint64_t cb = a.col_ptr[col_i];
 	const uint32_t n = (uint32_t)(a.col_ptr[col_i + 1] - cb);
 	if (n == 0) return;   // columns without entries in the batch are skipped (:389-394)
@@ -309,7 +309,7 @@ __global__ __launch_bounds__(256) void k_ov_w_level(LevelArgs a)
 	const uint64_t cb = a.col_ptr[col_i];
 	const uint32_t n = (uint32_t)(a.col_ptr[col_i + 1] - cb);
 	if (n == 0) return;   // (:364-368)
-	const uint32_t j = a.feats[col_i];
+	const uint32_t j = level_feat(a, col_i);
 	const uint2 *col = a.csc + cb;
 	const size_t pi = (size_t)j * a.ms_stride;
 	const double2 msj = a.ms[pi], natj = a.nat[(size_t)j * a.nat_stride];
@@ -447,7 +447,7 @@ __global__ __launch_bounds__(256) void k_ov_lord(LevelArgs a)
 	const uint32_t col_i = c0 + threadIdx.x / G;
 	const uint32_t lane = threadIdx.x % G;
 	const bool live = col_i < a.nfeat;
-	const uint32_t j = live ? a.feats[col_i] : 0u;
+	const uint32_t j = live ? level_feat(a, col_i) : 0u;
 	const uint64_t cb = live ? a.col_ptr[col_i] : 0u;
 	const uint32_t n = live ? (uint32_t)(a.col_ptr[col_i + 1] - cb) : 0u;
 	// the run's pieces into registers first, only as many rounds as the run needs (uniform
