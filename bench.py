@@ -82,10 +82,12 @@ def cpu_baseline(cfg, sample_rows, sample_factors, seed=1):
                                   "--seed", "1", "--sweep_factors", str(sample_factors)],
                                  cwd=tmp, capture_output=True, text=True, check=True, timeout=600).stdout
             r = json.loads([l for l in out.splitlines() if l.startswith("{")][0])
-            return {"value": r["nnz_k_per_s"], "unit": "nnz*k/s", "cores": 1, "kind": "reference",
-                    "sample": sample + "; oracle/_ref/ref_driver = the reference's fm_learn_vb compiled "
-                    "from its sources, taskset -c 0 (1 of %d host cores)" % os.cpu_count(),
-                    "seconds": r["sweep_s"]}
+            res = {"value": r["nnz_k_per_s"], "unit": "nnz*k/s", "cores": 1, "kind": "reference",
+                   "sample": sample + "; oracle/_ref/ref_driver = the reference's fm_learn_vb compiled "
+                   "from its sources, taskset -c 0 (1 of %d host cores)" % os.cpu_count(),
+                   "seconds": r["sweep_s"], "k0_seconds": r.get("k0_s")}
+            res.update(extrapolate_iteration(cfg, sample_rows, sample_factors, r["sweep_s"], r.get("k0_s")))
+            return res
         # no reference build on this host: time the oracle restatement (bit-exact port)
         import oracle_ctypes as oc
         tr = oc.Data(csr=(sample_rows, rp, f, v, y))
@@ -102,6 +104,19 @@ def cpu_baseline(cfg, sample_rows, sample_factors, seed=1):
                 "sample": sample + "; oracle/liboracle.so (C restatement, single thread)", "seconds": dt}
     finally:
         subprocess.run(["rm", "-rf", tmp])
+
+
+def extrapolate_iteration(cfg, sample_rows, sample_factors, sweep_s, k0_s):
+    """one reference iteration of the full configuration, extrapolated linearly
+    from the timed sample -- the k = 0 overhead (update_w0 + the w sweep) plus k factors of the
+    sweep, both scaled by rows (the per-row work is the same at every row count)."""
+    if k0_s is None or sweep_s <= 0:
+        return {}
+    scale = cfg["rows"] / float(sample_rows)
+    it = scale * (k0_s + sweep_s / sample_factors * cfg["k"])
+    return {"extrapolated_iteration_s": it,
+            "extrapolation": "extrapolated: (k0 + %d x one factor) x %d/%d rows" % (
+                cfg["k"], cfg["rows"], sample_rows)}
 
 
 def shard_plan(rows, world, rank, mode):

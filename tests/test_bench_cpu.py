@@ -104,3 +104,17 @@ def test_launch_event_stride_samples_every_level():
         for i in range(0, levels * k, s):
             timed[i % levels] += 1
         assert timed.max() - timed.min() <= 1
+
+
+def test_cpu_baseline_extrapolates_one_iteration():
+    """the reference's C4 iteration is extrapolated from the timed sample, the
+    k = 0 overhead plus k factors, scaled by rows, and labelled as such."""
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("bench", BENCH)
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+    cfg = dict(bench.CONFIGS["c4"])
+    r = bench.extrapolate_iteration(cfg, 2_000_000, 2, sweep_s=4.0, k0_s=0.5)
+    assert r["extrapolated_iteration_s"] == pytest.approx(50 * (0.5 + 2.0 * cfg["k"]))
+    assert r["extrapolation"].startswith("extrapolated")
+    assert bench.extrapolate_iteration(cfg, 2_000_000, 2, sweep_s=4.0, k0_s=None) == {}
