@@ -391,7 +391,8 @@ def main():
                   "k_mc_level_lord": "k_mc_lord_defer + all-reduce + post (per level)",
                   "k_v_level_fused": "k_v_level_stats + all-reduce + k_v_level_correct (per level)",
                   "k_mc_v_level": "k_mc_v_level stats + all-reduce + draw (per level)"}.get(kernel, kernel)
-    tf = os.path.join(ROOT, "profiles", "traffic_%s_%s%s.json" % (args.config, layout,
+    tlayout = ("level" if stats[-1].n_lord_batches else "column") if online else layout
+    tf = os.path.join(ROOT, "profiles", "traffic_%s_%s%s.json" % (args.config, tlayout,
                                                                    "_" + args.method if mc or online else ""))
     traffic_source = None
     if os.path.exists(tf) and not split:
