@@ -31,7 +31,11 @@
 extern "C" {
 #endif
 
-#define VBFM_ABI_VERSION 1
+/* 2: vbfm_synth_generate's model_seed / row_offset, vbfm_synth_multihot, VBFM_LAYOUT_ENTRY,
+ *    vbfm_iter_stats::ms_test_predict, checkpoints, vbfm_comm_info, vbfm_device_count and the
+ *    per-level step entry points. A binding checks vbfm_abi_version() against the value it was
+ *    built for and refuses a mismatch (struct sizes and argument lists differ). */
+#define VBFM_ABI_VERSION 2
 
 typedef struct vbfm_ctx vbfm_ctx;
 
@@ -107,6 +111,11 @@ int vbfm_create(vbfm_ctx **out, const vbfm_config *cfg);   /* fm_learn_vb::init 
 void vbfm_destroy(vbfm_ctx *ctx);
 const char *vbfm_last_error(const vbfm_ctx *ctx);
 int vbfm_abi_version(void);
+/* HIP devices visible to this process (0 without a GPU). No reference counterpart: the
+ * reference is single-threaded on the host; the multi-rank CLI (-devices) maps ranks to
+ * ordinals with it. It initialises the HIP runtime: call it only in the process that will
+ * use the GPU (never before a fork). */
+int vbfm_device_count(int32_t *n);
 
 /* ---- data (DataSubset hand-over, fm_learn_vb::learn, fm_learn_vb.h:746-786) ----------- */
 int vbfm_set_train(vbfm_ctx *ctx, const vbfm_csc *train);
@@ -158,6 +167,16 @@ int vbfm_step_w0(vbfm_ctx *ctx);                  /* update_w0, :504-525 */
 int vbfm_step_w(vbfm_ctx *ctx);                   /* the w sweep, :390-406 / :527-574 */
 int vbfm_step_qcache(vbfm_ctx *ctx, int32_t f);   /* zero + add_main_q, :411-418 / :354-381 */
 int vbfm_step_v(vbfm_ctx *ctx, int32_t f);        /* the v sweep of factor f, :420-438 / :577-644 */
+/* One dependency level of a sweep, for localising a parity miss below one
+ * sweep: level l (0-based, in order 0..L-1, L from vbfm_get_levels) of the w sweep, or of factor
+ * f's v sweep (its q-cache is made current at level 0). After level l the caches and parameters
+ * equal the reference's after its update_w / update_v of every feature of levels 0..l, features
+ * of a level in ascending id order (fm_learn_vb.h:390-406, 409-440; ref_driver levels). Same
+ * kernels as the whole sweep; one rank or the two-pass split (VBFM_DEFER=0), not the deferred
+ * split or feature shards. vbfm_get_rows / vbfm_get_params read the state between two levels;
+ * other steps are refused until the sweep's last level has run. */
+int vbfm_step_w_level(vbfm_ctx *ctx, int32_t level);
+int vbfm_step_v_level(vbfm_ctx *ctx, int32_t f, int32_t level);
 int vbfm_step_hyper(vbfm_ctx *ctx, int32_t *early_return); /* :446-498 */
 int vbfm_free_energy(vbfm_ctx *ctx, double *F);   /* :646-681 (value only, no file) */
 /* row caches: e (cache[].e), t/q/z of cache_t, q of cache (the factor q-cache) */

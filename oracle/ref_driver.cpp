@@ -22,6 +22,9 @@
 //   vb      : full VB run, per-iteration trace (trace.txt) and parameter dumps.
 //   steps   : one pass of the update_all sweep step by step (fm_learn_vb.h:383-440) with
 //             cache dumps after each step.
+//   levels  : the same sweeps with each dependency level's features in turn (ascending ids
+//             inside a level) and cache / parameter dumps after every level (the per-level
+//             parity of vbfm_step_w_level / vbfm_step_v_level).
 //   sweep   : CPU-baseline timing of the factor sweep (add_main_q + update_v over all
 //             features, fm_learn_vb.h:409-440) on a loaded data set; prints one JSON line.
 //   als/mcmc: MCMC/ALS learner (fm_learn_mcmc_simultaneous.h:50-305), per-iteration trace.
@@ -108,6 +111,7 @@ public:
 
 	virtual void _learn(DataSubset& train, DataSubset& test) {
 		if (mode == "steps") { run_steps(train, test); return; }
+		if (mode == "levels") { run_levels(train, test); return; }
 		if (mode == "sweep") { run_sweep(train); return; }
 		run_vb(train, test);
 	}
@@ -205,6 +209,76 @@ public:
 			dump_params(b.str());
 		}
 		std::cout << "STEPS_DONE" << std::endl;
+	}
+
+	// Dependency level of every train feature: level(j) = 1 + max level of a
+	// smaller feature id sharing a row with j, 1 without one -- the least fixed point of
+	// level[b] >= level[a] + 1 over consecutive distinct ids a < b of every row (read from the
+	// reference's own CSR, train.data).
+	std::vector<uint> feature_levels(DataSubset& train) {
+		const uint nf = train.data_t->getNumRows();
+		std::vector<std::pair<uint, uint> > edges;
+		for (train.data->begin(); !train.data->end(); train.data->next()) {
+			sparse_row<DATA_FLOAT>& row = train.data->getRow();
+			std::vector<uint> ids;
+			for (uint i = 0; i < row.size; i++) ids.push_back(row.data[i].id);
+			std::sort(ids.begin(), ids.end());
+			ids.erase(std::unique(ids.begin(), ids.end()), ids.end());
+			for (size_t i = 1; i < ids.size(); i++) edges.push_back(std::make_pair(ids[i - 1], ids[i]));
+		}
+		std::vector<uint> level(nf, 1);
+		for (bool changed = true; changed;) {
+			changed = false;
+			for (size_t e = 0; e < edges.size(); e++)
+				if (level[edges[e].second] < level[edges[e].first] + 1) {
+					level[edges[e].second] = level[edges[e].first] + 1;
+					changed = true;
+				}
+		}
+		return level;
+	}
+
+	// update_all's sweeps (fm_learn_vb.h:383-440) through the reference's own update_w /
+	// add_main_q / update_v, the features of each dependency level in ascending id order, level
+	// after level, with the caches and parameters dumped after every level. Features of
+	// different levels commute where the ascending sweep interleaves them (no shared row), so
+	// the state after the last level is the ascending sweep's bit for bit (checked against
+	// the "steps" dumps by tests/test_oracle_golden.py); after level l it is what the GPU's
+	// level kernels must hold after their level l (vbfm_step_w_level / vbfm_step_v_level).
+	void run_levels(DataSubset& train, DataSubset& test) {
+		init_caches(train, test);
+		const std::vector<uint> level = feature_levels(train);
+		uint L = 0;
+		for (size_t j = 0; j < level.size(); j++) L = std::max(L, level[j]);
+		std::cout << "LEVELS " << L << std::endl;
+		std::vector<double> lv(level.begin(), level.end());
+		dump_arr("levels", lv.data(), lv.size());
+		if (fm->k0) update_w0(train);
+		dump_rows("l_w0", train);
+		const uint nf = train.data_t->getNumRows();
+		if (fm->k1) {
+			for (uint l = 1; l <= L; l++) {
+				for (uint i = 0; i < nf; i++)
+					if (level[i] == l) update_w(mu_w_dash(i), sigma_w_dash(i), sigma_w(meta->attr_group(i)), train.data_t->getRow(i));
+				std::ostringstream a; a << "l_w_l" << (l - 1);
+				dump_rows(a.str(), train);
+				dump_params(a.str());
+			}
+		}
+		for (int f = 0; f < fm->num_factor; f++) {
+			for (uint c = 0; c < train.num_cases; c++) { cache[c].q = 0.0; cache_t[c].q = 0.0; cache_t[c].z = 0.0; }
+			add_main_q(train, f);
+			double* v = mu_v_dash.value[f];
+			double* v1 = sigma_v_dash.value[f];
+			for (uint l = 1; l <= L; l++) {
+				for (uint i = 0; i < nf; i++)
+					if (level[i] == l) update_v(f, v[i], v1[i], sigma_v(meta->attr_group(i), f), train.data_t->getRow(i));
+				std::ostringstream a; a << "l_f" << f << "_l" << (l - 1);
+				dump_rows(a.str(), train);
+				dump_params(a.str());
+			}
+		}
+		std::cout << "LEVELS_DONE" << std::endl;
 	}
 
 	// CPU baseline: time the factor sweep exactly as update_all runs it (fm_learn_vb.h:409-440).
@@ -315,7 +389,7 @@ static std::string arg(int argc, char** argv, const std::string& key, const std:
 
 int main(int argc, char** argv) {
 	if (argc < 2) {
-		fprintf(stderr, "usage: ref_driver vb|steps|sweep|als|mcmc --train F --test F --dim k0,k1,k --iter N --seed S [--init_stdev x] [--meta F] [--regular r0,rw,rv] [--dump DIR] [--sweep_factors n]\n");
+		fprintf(stderr, "usage: ref_driver vb|steps|levels|sweep|als|mcmc --train F --test F --dim k0,k1,k --iter N --seed S [--init_stdev x] [--meta F] [--regular r0,rw,rv] [--dump DIR] [--sweep_factors n]\n");
 		return 2;
 	}
 	std::cout.precision(17);

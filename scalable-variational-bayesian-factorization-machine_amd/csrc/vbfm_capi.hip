@@ -15,6 +15,7 @@
 #include <cstring>
 #include <string>
 #include <vector>
+#include <unistd.h>
 
 using namespace vbi;
 
@@ -900,6 +901,90 @@ void step_v(vbfm_ctx *c, int f)
 	else c->q_ready[(f + 1) & 1] = -1;
 }
 
+// ---- per-level steps (vbfm_step_w_level / vbfm_step_v_level) ----------------------------
+void no_partial(vbfm_ctx *c)
+{
+	if (c->part_kind >= 0)
+		throw std::string("a sweep driven level by level is in progress (finish it with vbfm_step_*_level)");
+}
+
+// level l of the w sweep (is_w) or of factor f's v sweep, exactly as the whole sweep runs it;
+// levels must come in order 0..L-1. One rank's fused kernels or the two-pass split (the
+// deferred split leaves a level's correction to the next level's kernel, so no per-level state
+// would exist to compare)
+void step_level(vbfm_ctx *c, bool is_w, int f, uint32_t l)
+{
+	const uint32_t L = nlevels(c);
+	if (c->shard_mode == VBFM_SHARD_FEATURES) throw std::string("per-level steps: not with feature shards");
+	if (c->deferred()) throw std::string("per-level steps: the deferred split keeps each level's correction pending (VBFM_DEFER=0)");
+	if (l >= L) throw std::string("level out of range");
+	const int kind = is_w ? 0 : 1;
+	if (c->part_kind < 0 ? l != 0 : (c->part_kind != kind || c->part_f != f || c->part_next != l))
+		throw std::string("per-level steps: levels of a sweep must come in order from level 0");
+	if (l == 0) {
+		if (is_w) rows_level_order(c);
+		else {
+			step_qcache(c, f);   // a no-op when current
+			rows_level_order(c);
+		}
+	}
+	c->part_kind = kind; c->part_f = f; c->part_next = l + 1;
+	sweep_level(c, l, is_w, f);
+	if (!is_w) c->qslot = f & 1;
+	if (l + 1 < L) return;
+	c->part_kind = -1;   // the sweep is complete: the bookkeeping of step_w / step_v
+	if (is_w) {
+		if (c->k > 0) c->q_ready[0] = 0;
+	} else {
+		c->q_ready[f & 1] = -1;
+		c->q_ready[(f + 1) & 1] = f + 1 < c->k ? f + 1 : -1;
+	}
+}
+
+// the records in row order while a level-by-level sweep of a level-ordered store is half done:
+// the field store holds them in the order of the next level (position p = the p-th entry of
+// that level's columns, features in schedule order, rows ascending), the entry store in the slot
+// of each row's next entry of a later level (else its first slot; rows without entries park at
+// nnz + r). Host-side debug readback.
+std::vector<RowRec> rows_mid_sweep(vbfm_ctx *c)
+{
+	const uint32_t n = c->tr.n, nf = c->tr.nf, L = nlevels(c);
+	const uint64_t nnz = c->tr.nnz;
+	std::vector<uint64_t> cp((size_t)nf + 1);
+	std::vector<uint2> ent(nnz);
+	std::vector<uint32_t> feats(nf);
+	HIPCHK(hipMemcpy(cp.data(), c->tr.col_ptr, cp.size() * 8, hipMemcpyDeviceToHost));
+	if (nnz) HIPCHK(hipMemcpy(ent.data(), c->tr.csc, nnz * 8, hipMemcpyDeviceToHost));
+	if (nf) HIPCHK(hipMemcpy(feats.data(), c->level_feats, (size_t)nf * 4, hipMemcpyDeviceToHost));
+	const size_t nrec = c->estore ? nnz + n : n;
+	std::vector<RowRec> store(nrec), out(n);
+	if (nrec) HIPCHK(hipMemcpy(store.data(), c->rows, nrec * sizeof(RowRec), hipMemcpyDeviceToHost));
+	const uint32_t done = c->part_next;   // levels 0 .. done-1 are swept
+	if (!c->estore) {
+		uint64_t p = 0;
+		for (uint32_t i = c->level_ptr[done % L]; i < c->level_ptr[done % L + 1]; i++) {
+			const uint32_t j = feats[i];
+			for (uint64_t e = cp[j]; e < cp[j + 1]; e++) out[ent[e].x & ~ROW_FIRST] = store[p++];
+		}
+		if (p != n) throw std::string("internal: a level of the field store does not hold every row");
+		return out;
+	}
+	std::vector<uint64_t> first(n, ~0ull), next(n, ~0ull);
+	uint64_t s = 0;
+	for (uint32_t l = 0; l < L; l++)
+		for (uint32_t i = c->level_ptr[l]; i < c->level_ptr[l + 1]; i++) {
+			const uint32_t j = feats[i];
+			for (uint64_t e = cp[j]; e < cp[j + 1]; e++, s++) {
+				const uint32_t r = ent[e].x & ~ROW_FIRST;
+				if (first[r] == ~0ull) first[r] = s;
+				if (l >= done && next[r] == ~0ull) next[r] = s;
+			}
+		}
+	for (uint32_t r = 0; r < n; r++)
+		out[r] = store[next[r] != ~0ull ? next[r] : first[r] != ~0ull ? first[r] : nnz + r];
+	return out;
+}
+
 double rows_energy(vbfm_ctx *c)
 {
 	rows_dense(c);
@@ -991,6 +1076,15 @@ float ev_ms(vbfm_ctx *c, int a, int b)
 extern "C" {
 
 int vbfm_abi_version(void) { return VBFM_ABI_VERSION; }
+
+int vbfm_device_count(int32_t *n)
+{
+	if (!n) return fail(nullptr, "vbfm_device_count: null argument");
+	int ndev = 0;
+	if (hipGetDeviceCount(&ndev) != hipSuccess) ndev = 0;
+	*n = ndev;
+	return 0;
+}
 
 const char *vbfm_last_error(const vbfm_ctx *ctx)
 {
@@ -1401,6 +1495,7 @@ int vbfm_init_caches(vbfm_ctx *c)
 		if (c->mc) throw std::string("an MCMC / ALS context: use the vbfm_mcmc_* entry points");
 		if (c->ov) throw std::string("an online VB context: use vbfm_online_epoch");
 		require_train(c);
+		no_partial(c);
 		// fm_learn_vb_simultaneous.h:37-44: yhat of train and test, T of train, e = y - yhat
 		rows_row_order(c);
 		const int bl = blocked_predict(c, c->tr);
@@ -1414,13 +1509,13 @@ int vbfm_init_caches(vbfm_ctx *c)
 int vbfm_step_w0(vbfm_ctx *c)
 {
 	if (!c) return fail(nullptr, "null context");
-	return guarded(c, [&] { require_train(c); if (c->k0) step_w0(c); sync(c); });
+	return guarded(c, [&] { require_train(c); no_partial(c); if (c->k0) step_w0(c); sync(c); });
 }
 
 int vbfm_step_w(vbfm_ctx *c)
 {
 	if (!c) return fail(nullptr, "null context");
-	return guarded(c, [&] { require_train(c); if (c->k1) step_w(c); sync(c); });
+	return guarded(c, [&] { require_train(c); no_partial(c); if (c->k1) step_w(c); sync(c); });
 }
 
 int vbfm_step_qcache(vbfm_ctx *c, int32_t f)
@@ -1429,6 +1524,7 @@ int vbfm_step_qcache(vbfm_ctx *c, int32_t f)
 	return guarded(c, [&] {
 		require_train(c);
 		if (f < 0 || f >= c->k) throw std::string("factor out of range");
+		no_partial(c);
 		step_qcache(c, f);
 		sync(c);
 	});
@@ -1440,8 +1536,31 @@ int vbfm_step_v(vbfm_ctx *c, int32_t f)
 	return guarded(c, [&] {
 		require_train(c);
 		if (f < 0 || f >= c->k) throw std::string("factor out of range");
+		no_partial(c);
 		if (c->q_ready[f & 1] != f) throw std::string("vbfm_step_v: q-cache of this factor is not current (vbfm_step_qcache)");
 		step_v(c, f);
+		sync(c);
+	});
+}
+
+int vbfm_step_w_level(vbfm_ctx *c, int32_t level)
+{
+	if (!c) return fail(nullptr, "null context");
+	return guarded(c, [&] {
+		require_train(c);
+		if (!c->k1) throw std::string("k1 = 0: there is no w sweep");
+		step_level(c, true, 0, (uint32_t)level);
+		sync(c);
+	});
+}
+
+int vbfm_step_v_level(vbfm_ctx *c, int32_t f, int32_t level)
+{
+	if (!c) return fail(nullptr, "null context");
+	return guarded(c, [&] {
+		require_train(c);
+		if (f < 0 || f >= c->k) throw std::string("factor out of range");
+		step_level(c, false, f, (uint32_t)level);
 		sync(c);
 	});
 }
@@ -1451,6 +1570,7 @@ int vbfm_step_hyper(vbfm_ctx *c, int32_t *early)
 	if (!c) return fail(nullptr, "null context");
 	return guarded(c, [&] {
 		require_train(c);
+		no_partial(c);
 		const bool e = step_hyper(c, nullptr, nullptr, nullptr);
 		if (early) *early = e ? 1 : 0;
 		sync(c);
@@ -1460,17 +1580,23 @@ int vbfm_step_hyper(vbfm_ctx *c, int32_t *early)
 int vbfm_free_energy(vbfm_ctx *c, double *F)
 {
 	if (!c || !F) return fail(c, "null argument");
-	return guarded(c, [&] { require_train(c); *F = free_energy(c, rows_energy(c)); });
+	return guarded(c, [&] { require_train(c); no_partial(c); *F = free_energy(c, rows_energy(c)); });
 }
 
 int vbfm_get_rows(vbfm_ctx *c, double *e, double *t, double *q, double *tq, double *tz)
 {
 	if (!c) return fail(nullptr, "null context");
 	return guarded(c, [&] {
-		rows_row_order(c);
-		sync(c);   // the readback below runs on the null stream, which does not wait for c->s
-		std::vector<RowRec> h(c->tr.n);
-		if (c->tr.n) HIPCHK(hipMemcpy(h.data(), c->rows, (size_t)c->tr.n * sizeof(RowRec), hipMemcpyDeviceToHost));
+		std::vector<RowRec> h;
+		if (c->part_kind >= 0 && c->lord) {   // half a level-by-level sweep on a level-ordered store
+			sync(c);
+			h = rows_mid_sweep(c);
+		} else {
+			rows_row_order(c);
+			sync(c);   // the readback below runs on the null stream, which does not wait for c->s
+			h.resize(c->tr.n);
+			if (c->tr.n) HIPCHK(hipMemcpy(h.data(), c->rows, (size_t)c->tr.n * sizeof(RowRec), hipMemcpyDeviceToHost));
+		}
 		const bool s1 = c->qslot == 1;
 		for (uint32_t i = 0; i < c->tr.n; i++) {
 			if (e) e[i] = h[i].e;
@@ -1519,7 +1645,9 @@ struct StateHeader {
 	int32_t nranks, rank;
 	uint32_t iter;
 	uint32_t level_order; // the records were in level-0 order (data-set sums add them in that order)
-	uint64_t reserved[4];
+	uint64_t layout;      // version 2: row layout (VBFM_LAYOUT_*) | shard mode << 8: both decide the
+	                      // order of the data-set sums, so a resume must use the same ones
+	uint64_t reserved[3];
 };
 static_assert(sizeof(StateHeader) == 104, "checkpoint header layout");
 constexpr char STATE_MAGIC[8] = {'V', 'B', 'F', 'M', 'S', 'T', '0', '1'};
@@ -1539,19 +1667,33 @@ uint64_t train_fingerprint(vbfm_ctx *c)
 	return h;
 }
 
+uint64_t state_layout(vbfm_ctx *c)
+{
+	const int lay = c->estore ? VBFM_LAYOUT_ENTRY : c->lord ? VBFM_LAYOUT_LEVEL : VBFM_LAYOUT_COLUMN;
+	return (uint64_t)lay | (uint64_t)c->shard_mode << 8;
+}
+
 StateHeader state_header(vbfm_ctx *c, uint32_t iter)
 {
 	StateHeader h;
 	memset(&h, 0, sizeof(h));
 	memcpy(h.magic, STATE_MAGIC, 8);
-	h.version = 1;
+	h.version = 2;
 	h.k0 = c->k0; h.k1 = c->k1; h.k = c->k;
 	h.D = c->D; h.G = c->G;
 	h.n_train = c->tr.n; h.nf_train = c->tr.nf; h.nnz_train = c->tr.nnz;
 	h.data_fp = train_fingerprint(c);
 	h.nranks = c->nranks; h.rank = c->rank;
 	h.iter = iter;
+	h.layout = state_layout(c);
 	return h;
+}
+
+// bytes that follow the header: ms_w, ms_v, hyper parameters, four scalars, the row records
+uint64_t state_payload(vbfm_ctx *c)
+{
+	return (uint64_t)c->D * 16 + (uint64_t)c->k * c->D * 16 + (uint64_t)c->G * 8 + (uint64_t)c->G * c->k * 8 + 32 +
+	       (uint64_t)c->tr.n * sizeof(RowRec);
 }
 
 struct File {
@@ -1609,19 +1751,31 @@ int vbfm_save_state(vbfm_ctx *c, const char *path, uint32_t iter)
 	if (!c || !path) return fail(c, "null argument");
 	return guarded(c, [&] {
 		require_vb_state(c, "vbfm_save_state");
+		no_partial(c);
 		StateHeader h = state_header(c, iter);
 		h.level_order = c->rows_lorder ? 1 : 0;
 		rows_row_order(c);
-		File f(path, "wb");
-		f.write(&h, sizeof(h));
-		dev_to_file(c, f, c->ms_w, (size_t)c->D * sizeof(double2));
-		dev_to_file(c, f, c->ms_v, (size_t)c->k * c->D * sizeof(double2));
-		f.write(c->hyp_w.data(), c->hyp_w.size() * 8);
-		f.write(c->hyp_v.data(), c->hyp_v.size() * 8);
-		const double sc[4] = {c->alpha, c->sigma_0, c->mu0, c->s0d};
-		f.write(sc, sizeof(sc));
-		dev_to_file(c, f, c->rows, (size_t)c->tr.n * sizeof(RowRec));
-		if (fflush(f.f) != 0) throw std::string("short write to ") + path;
+		// written beside the target and renamed over it once complete and on disk: a failed
+		// or interrupted save never destroys the previous checkpoint (-resume X -save_state X)
+		const std::string tmp = std::string(path) + ".tmp";
+		try {
+			File f(tmp.c_str(), "wb");
+			f.write(&h, sizeof(h));
+			dev_to_file(c, f, c->ms_w, (size_t)c->D * sizeof(double2));
+			dev_to_file(c, f, c->ms_v, (size_t)c->k * c->D * sizeof(double2));
+			f.write(c->hyp_w.data(), c->hyp_w.size() * 8);
+			f.write(c->hyp_v.data(), c->hyp_v.size() * 8);
+			const double sc[4] = {c->alpha, c->sigma_0, c->mu0, c->s0d};
+			f.write(sc, sizeof(sc));
+			dev_to_file(c, f, c->rows, (size_t)c->tr.n * sizeof(RowRec));
+			if (fflush(f.f) != 0 || fsync(fileno(f.f)) != 0) throw std::string("short write to ") + tmp;
+			if (fclose(f.f) != 0) { f.f = nullptr; throw std::string("short write to ") + tmp; }
+			f.f = nullptr;
+			if (rename(tmp.c_str(), path) != 0) throw std::string("cannot rename ") + tmp + " to " + path;
+		} catch (...) {
+			unlink(tmp.c_str());
+			throw;
+		}
 		if (h.level_order) rows_level_order(c);   // the run goes on exactly as without the save
 	});
 }
@@ -1631,11 +1785,12 @@ int vbfm_load_state(vbfm_ctx *c, const char *path, uint32_t *iter)
 	if (!c || !path) return fail(c, "null argument");
 	return guarded(c, [&] {
 		require_vb_state(c, "vbfm_load_state");
+		no_partial(c);
 		File f(path, "rb");
 		StateHeader h;
 		f.read(&h, sizeof(h));
-		if (memcmp(h.magic, STATE_MAGIC, 8) != 0 || h.version != 1)
-			throw std::string("not a libvbfm VB checkpoint: ") + path;
+		if (memcmp(h.magic, STATE_MAGIC, 8) != 0 || h.version != 2)
+			throw std::string("not a libvbfm VB checkpoint (version 2): ") + path;
 		if (h.k0 != c->k0 || h.k1 != c->k1 || h.k != c->k || h.D != c->D || h.G != c->G)
 			throw std::string("checkpoint of another model configuration (-dim / num_attribute / groups)");
 		if (h.nranks != c->nranks || h.rank != c->rank)
@@ -1643,6 +1798,13 @@ int vbfm_load_state(vbfm_ctx *c, const char *path, uint32_t *iter)
 		if (h.n_train != c->tr.n || h.nf_train != c->tr.nf || h.nnz_train != c->tr.nnz ||
 		    h.data_fp != train_fingerprint(c))
 			throw std::string("checkpoint of another train data set");
+		if (h.layout != state_layout(c))
+			throw std::string("checkpoint of another row layout or shard mode (the data-set sums would add the rows in "
+			                  "another order): resume with the same VBFM_LAYOUT / vbfm_set_layout and shard mode");
+		// the whole file is there before any state is replaced
+		if (fseek(f.f, 0, SEEK_END) != 0 || (uint64_t)ftell(f.f) != sizeof(h) + state_payload(c) ||
+		    fseek(f.f, (long)sizeof(h), SEEK_SET) != 0)
+			throw std::string("checkpoint file truncated or of another size: ") + path;
 		rows_row_order(c);
 		file_to_dev(c, f, c->ms_w, (size_t)c->D * sizeof(double2));
 		file_to_dev(c, f, c->ms_v, (size_t)c->k * c->D * sizeof(double2));
@@ -1670,6 +1832,7 @@ int vbfm_factor_sweep(vbfm_ctx *c, double *ms_device)
 	if (!c) return fail(nullptr, "null context");
 	return guarded(c, [&] {
 		require_train(c);
+		no_partial(c);
 		HIPCHK(hipEventRecord(c->ev[EV_BEGIN], c->s));
 		for (int f = 0; f < c->k; f++) { step_qcache(c, f); step_v(c, f); }
 		HIPCHK(hipEventRecord(c->ev[EV_V], c->s));
@@ -1685,6 +1848,7 @@ int vbfm_iterate(vbfm_ctx *c, vbfm_iter_stats *o)
 		if (c->mc) throw std::string("an MCMC / ALS context: use the vbfm_mcmc_* entry points");
 		if (c->ov) throw std::string("an online VB context: use vbfm_online_epoch");
 		require_train(c);
+		no_partial(c);
 		if (!c->e_test) throw std::string("no test data set (vbfm_set_test)");
 		vbfm_iter_stats st;
 		memset(&st, 0, sizeof(st));
@@ -1727,11 +1891,16 @@ int vbfm_iterate(vbfm_ctx *c, vbfm_iter_stats *o)
 		}
 		double energy = 0.0;
 		bool early;
-		{
+		try {
 			Range r("hyper + free energy");
 			early = step_hyper(c, &energy, &st.nan_alpha, &st.inf_alpha);
 			st.free_energy_valid = early ? 0 : 1;
 			st.free_energy = early ? NAN : free_energy(c, energy);
+		} catch (...) {
+			// the overlapped prediction is still queued on s_test: later calls on c->s (the next
+			// sweeps write ms_v, get_test_pred reads e_test) must not race it
+			if (overlap) (void)hipStreamWaitEvent(c->s, c->ev[EV_TP1], 0);
+			throw;
 		}
 		HIPCHK(hipEventRecord(c->ev[EV_HYPER], c->s));
 		// test prediction and metrics (fm_learn_vb_simultaneous.h:125-222)

@@ -10,7 +10,18 @@
 //     predict() body is commented out and leaves the vector uninitialised, fm_learn_vb.h:321);
 //   * -method sgd/sgda/... and -task c are rejected with an error instead of running
 //     other learners; -relation is not supported;
-//   * extra flags: -device (HIP ordinal), -vfile 0 (skip writing v_file.txt).
+//   * extra flags: -device (HIP ordinal), -vfile 0 (skip writing v_file.txt), -save_state /
+//     -resume (checkpoints), and the multi-GPU launch: -devices N | o0,o1,..., -shard
+//     rows|features, -transport rccl|host, -plan 1 (print the ranks' shard plan, no GPU).
+//
+// Multi-GPU (-devices): the reference is one process on one core. Here this process parses the
+// flags and loads the data (host code only, no HIP call), then forks one rank process per GPU
+// BEFORE anything touches a GPU; each rank hands its slice of the train and test rows to its
+// own libvbfm context (row shards: rows [N r/P, N (r+1)/P), the exact mode) or all rows
+// (feature shards) and joins the communicator: RCCL over xGMI (rank 0's ncclUniqueId travels
+// through a shared-memory page) or, with -transport host, an all-reduce through shared memory
+// (several ranks may then share one GPU, which RCCL refuses). Rank 0 prints the reference's
+// lines and writes its files; this process waits, and kills the other ranks when one fails.
 #include "../../include/vbfm.h"
 
 #include <cmath>
@@ -23,7 +34,14 @@
 #include <map>
 #include <sstream>
 #include <string>
+#include <algorithm>
+#include <csignal>
+#include <cstring>
+#include <pthread.h>
+#include <sys/mman.h>
 #include <sys/resource.h>
+#include <sys/wait.h>
+#include <unistd.h>
 #include <vector>
 
 namespace {
@@ -136,6 +154,133 @@ void load(const std::string &fn, Data &d, const char *what)
 	          << "\tmin_target=" << d.h.min_target << "\tmax_target=" << d.h.max_target << std::endl;
 }
 
+// ---- ranks ------------------------------------------------------------------------------
+// The shared-memory page the forked ranks use: a process-shared barrier, rank 0's RCCL
+// unique id, one slot per rank for the host all-reduce, and the gathered test predictions
+// (-out). Created by the launching process before fork (MAP_SHARED | MAP_ANONYMOUS).
+struct ShmHeader {
+	pthread_barrier_t bar;
+	uint8_t uid[128];
+	uint64_t slot_bytes;
+	int32_t nranks;
+};
+
+struct Slice {   // one rank's rows of a data set as the C-ABI takes them
+	std::vector<uint64_t> cp;
+	std::vector<vbfm_entry> ent;
+	std::vector<float> y;
+	vbfm_csc csc{};
+};
+
+struct Rank {
+	int32_t rank = 0, nranks = 1;
+	int32_t device = 0;            // HIP ordinal of this rank (-1: rank % visible devices, resolved in the rank)
+	bool host = false;             // -transport host
+	int32_t shard = VBFM_SHARD_ROWS;
+	ShmHeader *shm = nullptr;
+	char *slots = nullptr;         // nranks x slot_bytes
+	double *test_pred = nullptr;   // [test rows] gathered predictions
+	bool lead() const { return rank == 0; }
+	bool multi() const { return nranks > 1; }
+	bool row_shards() const { return multi() && shard == VBFM_SHARD_ROWS; }
+	void barrier() const
+	{
+		if (shm) pthread_barrier_wait(&shm->bar);
+	}
+	// this rank's rows [lo, hi) of n (row shards; all rows otherwise)
+	void range(uint32_t n, uint32_t *lo, uint32_t *hi) const
+	{
+		if (!row_shards()) { *lo = 0; *hi = n; return; }
+		*lo = (uint32_t)((uint64_t)n * rank / nranks);
+		*hi = (uint32_t)((uint64_t)n * (rank + 1) / nranks);
+	}
+	// the rank's slice of a loaded data set: each column's entries of rows [lo, hi) (a
+	// contiguous run: create_data_t lists a column's rows in ascending order, Data.h:457-509),
+	// row ids made local, every column kept (the feature count stays global)
+	Slice slice(const vbfm_host_data &h) const
+	{
+		Slice s;
+		uint32_t lo, hi;
+		range(h.num_rows, &lo, &hi);
+		s.cp.assign((size_t)h.num_feature + 1, 0);
+		for (uint32_t j = 0; j < h.num_feature; j++) {
+			const vbfm_entry *b = h.col_ent + h.col_ptr[j], *e = h.col_ent + h.col_ptr[j + 1];
+			const vbfm_entry *a = std::lower_bound(b, e, lo, [](const vbfm_entry &x, uint32_t r) { return x.id < r; });
+			const vbfm_entry *z = std::lower_bound(a, e, hi, [](const vbfm_entry &x, uint32_t r) { return x.id < r; });
+			for (const vbfm_entry *p = a; p < z; p++) s.ent.push_back(vbfm_entry{p->id - lo, p->value});
+			s.cp[j + 1] = s.ent.size();
+		}
+		s.y.assign(h.target + lo, h.target + hi);
+		s.csc = vbfm_csc{hi - lo, h.num_feature, (uint64_t)s.ent.size(), s.cp.data(), s.ent.data(), s.y.data()};
+		return s;
+	}
+	// a per-rank file name for -save_state / -resume (one checkpoint per rank)
+	std::string rank_file(const std::string &path) const
+	{
+		return multi() ? path + "." + std::to_string(rank) : path;
+	}
+};
+
+// host all-reduce through the shared slots: every rank copies its chunk into its slot, then
+// every rank reduces the slots in rank order 0..P-1 (the same arithmetic on every rank, so
+// all ranks hold identical results), chunk by chunk
+template <typename T>
+void reduce_slots(const Rank &rk, T *out, size_t n, size_t stride, int32_t op)
+{
+	for (size_t i = 0; i < n; i++) {
+		T acc = ((const T *)rk.slots)[i];
+		for (int32_t r = 1; r < rk.nranks; r++) {
+			const T v = ((const T *)(rk.slots + (size_t)r * stride))[i];
+			acc = op == VBFM_X_MAX ? std::max(acc, v) : (T)(acc + v);
+		}
+		out[i] = acc;
+	}
+}
+
+int shm_exchange(void *user, void *buf, uint64_t count, int32_t dtype, int32_t op)
+{
+	const Rank &rk = *(const Rank *)user;
+	const size_t es = dtype == VBFM_X_F64 ? 8 : dtype == VBFM_X_U32 ? 4 : 1;
+	const size_t stride = rk.shm->slot_bytes, per = stride / es;
+	char *b = (char *)buf;
+	for (uint64_t off = 0; off < count; off += per) {
+		const size_t n = (size_t)std::min<uint64_t>(per, count - off);
+		memcpy(rk.slots + (size_t)rk.rank * stride, b + off * es, n * es);
+		rk.barrier();
+		if (dtype == VBFM_X_F64) reduce_slots(rk, (double *)(b + off * es), n, stride, op);
+		else if (dtype == VBFM_X_U32) reduce_slots(rk, (uint32_t *)(b + off * es), n, stride, op);
+		else reduce_slots(rk, (uint8_t *)(b + off * es), n, stride, op);
+		rk.barrier();   // no slot is overwritten before every rank has read it
+	}
+	return 0;
+}
+
+// the rank joins its communicator (before vbfm_set_train) and picks the shard mode
+void join(vbfm_ctx *ctx, const Rank &rk)
+{
+	if (!rk.multi()) return;
+	check(vbfm_set_shard_mode(ctx, rk.shard, 0), ctx);
+	if (rk.host) {
+		check(vbfm_comm_init_host(ctx, rk.nranks, rk.rank, shm_exchange, (void *)&rk), ctx);
+		return;
+	}
+	if (rk.lead()) check(vbfm_comm_unique_id(rk.shm->uid), nullptr);
+	rk.barrier();
+	check(vbfm_comm_init(ctx, rk.nranks, rk.rank, rk.shm->uid), ctx);
+}
+
+// test predictions of every rank into the shared array (row shards): rank 0 then has them all
+void gather_test(const Rank &rk, const Data &test, const std::vector<double> &local, std::vector<double> *all)
+{
+	if (!rk.row_shards()) { *all = local; return; }
+	uint32_t lo, hi;
+	rk.range(test.h.num_rows, &lo, &hi);
+	std::copy(local.begin(), local.end(), rk.test_pred + lo);
+	rk.barrier();
+	if (rk.lead()) all->assign(rk.test_pred, rk.test_pred + test.h.num_rows);
+	rk.barrier();
+}
+
 }  // namespace
 
 // -method mcmc | als (libfm.cpp:131-135, 297-305, 367-411; fm_learn_mcmc_simultaneous.h:50-305)
@@ -148,27 +293,29 @@ struct McmcRun {
 	const uint32_t *groups;
 	uint32_t G, D;
 	int k0, k1, k;
-	int32_t device;
 	bool vfile;
 	std::string rlog_file, out_file;
 };
 
-static void run_mcmc(const McmcRun &r, Data &train, Data &test)
+static void run_mcmc(const McmcRun &r, Data &train, Data &test, const Rank &rk)
 {
 	vbfm_ctx *ctx = nullptr;
 	try {
-		vbfm_config cfg{r.k0, r.k1, r.k, r.D, r.G, r.groups, train.h.min_target, train.h.max_target, r.device, 0};
+		vbfm_config cfg{r.k0, r.k1, r.k, r.D, r.G, r.groups, train.h.min_target, train.h.max_target, rk.device, 0};
 		check(vbfm_create(&ctx, &cfg), nullptr);
-		const vbfm_csc tr = train.csc(), te = test.csc();
-		check(vbfm_set_train(ctx, &tr), ctx);
-		check(vbfm_set_test(ctx, &te), ctx);
+		join(ctx, rk);
+		{
+			const Slice tr = rk.slice(train.h), te = rk.slice(test.h);
+			check(vbfm_set_train(ctx, &tr.csc), ctx);
+			check(vbfm_set_test(ctx, &te.csc), ctx);
+		}
 		vbfm_mcmc_config mc{r.sample, r.sample, VBFM_RNG_REFERENCE, r.seed, r.init_stdev,
 		                    r.reg.empty() ? nullptr : r.reg.data(), (int32_t)r.reg.size()};
 		check(vbfm_mcmc_init(ctx, &mc), ctx);
 		const size_t kd = (size_t)r.k * r.D, gk = (size_t)r.G * r.k;
 		std::vector<double> w(r.D), v(kd), wmu(r.G), wl(r.G), vmu(gk), vl(gk);
 		vbfm_mcmc_params p{w.data(), v.data(), wmu.data(), wl.data(), vmu.data(), vl.data(), 0, 0, 0};
-		if (r.vfile) {   // fm_model.h:98: the initial factors (DMatrix::save, matrix.h:129-152)
+		if (r.vfile && rk.lead()) {   // fm_model.h:98: the initial factors (DMatrix::save, matrix.h:129-152)
 			check(vbfm_mcmc_get_params(ctx, &p), ctx);
 			std::ofstream vf("v_file.txt");
 			for (int f = 0; f < r.k; f++) {
@@ -178,7 +325,7 @@ static void run_mcmc(const McmcRun &r, Data &train, Data &test)
 		}
 		std::ofstream *rlog_out = nullptr;
 		RLog *rlog = nullptr;
-		if (!r.rlog_file.empty()) {   // fm_learn::init + fm_learn_mcmc::init fields (:1118-1149)
+		if (!r.rlog_file.empty() && rk.lead()) {   // fm_learn::init + fm_learn_mcmc::init fields (:1118-1149)
 			rlog_out = new std::ofstream(r.rlog_file.c_str());
 			if (!rlog_out->is_open()) throw std::string("Unable to open file " + r.rlog_file);
 			std::cout << "logging to " << r.rlog_file << std::endl;
@@ -202,7 +349,7 @@ static void run_mcmc(const McmcRun &r, Data &train, Data &test)
 		std::ostringstream tag;
 		tag << r.k0 << r.k1 << r.k;
 		const std::string f_rmse = "test_rmse_" + tag.str() + "_mcmc";
-		{ std::ofstream a(f_rmse.c_str()); }   // truncate (:52-62)
+		if (rk.lead()) { std::ofstream a(f_rmse.c_str()); }   // truncate (:52-62)
 		for (uint32_t it = 0; it < r.num_iter; it++) {
 			const double t_user = usertime();
 			const clock_t t_clock = clock();
@@ -242,15 +389,22 @@ static void run_mcmc(const McmcRun &r, Data &train, Data &test)
 			}
 			std::cout << "#Iter=" << std::setw(3) << it << "\tTrain=" << st.train_rmse << "\tTest=" << st.rmse_all
 			          << std::endl;
-			std::ofstream fr(f_rmse.c_str(), std::ios_base::app);
-			fr << st.rmse_all << "\n";
+			if (rk.lead()) {
+				std::ofstream fr(f_rmse.c_str(), std::ios_base::app);
+				fr << st.rmse_all << "\n";
+			}
 		}
 		std::cout << "after learn" << std::endl;   // libfm.cpp:507; no Final line for mcmc (:509)
 		if (!r.out_file.empty()) {                 // libfm.cpp:514-519
-			std::vector<double> pred(test.h.num_rows);
+			uint32_t lo, hi;
+			rk.range(test.h.num_rows, &lo, &hi);
+			std::vector<double> pred(hi - lo), all;
 			check(vbfm_mcmc_get_test_pred(ctx, (int32_t)r.num_iter, pred.data()), ctx);
-			std::ofstream o(r.out_file.c_str());
-			for (double x : pred) o << x << std::endl;
+			gather_test(rk, test, pred, &all);
+			if (rk.lead()) {
+				std::ofstream o(r.out_file.c_str());
+				for (double x : all) o << x << std::endl;
+			}
 		}
 		delete rlog;
 		delete rlog_out;
@@ -294,16 +448,16 @@ struct OnlineRun {
 	const uint32_t *groups;
 	uint32_t G, D;
 	int k0, k1, k;
-	int32_t device;
 	bool vfile;
 	std::string rlog_file, out_file;
 };
 
-static void run_online(const OnlineRun &r, Data &train, Data &test)
+static void run_online(const OnlineRun &r, Data &train, Data &test, const Rank &rk)
 {
+	if (rk.multi()) throw std::string("-method vb_online runs on one GPU (-devices 1)");
 	vbfm_ctx *ctx = nullptr;
 	try {
-		vbfm_config cfg{r.k0, r.k1, r.k, r.D, r.G, r.groups, train.h.min_target, train.h.max_target, r.device, 0};
+		vbfm_config cfg{r.k0, r.k1, r.k, r.D, r.G, r.groups, train.h.min_target, train.h.max_target, rk.device, 0};
 		check(vbfm_create(&ctx, &cfg), nullptr);
 		const vbfm_csc tr = train.csc(), te = test.csc();
 		check(vbfm_set_train(ctx, &tr), ctx);
@@ -389,15 +543,295 @@ static void run_online(const OnlineRun &r, Data &train, Data &test)
 	}
 }
 
-int main(int argc, char **argv)
+// -method vb (libfm.cpp:306-311, 366, 496-519; fm_learn_vb_simultaneous.h:18-259)
+struct VbRun {
+	uint32_t seed;
+	double init_stdev;
+	uint32_t num_iter;
+	const uint32_t *groups;
+	uint32_t G, D;
+	int k0, k1, k;
+	bool vfile;
+	std::string rlog_file, out_file, save_file, resume_file;
+};
+
+static void run_vb(const VbRun &r, Data &train, Data &test, const Rank &rk)
 {
 	vbfm_ctx *ctx = nullptr;
+	try {
+		vbfm_config cfg{r.k0, r.k1, r.k, r.D, r.G, r.groups, train.h.min_target, train.h.max_target, rk.device, 0};
+		check(vbfm_create(&ctx, &cfg), nullptr);
+		join(ctx, rk);
+		{
+			const Slice tr = rk.slice(train.h), te = rk.slice(test.h);
+			check(vbfm_set_train(ctx, &tr.csc), ctx);
+			check(vbfm_set_test(ctx, &te.csc), ctx);
+		}
+		const int k = r.k;
+		const uint32_t D = r.D, G = r.G;
+
+		// fm.init + fm.w.init_normal + fml->init draws (libfm.cpp:123-366): the same stream on
+		// the host (small models) or generated on the device (VBFM_INIT=host|replay overrides);
+		// every rank draws the same values. -resume takes the state from its file instead (no
+		// draws, no v_file.txt)
+		const bool resume = !r.resume_file.empty();
+		const size_t kd = (size_t)k * D;
+		const bool vfile = r.vfile && !resume && rk.lead();
+		const char *init_env = getenv("VBFM_INIT");
+		const bool replay = init_env ? std::string(init_env) == "replay" : kd + D >= 2000000;
+		std::vector<double> fm_v(vfile || (!replay && !resume) ? kd : 0);
+		if (replay && !resume) {
+			check(vbfm_init_params_replay(ctx, r.seed, r.init_stdev, vfile ? fm_v.data() : nullptr, nullptr), ctx);
+		} else if (!resume) {
+			std::vector<double> mu_w(D), sig_w(D), mu_v(kd), sig_v(kd), hw(G), hv((size_t)G * k);
+			vbfm_params p{mu_w.data(), sig_w.data(), mu_v.data(), sig_v.data(), hw.data(), hv.data(), 0, 0, 0, 0};
+			check(vbfm_init_params_host(r.seed, r.init_stdev, k, D, G, &p, fm_v.data(), nullptr), nullptr);
+			check(vbfm_set_params(ctx, &p), ctx);
+		}
+		if (vfile) write_vfile(fm_v, k, D);
+		fm_v.clear();
+		fm_v.shrink_to_fit();
+
+		// -rlog (libfm.cpp:353-363; fields of fm_learn::init and fm_learn_vb::init)
+		std::ofstream *rlog_out = nullptr;
+		RLog *rlog = nullptr;
+		if (!r.rlog_file.empty() && rk.lead()) {
+			rlog_out = new std::ofstream(r.rlog_file.c_str());
+			if (!rlog_out->is_open()) throw std::string("Unable to open file " + r.rlog_file);
+			std::cout << "logging to " << r.rlog_file << std::endl;
+			rlog = new RLog(rlog_out);
+			for (const char *f : {"rmse", "mae", "time_pred", "time_learn", "time_learn2", "time_learn4", "alpha",
+			                      "rmse_mcmc_this", "rmse_mcmc_all"})
+				rlog->add(f);
+			for (uint32_t g = 0; g < G; g++) {
+				std::ostringstream ss;
+				ss << "wmu[" << g << "]"; rlog->add(ss.str()); ss.str("");
+				ss << "wlambda[" << g << "]"; rlog->add(ss.str()); ss.str("");
+				for (int f = 0; f < k; f++) {
+					ss << "vmu[" << g << "," << f << "]"; rlog->add(ss.str()); ss.str("");
+					ss << "vlambda[" << g << "," << f << "]"; rlog->add(ss.str()); ss.str("");
+				}
+			}
+			rlog->init();
+		}
+
+		// fm_learn_vb_simultaneous::_learn
+		uint32_t it0 = 0;
+		if (resume) {
+			check(vbfm_load_state(ctx, rk.rank_file(r.resume_file).c_str(), &it0), ctx);
+			std::cout << "resuming from " << r.resume_file << " after " << it0 << " iterations" << std::endl;
+		} else {
+			check(vbfm_init_caches(ctx), ctx);
+		}
+		std::ostringstream tag;
+		tag << r.k0 << r.k1 << k;
+		const std::string f_rmse = "test_rmse_" + tag.str() + "_vb", f_fe = "free_energy_" + tag.str() + "_vb";
+		if (!resume && rk.lead()) { std::ofstream a(f_rmse.c_str()); std::ofstream b(f_fe.c_str()); }   // truncate (:58-73); a resumed run appends
+		for (uint32_t it = it0; it < it0 + r.num_iter; it++) {
+			time_t now = time(0);
+			std::cout << ctime(&now) << std::endl;
+			const double t_user = usertime();
+			const clock_t t_clock = clock();
+			const double t_wall = (double)time(NULL);
+			vbfm_iter_stats st;
+			check(vbfm_iterate(ctx, &st), ctx);
+			if (st.free_energy_valid) {   // fm_learn_vb.h:678-680
+				if (rk.lead()) {
+					std::ofstream fe(f_fe.c_str(), std::ios_base::app);
+					fe << -st.free_energy << "\n";
+				}
+				std::cout << "free energy " << st.free_energy << std::endl;
+			}
+			nan_reports(st.nan_alpha, st.inf_alpha, st.nan_mu_w, st.inf_mu_w, st.nan_sigma_w, st.nan_mu_v, st.inf_mu_v,
+			            st.nan_sigma_v);
+			if (rlog) {
+				rlog->log("time_learn", usertime() - t_user);
+				rlog->log("time_learn2", (double)(clock() - t_clock) / CLOCKS_PER_SEC);
+				rlog->log("time_learn4", (double)time(NULL) - t_wall);
+				rlog->log("rmse_mcmc_this", st.rmse);
+				rlog->newline();
+			}
+			if (rk.lead()) {
+				std::ofstream fr(f_rmse.c_str(), std::ios_base::app);
+				fr << st.rmse << "\n";
+			}
+			std::cout << "#Iter=" << std::setw(3) << it << "\tTrain=" << st.train_quirk << "\tTest=" << st.rmse << std::endl;
+		}
+		if (!r.save_file.empty())
+			check(vbfm_save_state(ctx, rk.rank_file(r.save_file).c_str(), it0 + r.num_iter), ctx);
+		// libfm.cpp:509-511: fm_learn_vb::evaluate returns NaN
+		std::cout << "Final\tTrain=" << NAN << "\tTest=" << NAN << std::endl;
+		if (!r.out_file.empty()) {   // libfm.cpp:514-519, DVector::save (matrix.h:284-295)
+			uint32_t lo, hi;
+			rk.range(test.h.num_rows, &lo, &hi);
+			std::vector<double> pred(hi - lo), all;
+			check(vbfm_get_test_pred(ctx, pred.data()), ctx);
+			gather_test(rk, test, pred, &all);
+			if (rk.lead()) {
+				std::ofstream o(r.out_file.c_str());
+				for (double v : all) o << v << std::endl;
+			}
+		}
+		delete rlog;
+		delete rlog_out;
+		vbfm_destroy(ctx);
+	} catch (...) {
+		if (ctx) vbfm_destroy(ctx);
+		throw;
+	}
+}
+
+// everything one rank runs, given the parsed command line
+struct Job {
+	std::string method;
+	VbRun vb;
+	McmcRun mc;
+	OnlineRun online;
+	bool plan = false;
+};
+
+// -plan 1: the rank's launch and shard plan as one JSON line; with -transport host the ranks
+// also all-reduce their rank numbers through the shared slots (sum and max), so the exchange
+// itself is exercised without a GPU
+static void print_plan(const Job &job, const Data &train, const Data &test, const Rank &rk)
+{
+	const Slice tr = rk.slice(train.h), te = rk.slice(test.h);
+	uint32_t lo, hi, tlo, thi;
+	rk.range(train.h.num_rows, &lo, &hi);
+	rk.range(test.h.num_rows, &tlo, &thi);
+	double xs[2] = {(double)rk.rank, (double)tr.csc.nnz};
+	uint32_t xm = (uint32_t)rk.rank;
+	const bool xchg = rk.multi() && rk.host;
+	if (xchg) {
+		shm_exchange((void *)&rk, xs, 2, VBFM_X_F64, VBFM_X_SUM);
+		shm_exchange((void *)&rk, &xm, 1, VBFM_X_U32, VBFM_X_MAX);
+	}
+	char line[1024];
+	snprintf(line, sizeof(line),
+	         "{\"rank\": %d, \"nranks\": %d, \"device\": %d, \"transport\": \"%s\", \"shard\": \"%s\", "
+	         "\"method\": \"%s\", \"train_rows\": [%u, %u], \"train_nnz\": %llu, \"train_features\": %u, "
+	         "\"test_rows\": [%u, %u], \"test_nnz\": %llu, \"xchg_rank_sum\": %.17g, \"xchg_nnz_sum\": %.17g, "
+	         "\"xchg_rank_max\": %d}\n",
+	         rk.rank, rk.nranks, rk.device, !rk.multi() ? "none" : rk.host ? "host" : "rccl",
+	         rk.shard == VBFM_SHARD_ROWS ? "rows" : "features", job.method.c_str(), lo, hi,
+	         (unsigned long long)tr.csc.nnz, tr.csc.num_feature, tlo, thi, (unsigned long long)te.csc.nnz,
+	         xchg ? xs[0] : -1.0, xchg ? xs[1] : -1.0, xchg ? (int)xm : -1);
+	fputs(line, stdout);
+	fflush(stdout);
+}
+
+// one rank of the run. Returns the process exit status of a rank (0 ok).
+static int run_rank(const Job &job, Data &train, Data &test, Rank &rk)
+{
+	try {
+		if (job.plan) { print_plan(job, train, test, rk); return 0; }
+		if (rk.device < 0) {   // -devices N -transport host: rank r on device r % visible
+			int32_t n = 0;
+			check(vbfm_device_count(&n), nullptr);
+			if (n <= 0) throw std::string("no HIP device available");
+			rk.device = rk.rank % n;
+		}
+		if (job.method == "vb_online") run_online(job.online, train, test, rk);
+		else if (job.method == "vb") run_vb(job.vb, train, test, rk);
+		else run_mcmc(job.mc, train, test, rk);
+		return 0;
+	} catch (std::string &e) {
+		std::cerr << std::endl << "ERROR: " << (rk.multi() ? "rank " + std::to_string(rk.rank) + ": " : "") << e
+		          << std::endl;
+	} catch (char const *e) {
+		std::cerr << std::endl << "ERROR: " << (rk.multi() ? "rank " + std::to_string(rk.rank) + ": " : "") << e
+		          << std::endl;
+	}
+	return 1;
+}
+
+// Fork one process per rank (no HIP call has happened in this process), wait for them, kill the
+// others when one fails (a rank left waiting at a barrier or inside a collective would never
+// return). The shared page is mapped before the fork, so every rank sees the same one.
+static int launch(const Job &job, Data &train, Data &test, Rank proto, const std::vector<int32_t> &ordinals)
+{
+	const int P = proto.nranks;
+	const size_t slot = (size_t)4 << 20;   // 4 MB per rank and exchange chunk
+	const size_t hdr = (sizeof(ShmHeader) + 4095) / 4096 * 4096;
+	const size_t bytes = hdr + (size_t)P * slot + (size_t)test.h.num_rows * sizeof(double) + 4096;
+	void *mem = mmap(nullptr, bytes, PROT_READ | PROT_WRITE, MAP_SHARED | MAP_ANONYMOUS, -1, 0);
+	if (mem == MAP_FAILED) throw std::string("cannot map the ranks' shared page");
+	ShmHeader *shm = (ShmHeader *)mem;
+	pthread_barrierattr_t at;
+	pthread_barrierattr_init(&at);
+	pthread_barrierattr_setpshared(&at, PTHREAD_PROCESS_SHARED);
+	if (pthread_barrier_init(&shm->bar, &at, (unsigned)P) != 0) throw std::string("cannot create the ranks' barrier");
+	pthread_barrierattr_destroy(&at);
+	shm->slot_bytes = slot;
+	shm->nranks = P;
+	proto.shm = shm;
+	proto.slots = (char *)mem + hdr;
+	proto.test_pred = (double *)(proto.slots + (size_t)P * slot);
+	std::cout.flush();
+	fflush(stdout);
+	fflush(stderr);
+	std::vector<pid_t> pids;
+	for (int r = 0; r < P; r++) {
+		const pid_t pid = fork();
+		if (pid < 0) {
+			for (pid_t q : pids) kill(q, SIGKILL);
+			throw std::string("fork failed");
+		}
+		if (pid == 0) {
+			Rank rk = proto;
+			rk.rank = r;
+			rk.device = ordinals.empty() ? (proto.host ? -1 : r) : ordinals[r];
+			if (!rk.lead() && !job.plan) std::cout.setstate(std::ios::badbit);   // rank 0 speaks for the job
+			const int rc = run_rank(job, train, test, rk);
+			std::cout.flush();
+			fflush(stdout);
+			fflush(stderr);
+			_exit(rc);
+		}
+		pids.push_back(pid);
+	}
+	int failed = -1, status_failed = 0;
+	size_t left = pids.size();
+	while (left > 0) {
+		int status = 0;
+		const pid_t pid = waitpid(-1, &status, 0);
+		if (pid < 0) break;
+		const auto it = std::find(pids.begin(), pids.end(), pid);
+		if (it == pids.end()) continue;
+		left--;
+		const bool ok = WIFEXITED(status) && WEXITSTATUS(status) == 0;
+		if (!ok && failed < 0) {
+			failed = (int)(it - pids.begin());
+			status_failed = status;
+			for (pid_t q : pids)
+				if (q != pid) kill(q, SIGKILL);
+		}
+		*it = -1;
+	}
+	pthread_barrier_destroy(&shm->bar);
+	munmap(mem, bytes);
+	if (failed >= 0) {
+		std::ostringstream m;
+		m << "rank " << failed << " of " << P << " failed ("
+		  << (WIFSIGNALED(status_failed) ? "signal " + std::to_string(WTERMSIG(status_failed))
+		                                 : "exit status " + std::to_string(WEXITSTATUS(status_failed)))
+		  << "); the other ranks were stopped";
+		throw m.str();
+	}
+	return 0;
+}
+
+int main(int argc, char **argv)
+{
 	try {
 		CmdLine cmd(argc, argv);
 		std::cout << "----------------------------------------------------------------------------" << std::endl;
 		std::cout << "libFM (VB learner on MI355X, libvbfm ABI " << vbfm_abi_version() << ")" << std::endl;
 		std::cout << "  Version: 1.4.2 (reference CLI surface)" << std::endl;
 		std::cout << "----------------------------------------------------------------------------" << std::endl;
+		if (vbfm_abi_version() != VBFM_ABI_VERSION)
+			throw std::string("libvbfm.so ABI " + std::to_string(vbfm_abi_version()) + " but this libFM was built for ABI " +
+			                  std::to_string(VBFM_ABI_VERSION));
 		const std::string p_task = cmd.reg("task", "r=regression, c=binary classification [MANDATORY]");
 		const std::string p_meta = cmd.reg("meta", "filename for meta information about data set");
 		const std::string p_train = cmd.reg("train", "filename for training data [MANDATORY]");
@@ -418,9 +852,13 @@ int main(int argc, char **argv)
 		const std::string p_rel = cmd.reg("relation", "BS: filenames for the relations, default=''");
 		cmd.reg("cache_size", "cache size for data storage (only applicable if data is in binary format), default=infty");
 		const std::string p_batch = cmd.reg("batch", "How many batches for online algorithm");
-		const std::string p_dev = cmd.reg("device", "HIP device ordinal; default=0");
+		const std::string p_dev = cmd.reg("device", "HIP device ordinal of a one-GPU run; default=0");
+		const std::string p_devs = cmd.reg("devices", "GPUs: a count N (ranks on ordinals 0..N-1) or a list 'o0,o1,...' of ordinals, one rank each; default=1");
+		const std::string p_shard = cmd.reg("shard", "partition over the ranks: rows (exact, default) or features (the columns of every level; Jacobi across ranks, vb only)");
+		const std::string p_trans = cmd.reg("transport", "rank exchange: rccl (one GPU per rank, default) or host (shared memory; ranks may share a GPU)");
+		const std::string p_plan = cmd.reg("plan", "1: every rank prints its launch and shard plan as JSON and exits (no GPU)");
 		const std::string p_vfile = cmd.reg("vfile", "write v_file.txt like the reference (1) or not (0); default=1");
-		const std::string p_save = cmd.reg("save_state", "vb: write the learner's state to this file after the last iteration");
+		const std::string p_save = cmd.reg("save_state", "vb: write the learner's state to this file after the last iteration (.<rank> per rank with -devices)");
 		const std::string p_resume = cmd.reg("resume", "vb: continue from a -save_state file (same data and -dim) instead of the initial draws");
 		if (cmd.has(p_help) || argc == 1) { cmd.print_help(); return 0; }
 		cmd.check();
@@ -432,10 +870,43 @@ int main(int argc, char **argv)
 		if (cmd.get(p_task) != "r") throw std::string("unknown task");   // regression only
 		if (!cmd.list(p_rel).empty()) throw std::string("-relation is not supported by this build");
 
+		// the ranks: -devices N | o0,o1,..., -shard, -transport (checked before the data load)
+		Rank proto;
+		std::vector<int32_t> ordinals;
+		{
+			const std::vector<std::string> devs = cmd.list(p_devs);
+			if (devs.size() > 1) {
+				for (const std::string &d : devs) ordinals.push_back((int32_t)atoi(d.c_str()));
+				proto.nranks = (int32_t)ordinals.size();
+			} else if (devs.size() == 1) {
+				proto.nranks = (int32_t)atoi(devs[0].c_str());
+			}
+			if (proto.nranks < 1 || proto.nranks > 256) throw std::string("-devices: expected a rank count 1..256 or a list of ordinals");
+			for (int32_t o : ordinals)
+				if (o < 0) throw std::string("-devices: negative ordinal");
+			const std::string tr = cmd.get(p_trans, "rccl"), sh = cmd.get(p_shard, "rows");
+			if (tr != "rccl" && tr != "host") throw std::string("-transport: rccl or host");
+			if (sh != "rows" && sh != "features") throw std::string("-shard: rows or features");
+			proto.host = tr == "host";
+			proto.shard = sh == "rows" ? VBFM_SHARD_ROWS : VBFM_SHARD_FEATURES;
+			if (proto.shard == VBFM_SHARD_FEATURES && method != "vb")
+				throw std::string("-shard features is a -method vb mode");
+			if (proto.nranks > 1 && method == "vb_online") throw std::string("-method vb_online runs on one GPU (-devices 1)");
+			if (!proto.host && !ordinals.empty()) {
+				std::vector<int32_t> o = ordinals;
+				std::sort(o.begin(), o.end());
+				if (std::adjacent_find(o.begin(), o.end()) != o.end())
+					throw std::string("-devices: RCCL needs one GPU per rank (-transport host lets ranks share one)");
+			}
+			proto.device = proto.nranks == 1 ? (ordinals.empty() ? (int32_t)cmd.geti(p_dev, 0) : ordinals[0]) : 0;
+		}
+
 		Data train, test;
 		load(cmd.get(p_train), train, "train");
 		load(cmd.get(p_test), test, "test");
 		if (cmd.geti(p_verb, 0) > 0) std::cout << "seed=" << seed << std::endl;
+		if (proto.row_shards() && train.h.num_rows < (uint32_t)proto.nranks)
+			throw std::string("-devices: fewer train rows than ranks");
 
 		// libfm.cpp:215-256: attributes and groups. For vb_online the train file is only scanned
 		// (find_max_feature, libfm.cpp:167-170, 528-600), which leaves the largest feature ids in
@@ -462,132 +933,31 @@ int main(int argc, char **argv)
 		const int k0 = atoi(dim[0].c_str()) != 0, k1 = atoi(dim[1].c_str()) != 0, k = atoi(dim[2].c_str());
 		const double init_stdev = cmd.getd(p_init, 0.1);
 		const uint32_t num_iter = (uint32_t)cmd.geti(p_iter, 100);
+		const uint32_t *gp = cmd.has(p_meta) ? groups.data() : nullptr;
+		const bool vfile = cmd.geti(p_vfile, 1) != 0;
+		const std::string rlog = cmd.has(p_rlog) ? cmd.get(p_rlog) : std::string();
+		const std::string out = cmd.has(p_out) ? cmd.get(p_out) : std::string();
 
-		if (method == "vb_online") {
-			OnlineRun run{seed, init_stdev, num_iter, (uint32_t)cmd.geti(p_batch, 50), cmd.has(p_meta) ? groups.data() : nullptr,
-			              G, D, k0, k1, k, (int32_t)cmd.geti(p_dev, 0), cmd.geti(p_vfile, 1) != 0,
-			              cmd.has(p_rlog) ? cmd.get(p_rlog) : std::string(), cmd.has(p_out) ? cmd.get(p_out) : std::string()};
-			run_online(run, train, test);
+		Job job;
+		job.method = method;
+		job.plan = cmd.geti(p_plan, 0) != 0;
+		job.online = OnlineRun{seed, init_stdev, num_iter, (uint32_t)cmd.geti(p_batch, 50), gp, G, D, k0, k1, k, vfile,
+		                       rlog, out};
+		std::vector<double> reg;
+		for (const std::string &r : cmd.list(p_reg)) reg.push_back(atof(r.c_str()));
+		job.mc = McmcRun{method == "mcmc", seed, init_stdev, num_iter, reg, gp, G, D, k0, k1, k, vfile, rlog, out};
+		job.vb = VbRun{seed, init_stdev, num_iter, gp, G, D, k0, k1, k, vfile, rlog, out,
+		               cmd.has(p_save) ? cmd.get(p_save) : std::string(), cmd.has(p_resume) ? cmd.get(p_resume) : std::string()};
+
+		if (proto.nranks == 1) {   // one GPU, this process
+			run_rank(job, train, test, proto);
 			return 0;
 		}
-		if (method != "vb") {
-			std::vector<double> reg;
-			for (const std::string &r : cmd.list(p_reg)) reg.push_back(atof(r.c_str()));
-			McmcRun run{method == "mcmc", seed, init_stdev, num_iter, reg, cmd.has(p_meta) ? groups.data() : nullptr,
-			            G, D, k0, k1, k, (int32_t)cmd.geti(p_dev, 0), cmd.geti(p_vfile, 1) != 0,
-			            cmd.has(p_rlog) ? cmd.get(p_rlog) : std::string(), cmd.has(p_out) ? cmd.get(p_out) : std::string()};
-			run_mcmc(run, train, test);
-			return 0;
-		}
-
-		vbfm_config cfg{k0, k1, k, D, G, cmd.has(p_meta) ? groups.data() : nullptr, train.h.min_target,
-		                train.h.max_target, (int32_t)cmd.geti(p_dev, 0), 0};
-		check(vbfm_create(&ctx, &cfg), nullptr);
-		const vbfm_csc tr = train.csc(), te = test.csc();
-		check(vbfm_set_train(ctx, &tr), ctx);
-		check(vbfm_set_test(ctx, &te), ctx);
-
-		// fm.init + fm.w.init_normal + fml->init draws (libfm.cpp:123-366): the same stream on
-		// the host (small models) or generated on the device (VBFM_INIT=host|replay overrides).
-		// -resume takes the state from its file instead (no draws, no v_file.txt)
-		const bool resume = cmd.has(p_resume);
-		const size_t kd = (size_t)k * D;
-		const bool vfile = cmd.geti(p_vfile, 1) != 0 && !resume;
-		const char *init_env = getenv("VBFM_INIT");
-		const bool replay = init_env ? std::string(init_env) == "replay" : kd + D >= 2000000;
-		std::vector<double> fm_v(vfile || (!replay && !resume) ? kd : 0);
-		if (replay && !resume) {
-			check(vbfm_init_params_replay(ctx, seed, init_stdev, vfile ? fm_v.data() : nullptr, nullptr), ctx);
-		} else if (!resume) {
-			std::vector<double> mu_w(D), sig_w(D), mu_v(kd), sig_v(kd), hw(G), hv((size_t)G * k);
-			vbfm_params p{mu_w.data(), sig_w.data(), mu_v.data(), sig_v.data(), hw.data(), hv.data(), 0, 0, 0, 0};
-			check(vbfm_init_params_host(seed, init_stdev, k, D, G, &p, fm_v.data(), nullptr), nullptr);
-			check(vbfm_set_params(ctx, &p), ctx);
-		}
-		if (vfile) write_vfile(fm_v, k, D);
-		fm_v.clear();
-		fm_v.shrink_to_fit();
-
-		// -rlog (libfm.cpp:353-363; fields of fm_learn::init and fm_learn_vb::init)
-		std::ofstream *rlog_out = nullptr;
-		RLog *rlog = nullptr;
-		if (cmd.has(p_rlog)) {
-			rlog_out = new std::ofstream(cmd.get(p_rlog).c_str());
-			if (!rlog_out->is_open()) throw std::string("Unable to open file " + cmd.get(p_rlog));
-			std::cout << "logging to " << cmd.get(p_rlog) << std::endl;
-			rlog = new RLog(rlog_out);
-			for (const char *f : {"rmse", "mae", "time_pred", "time_learn", "time_learn2", "time_learn4", "alpha",
-			                      "rmse_mcmc_this", "rmse_mcmc_all"})
-				rlog->add(f);
-			for (uint32_t g = 0; g < G; g++) {
-				std::ostringstream ss;
-				ss << "wmu[" << g << "]"; rlog->add(ss.str()); ss.str("");
-				ss << "wlambda[" << g << "]"; rlog->add(ss.str()); ss.str("");
-				for (int f = 0; f < k; f++) {
-					ss << "vmu[" << g << "," << f << "]"; rlog->add(ss.str()); ss.str("");
-					ss << "vlambda[" << g << "," << f << "]"; rlog->add(ss.str()); ss.str("");
-				}
-			}
-			rlog->init();
-		}
-
-		// fm_learn_vb_simultaneous::_learn
-		uint32_t it0 = 0;
-		if (resume) {
-			check(vbfm_load_state(ctx, cmd.get(p_resume).c_str(), &it0), ctx);
-			std::cout << "resuming from " << cmd.get(p_resume) << " after " << it0 << " iterations" << std::endl;
-		} else {
-			check(vbfm_init_caches(ctx), ctx);
-		}
-		std::ostringstream tag;
-		tag << k0 << k1 << k;
-		const std::string f_rmse = "test_rmse_" + tag.str() + "_vb", f_fe = "free_energy_" + tag.str() + "_vb";
-		if (!resume) { std::ofstream a(f_rmse.c_str()); std::ofstream b(f_fe.c_str()); }   // truncate (:58-73); a resumed run appends
-		for (uint32_t it = it0; it < it0 + num_iter; it++) {
-			time_t now = time(0);
-			std::cout << ctime(&now) << std::endl;
-			const double t_user = usertime();
-			const clock_t t_clock = clock();
-			const double t_wall = (double)time(NULL);
-			vbfm_iter_stats st;
-			check(vbfm_iterate(ctx, &st), ctx);
-			if (st.free_energy_valid) {   // fm_learn_vb.h:678-680
-				std::ofstream fe(f_fe.c_str(), std::ios_base::app);
-				fe << -st.free_energy << "\n";
-				std::cout << "free energy " << st.free_energy << std::endl;
-			}
-			nan_reports(st.nan_alpha, st.inf_alpha, st.nan_mu_w, st.inf_mu_w, st.nan_sigma_w, st.nan_mu_v, st.inf_mu_v,
-			            st.nan_sigma_v);
-			if (rlog) {
-				rlog->log("time_learn", usertime() - t_user);
-				rlog->log("time_learn2", (double)(clock() - t_clock) / CLOCKS_PER_SEC);
-				rlog->log("time_learn4", (double)time(NULL) - t_wall);
-				rlog->log("rmse_mcmc_this", st.rmse);
-				rlog->newline();
-			}
-			std::ofstream fr(f_rmse.c_str(), std::ios_base::app);
-			fr << st.rmse << "\n";
-			std::cout << "#Iter=" << std::setw(3) << it << "\tTrain=" << st.train_quirk << "\tTest=" << st.rmse << std::endl;
-		}
-		if (cmd.has(p_save)) check(vbfm_save_state(ctx, cmd.get(p_save).c_str(), it0 + num_iter), ctx);
-		// libfm.cpp:509-511: fm_learn_vb::evaluate returns NaN
-		std::cout << "Final\tTrain=" << NAN << "\tTest=" << NAN << std::endl;
-		if (cmd.has(p_out)) {   // libfm.cpp:514-519, DVector::save (matrix.h:284-295)
-			std::vector<double> pred(test.h.num_rows);
-			check(vbfm_get_test_pred(ctx, pred.data()), ctx);
-			std::ofstream o(cmd.get(p_out).c_str());
-			for (double v : pred) o << v << std::endl;
-		}
-		delete rlog;
-		delete rlog_out;
-		vbfm_destroy(ctx);
-		ctx = nullptr;
+		launch(job, train, test, proto, ordinals);
 	} catch (std::string &e) {
 		std::cerr << std::endl << "ERROR: " << e << std::endl;   // libfm.cpp:521-525 (exit code 0 there too)
-		if (ctx) vbfm_destroy(ctx);
 	} catch (char const *e) {
 		std::cerr << std::endl << "ERROR: " << e << std::endl;
-		if (ctx) vbfm_destroy(ctx);
 	}
 	return 0;
 }

@@ -30,6 +30,7 @@ P_u32, P_u64, P_f32, P_f64, P_u8 = (C.POINTER(C.c_uint32), C.POINTER(C.c_uint64)
                                     C.POINTER(C.c_double), C.POINTER(C.c_uint8))
 
 
+ABI_VERSION = 2        # VBFM_ABI_VERSION of include/vbfm.h this binding is written for
 LAYOUTS = {"auto": 0, "column": 1, "level": 2, "entry": 3}   # VBFM_LAYOUT_* (include/vbfm.h)
 SYNTH_MODEL_SEED = 7   # tests/synth.py MODEL_SEED: the planted model shared by train, test and all shards
 
@@ -143,7 +144,8 @@ class HostData(C.Structure):
 EXPORTS = ["vbfm_abi_version", "vbfm_last_error", "vbfm_create", "vbfm_destroy", "vbfm_set_train",
            "vbfm_set_test", "vbfm_synth_generate", "vbfm_synth_multihot", "vbfm_get_csc", "vbfm_get_shape", "vbfm_get_levels",
            "vbfm_set_params", "vbfm_get_params", "vbfm_init_params_device", "vbfm_init_params_replay", "vbfm_init_caches", "vbfm_iterate", "vbfm_get_test_pred",
-           "vbfm_step_w0", "vbfm_step_w", "vbfm_step_qcache", "vbfm_step_v", "vbfm_step_hyper",
+           "vbfm_step_w0", "vbfm_step_w", "vbfm_step_qcache", "vbfm_step_v", "vbfm_step_w_level",
+           "vbfm_step_v_level", "vbfm_step_hyper", "vbfm_device_count",
            "vbfm_free_energy", "vbfm_get_rows", "vbfm_get_test_e", "vbfm_factor_sweep", "vbfm_set_profiling",
            "vbfm_set_layout", "vbfm_get_layout", "vbfm_set_shard_mode",
            "vbfm_comm_unique_id", "vbfm_comm_init", "vbfm_comm_init_host", "vbfm_comm_info", "vbfm_load_data", "vbfm_free_host_data", "vbfm_save_data",
@@ -165,6 +167,9 @@ def lib():
         if not os.path.exists(LIB_PATH):
             raise VbfmError("libvbfm.so not built (expected %s); run `make -C %s`" % (LIB_PATH, _PKG))
         L = C.CDLL(LIB_PATH)
+        if L.vbfm_abi_version() != ABI_VERSION:   # struct layouts / argument lists differ otherwise
+            raise VbfmError("libvbfm.so has ABI %d, this binding expects %d (rebuild: make -C %s)" % (
+                L.vbfm_abi_version(), ABI_VERSION, _PKG))
         V = C.c_void_p
         L.vbfm_last_error.argtypes = [V]
         L.vbfm_last_error.restype = C.c_char_p
@@ -191,6 +196,9 @@ def lib():
             getattr(L, fn).argtypes = [V]
         L.vbfm_step_qcache.argtypes = [V, C.c_int32]
         L.vbfm_step_v.argtypes = [V, C.c_int32]
+        L.vbfm_step_w_level.argtypes = [V, C.c_int32]
+        L.vbfm_step_v_level.argtypes = [V, C.c_int32, C.c_int32]
+        L.vbfm_device_count.argtypes = [C.POINTER(C.c_int32)]
         L.vbfm_step_hyper.argtypes = [V, C.POINTER(C.c_int32)]
         L.vbfm_free_energy.argtypes = [V, P_f64]
         L.vbfm_get_rows.argtypes = [V, P_f64, P_f64, P_f64, P_f64, P_f64]
@@ -511,6 +519,14 @@ class FMLearnVB:
 
     def step_v(self, f):
         _check(lib().vbfm_step_v(self._ctx, f), self._ctx)
+
+    def step_w_level(self, level):
+        """Level `level` (0-based, in order) of the w sweep (vbfm_step_w_level)."""
+        _check(lib().vbfm_step_w_level(self._ctx, level), self._ctx)
+
+    def step_v_level(self, f, level):
+        """Level `level` (0-based, in order) of factor f's v sweep (vbfm_step_v_level)."""
+        _check(lib().vbfm_step_v_level(self._ctx, f, level), self._ctx)
 
     def step_hyper(self):
         e = C.c_int32()

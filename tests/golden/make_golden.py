@@ -149,6 +149,19 @@ def online_cases(ref):
     shutil.rmtree(tmp)
 
 
+def levels_cases(ref):
+    """update_all's sweeps one dependency level at a time (ref_driver levels): caches and
+    parameters after every level of the w sweep and of every factor's v sweep."""
+    for case in ("tiny", "tiny_dup"):
+        d = os.path.join(HERE, case)
+        tr, te = os.path.join(d, "train.libfm"), os.path.join(d, "test.libfm")
+        out, arr = run_ref(ref, "levels", tr, te, "1,1,3", 1, 5)
+        nums, _ = parse_vb(out)
+        L = int(re.search(r"^LEVELS (\d+)$", out, re.M).group(1))
+        keep = {k: arr[k] for k in arr if k.startswith("l_") or k == "levels" or k.startswith("init_")}
+        save_case(case + "/levels", nums, [], keep, {"dim": "1,1,3", "seed": 5, "init_stdev": 0.1, "num_levels": L})
+
+
 def save_case(name, nums, trace, arrays, meta):
     d = os.path.join(HERE, name)
     os.makedirs(d, exist_ok=True)
@@ -251,7 +264,7 @@ def mcmc_cases(ref):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--ref", default=os.path.join(HERE, "..", "..", "oracle", "_ref", "ref_driver"))
-    ap.add_argument("--only", default="", help="comma list of groups: rng,tiny,meta,synth,sa,mcmc,online")
+    ap.add_argument("--only", default="", help="comma list of groups: rng,tiny,meta,synth,sa,mcmc,online,levels")
     args = ap.parse_args()
     ref = os.path.abspath(args.ref)
     only = set(filter(None, args.only.split(",")))
@@ -259,11 +272,13 @@ def main():
     def want(group):
         return not only or group in only
 
+    if want("levels"):
+        levels_cases(ref)
     if want("mcmc"):
         mcmc_cases(ref)
     if want("online"):
         online_cases(ref)
-    if only and not only - {"mcmc", "online"}:
+    if only and not only - {"mcmc", "online", "levels"}:
         return
 
     # --- RNG known answers: glibc rand() as the reference calls it (random.h:174-176)

@@ -135,3 +135,52 @@ def test_cli_save_state_and_resume(tmp_path):
     it_one = re.findall(r"#Iter=\s*(\d+)\tTrain=(\S+)\tTest=(\S+)", s_one)
     it_two = re.findall(r"#Iter=\s*(\d+)\tTrain=(\S+)\tTest=(\S+)", s_two)
     assert it_two == it_one[3:]
+
+
+def test_load_refuses_truncated_file_and_other_layout_without_touching_state(tmp_path):
+    """A truncated checkpoint is refused before anything is replaced (the context then runs on
+    exactly as if the load had not been tried); a checkpoint of the level-ordered store is
+    refused by a column-layout context (the data-set sums would add the rows in another order)."""
+    tr, te, nf = _data(n=5000)
+    g = _learner(tr, te, nf, 3, "level")
+    g.init_caches()
+    g.iterate()
+    path = str(tmp_path / "vb.state")
+    g.save_state(path)
+    assert not os.path.exists(path + ".tmp")
+    g.close()
+    raw = open(path, "rb").read()
+    cut = tmp_path / "cut.state"
+    cut.write_bytes(raw[:-64])
+    ref = _learner(tr, te, nf, 3, "level")
+    ref.init_caches()
+    want = _trace([ref.iterate()])
+    ref.close()
+    h = _learner(tr, te, nf, 3, "level")
+    h.init_caches()
+    with pytest.raises(vbfm.VbfmError, match="truncated"):
+        h.load_state(str(cut))
+    assert _trace([h.iterate()]) == want
+    h.close()
+    h = _learner(tr, te, nf, 3, "column")
+    with pytest.raises(vbfm.VbfmError, match="another row layout"):
+        h.load_state(path)
+    h.close()
+
+
+def test_failed_save_keeps_the_previous_checkpoint(tmp_path):
+    """The file is written beside the target and renamed over it: a save that cannot be
+    written (here: the temporary name is a directory) leaves the old checkpoint intact."""
+    tr, te, nf = _data(n=5000)
+    g = _learner(tr, te, nf, 3, "auto")
+    g.init_caches()
+    g.iterate()
+    path = str(tmp_path / "vb.state")
+    g.save_state(path)
+    before = open(path, "rb").read()
+    os.mkdir(path + ".tmp")
+    g.iterate()
+    with pytest.raises(vbfm.VbfmError, match="cannot open checkpoint file"):
+        g.save_state(path)
+    assert open(path, "rb").read() == before
+    g.close()

@@ -86,6 +86,32 @@ def test_vb_steps_bit_exact(case):
         np.testing.assert_array_equal(p["sigma_v"], a["s4_f%d_v_sigma_v" % f])
 
 
+@pytest.mark.parametrize("case", ["tiny", "tiny_dup"])
+def test_level_by_level_sweep_ends_at_the_ascending_sweep(case):
+    """The reference's update_w / update_v called one dependency level at a time (ref_driver
+    levels, tests/golden/<case>/levels) end each sweep exactly where the ascending sweep
+    (steps) ends, bit for bit -- the exactness argument of the level schedule
+    checked on the reference's own code -- and the levels are the schedule's definition
+    (tests/shards.py) on the loaded rows."""
+    import shards
+    t, a = load_case(case + "/levels")
+    _, s = load_case(case + "/steps")
+    L = t["meta"]["num_levels"]
+    k = int(t["meta"]["dim"].split(",")[2])
+    tr, _ = _tiny(case)
+    rp, rf, _, _ = tr.csr()
+    np.testing.assert_array_equal(a["levels"], shards.levels(rp, rf, tr.num_feature))
+    for key in ("e", "t"):
+        np.testing.assert_array_equal(a["l_w_l%d_%s" % (L - 1, key)], s["s2_w_" + key])
+    for f in range(k):
+        for key in ("e", "t", "q", "tq", "tz"):
+            np.testing.assert_array_equal(a["l_f%d_l%d_%s" % (f, L - 1, key)], s["s4_f%d_v_%s" % (f, key)])
+        for key in ("mu_v", "sigma_v"):
+            np.testing.assert_array_equal(a["l_f%d_l%d_%s" % (f, L - 1, key)], s["s4_f%d_v_%s" % (f, key)])
+    # intermediate levels are genuinely intermediate (each level changes the caches)
+    assert not np.array_equal(a["l_f0_l0_e"], a["l_f0_l%d_e" % (L - 1)])
+
+
 def _run_vb_trace(case, tr, te, attr_group=None):
     t, a = load_case(case)
     m = t["meta"]
