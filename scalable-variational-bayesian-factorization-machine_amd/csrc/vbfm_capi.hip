@@ -50,6 +50,41 @@ void allreduce_dev(vbfm_ctx *c, void *buf, size_t n, ncclDataType_t t, ncclRedOp
 	sync(c);
 }
 
+uint32_t ar_chunks(vbfm_ctx *c, uint32_t nfeat)
+{
+	if (!c->row_comm()) return 1;
+	static const int env = [] {
+		const char *e = getenv("VBFM_AR_CHUNKS");
+		return e ? atoi(e) : 4;
+	}();
+	// at least 2048 columns per chunk: a smaller launch leaves the chip idle at its tail
+	const uint32_t C = std::min<uint32_t>((uint32_t)std::max(env, 1), nfeat / 2048);
+	return std::max<uint32_t>(1, std::min<uint32_t>(C, vbfm_ctx::AR_MAX_CHUNKS));
+}
+
+void allreduce_chunk(vbfm_ctx *c, double2 *buf, size_t n, uint32_t i)
+{
+	if (!c->comm) {   // the host exchange is synchronous: nothing to overlap
+		allreduce_dev(c, buf, n, ncclDouble, ncclSum);
+		return;
+	}
+	if (!c->s_comm) {
+		HIPCHK(hipStreamCreateWithFlags(&c->s_comm, hipStreamNonBlocking));
+		for (auto &e : c->ev_ar) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+		HIPCHK(hipEventCreateWithFlags(&c->ev_arj, hipEventDisableTiming));
+	}
+	HIPCHK(hipEventRecord(c->ev_ar[i], c->s));
+	HIPCHK(hipStreamWaitEvent(c->s_comm, c->ev_ar[i], 0));
+	NCCLCHK(ncclAllReduce(buf, buf, n, ncclDouble, ncclSum, c->comm, c->s_comm));
+}
+
+void allreduce_join(vbfm_ctx *c)
+{
+	if (!c->comm || !c->s_comm) return;
+	HIPCHK(hipEventRecord(c->ev_arj, c->s_comm));
+	HIPCHK(hipStreamWaitEvent(c->s, c->ev_arj, 0));
+}
+
 // all-reduce a few host doubles across the row shards (identity with one rank)
 void allreduce_host(vbfm_ctx *c, double *v, int n)
 {
@@ -797,9 +832,7 @@ void sweep_level(vbfm_ctx *c, uint32_t l, bool is_w, int f)
 			a.pending = (l > 0 || carried) ? 1 : 0;
 			if (c->tr.n > 50000000u) a.pending |= 2;     // non-temporal record loads (large shards)
 			a.first_prev = l == 1;
-			HIPCHK(vbk::lord_defer_level(a, is_w, c->s));
-			if (c->row_comm())
-				allreduce_dev(c, c->stats, 2 * (size_t)a.nfeat, ncclDouble, ncclSum);
+			stats_exchange(c, a, [&](const LevelArgs &b) { HIPCHK(vbk::lord_defer_level(b, is_w, c->s)); });
 			HIPCHK(vbk::lord_defer_post(a, is_w, c->s));
 			if (l + 1 == nlevels(c)) {
 				// the sweep's last correction: left to level 0 of the next sweep when one follows
@@ -815,9 +848,7 @@ void sweep_level(vbfm_ctx *c, uint32_t l, bool is_w, int f)
 				}
 			}
 		} else {
-			HIPCHK(vbk::lord_level_stats(a, is_w, c->s));
-			if (c->row_comm())
-				allreduce_dev(c, c->stats, 2 * (size_t)a.nfeat, ncclDouble, ncclSum);
+			stats_exchange(c, a, [&](const LevelArgs &b) { HIPCHK(vbk::lord_level_stats(b, is_w, c->s)); });
 			HIPCHK(vbk::lord_level_move(a, is_w, c->s));
 		}
 		std::swap(c->rows, c->rows_alt);
@@ -838,9 +869,9 @@ void sweep_level(vbfm_ctx *c, uint32_t l, bool is_w, int f)
 	}
 	// row-sharded form: per-feature sufficient statistics of this shard's rows, summed over
 	// the shards, then every shard applies the identical posterior to its own rows
-	HIPCHK(is_w ? vbk::w_level_stats(a, c->s) : vbk::v_level_stats(a, c->s));
-	if (c->row_comm())
-		allreduce_dev(c, c->stats, 2 * (size_t)a.nfeat, ncclDouble, ncclSum);
+	stats_exchange(c, a, [&](const LevelArgs &b) {
+		HIPCHK(is_w ? vbk::w_level_stats(b, c->s) : vbk::v_level_stats(b, c->s));
+	});
 	HIPCHK(is_w ? vbk::w_level_correct(a, c->s) : vbk::v_level_correct(a, c->s));
 	prof_end(c, p);
 }
@@ -1168,6 +1199,10 @@ void vbfm_destroy(vbfm_ctx *c)
 	mc_free(c);
 	ov_free(c);
 	if (c->comm) ncclCommDestroy(c->comm);
+	for (hipEvent_t e : c->ev_ar)
+		if (e) (void)hipEventDestroy(e);
+	if (c->ev_arj) (void)hipEventDestroy(c->ev_arj);
+	if (c->s_comm) (void)hipStreamDestroy(c->s_comm);
 	for (hipEvent_t e : c->pev) (void)hipEventDestroy(e);
 	for (int i = 0; i < EV_N; i++)
 		if (c->ev[i]) (void)hipEventDestroy(c->ev[i]);

@@ -86,6 +86,12 @@ struct vbfm_ctx {
 	int dev = 0;
 	hipStream_t s = nullptr;
 	hipStream_t s_test = nullptr;   // the test prediction, overlapping the hyper-parameter step
+	// row shards over RCCL: the per-level all-reduce of chunk i of a level's statistics runs on
+	// s_comm while chunk i+1 computes on s (stats_exchange); events order the two
+	hipStream_t s_comm = nullptr;
+	static constexpr int AR_MAX_CHUNKS = 8;
+	hipEvent_t ev_ar[AR_MAX_CHUNKS] = {};
+	hipEvent_t ev_arj = nullptr;
 	int k0 = 1, k1 = 1, k = 0;
 	uint32_t D = 0, G = 1;
 	std::vector<uint32_t> group_h, per_group;
@@ -221,6 +227,48 @@ void allreduce_host(vbfm_ctx *c, double *v, int n);
 // in-place all-reduce of a device buffer over the ranks (RCCL on c->s, or the host exchange)
 void allreduce_dev(vbfm_ctx *c, void *buf, size_t n, ncclDataType_t t, ncclRedOp_t op);
 double finish_sum(vbfm_ctx *c, uint32_t nblocks);
+// chunks the per-level exchange is cut into (1: one all-reduce after the level's statistics)
+uint32_t ar_chunks(vbfm_ctx *c, uint32_t nfeat);
+// in-place fp64 sum over the ranks of n doubles of chunk i (< ar_chunks) of a level, issued after
+// the work queued on c->s so far; RCCL: on s_comm, so that c->s can go on with the next chunk
+void allreduce_chunk(vbfm_ctx *c, double2 *buf, size_t n, uint32_t i);
+// c->s waits for every chunk's all-reduce issued since the last join
+void allreduce_join(vbfm_ctx *c);
+
+// chunk [c0, c1) of a level's features as a launch of its own (LevelArgs / McArgs): the
+// kernels index their columns, runs and statistics by the launch's feature index
+template <class A>
+A level_chunk(const A &a, uint32_t c0, uint32_t c1)
+{
+	A b = a;
+	b.nfeat = c1 - c0;
+	if (b.feat_contig) b.feat_base += c0;
+	else b.feats += c0;
+	if (b.lcp) b.lcp += c0;
+	b.stats += c0;
+	return b;
+}
+
+// a level's statistics kernel(s) and their all-reduce over the row shards: the level's columns
+// in ar_chunks() chunks, chunk i's all-reduce overlapping chunk i+1's kernel; every chunk sums
+// the same columns' entries as one launch would, so the results are bit-identical
+template <class A, class F>
+void stats_exchange(vbfm_ctx *c, const A &a, F launch)
+{
+	const uint32_t C = ar_chunks(c, a.nfeat);
+	if (C <= 1) {
+		launch(a);
+		if (c->row_comm()) allreduce_dev(c, a.stats, 2 * (size_t)a.nfeat, ncclDouble, ncclSum);
+		return;
+	}
+	for (uint32_t i = 0; i < C; i++) {
+		const uint32_t c0 = (uint32_t)((uint64_t)a.nfeat * i / C), c1 = (uint32_t)((uint64_t)a.nfeat * (i + 1) / C);
+		const A b = level_chunk(a, c0, c1);
+		launch(b);
+		allreduce_chunk(c, b.stats, 2 * (size_t)b.nfeat, i);
+	}
+	allreduce_join(c);
+}
 void require_train(vbfm_ctx *c);
 uint32_t nlevels(vbfm_ctx *c);
 constexpr size_t NO_SPAN = ~(size_t)0;   // prof_begin: this launch is not timed

@@ -343,18 +343,14 @@ void mc_sweep(vbfm_ctx *c, bool is_w, int f)
 				a.lpay2 = c->lpay2;
 				a.tab = c->post_tab;
 				a.pending = l > 0 ? 3 : 0;
-				HIPCHK(vbk::mc_lord_defer_level(a, is_w, c->s));
-				if (c->row_comm())
-					allreduce_dev(c, c->stats, 2 * (size_t)a.nfeat, ncclDouble, ncclSum);
+				stats_exchange(c, a, [&](const McArgs &b) { HIPCHK(vbk::mc_lord_defer_level(b, is_w, c->s)); });
 				HIPCHK(vbk::mc_lord_defer_post(a, is_w, c->s));
 				if (l + 1 == nlevels(c)) {   // the sweep's last correction, on level-0-ordered records
 					a.dst = c->rows_alt;      // (swapped below)
 					HIPCHK(vbk::mc_lord_defer_flush(a, is_w, c->tr.n, c->s));
 				}
 			} else {
-				HIPCHK(vbk::mc_lord_level(a, 1, is_w, c->s));
-				if (c->row_comm())
-					allreduce_dev(c, c->stats, 2 * (size_t)a.nfeat, ncclDouble, ncclSum);
+				stats_exchange(c, a, [&](const McArgs &b) { HIPCHK(vbk::mc_lord_level(b, 1, is_w, c->s)); });
 				HIPCHK(vbk::mc_lord_level(a, 2, is_w, c->s));
 			}
 			std::swap(c->rows, c->rows_alt);
@@ -364,9 +360,9 @@ void mc_sweep(vbfm_ctx *c, bool is_w, int f)
 		if (!c->row_comm() && !c->force_split) {
 			HIPCHK(is_w ? vbk::mc_w_level(a, 0, c->s) : vbk::mc_v_level(a, 0, c->s));
 		} else {   // row-sharded: statistics of this shard, summed over shards, identical draws
-			HIPCHK(is_w ? vbk::mc_w_level(a, 1, c->s) : vbk::mc_v_level(a, 1, c->s));
-			if (c->row_comm())
-				allreduce_dev(c, c->stats, 2 * (size_t)a.nfeat, ncclDouble, ncclSum);
+			stats_exchange(c, a, [&](const McArgs &b) {
+				HIPCHK(is_w ? vbk::mc_w_level(b, 1, c->s) : vbk::mc_v_level(b, 1, c->s));
+			});
 			HIPCHK(is_w ? vbk::mc_w_level(a, 2, c->s) : vbk::mc_v_level(a, 2, c->s));
 		}
 		prof_end(c, p);

@@ -4,11 +4,13 @@
   skewed item popularity (long item columns take the segmented kernels), k = 20, three VB
   iterations against the oracle.
 * C3 (1e7 rows x 40 one-hot fields x 25,000 ids), k = 2, one VB iteration against the
-  oracle on the full data set (the oracle reads the device-generated data back).
-* C4 rows (1e8 x 40 x 125,000 ids), k = 2: two iterations on every kernel form the sizes
-  select -- level and column layouts, fused and deferred-split (row-shard) kernels -- agree
-  to summation order; the split form is the fused one bit for bit.
-* C5: the MCMC Gibbs sweep with device RNG streams at C4 rows, k = 2: the fused and the
+  oracle on the full data set (the oracle reads the device-generated data back); and at C3's
+  own k = 50, two iterations against the COMPILED REFERENCE's run on the same data
+  (tests/golden/c3_k50, made by tests/golden/make_c3_k50.py with oracle/_ref/ref_driver).
+* C4 (1e8 x 40 x 125,000 ids) at its own k = 100: two iterations on every kernel form the
+  sizes select -- level and column layouts, fused and deferred-split (row-shard) kernels --
+  agree to summation order; the split form is the fused one bit for bit; F finite, RMSE falls.
+* C5: the MCMC Gibbs sweep with device RNG streams at C4 size, k = 100: the fused and the
   row-shard split kernels draw the same chain bit for bit; ALS (no sampling) on the level
   and column layouts agrees to summation order.
 
@@ -126,7 +128,7 @@ def test_c3_full_size_one_iteration_vs_oracle():
         close(p[key], op[key])
 
 
-C4 = dict(n=100_000_000, F=40, S=125_000, k=2, n_test=1_000_000)
+C4 = dict(n=100_000_000, F=40, S=125_000, k=100, n_test=1_000_000)
 
 
 def _c4_vb(layout, split, defer=True):
@@ -150,7 +152,8 @@ def _c4_vb(layout, split, defer=True):
         os.environ.pop("VBFM_DEFER", None)
 
 
-def test_c4_rows_layouts_and_split_agree():
+def test_c4_k100_layouts_and_split_agree():
+    """C4 at the metric's own configuration (k = 100): the bench's data and init."""
     base = _c4_vb("level", "0")
     assert all(np.isfinite(base[0])) and base[1][1] < base[1][0]
     split = _c4_vb("level", "1")
@@ -180,7 +183,7 @@ def _c4_mc(method, layout, split):
         os.environ.pop("VBFM_FORCE_SPLIT", None)
 
 
-def test_c5_mcmc_device_rng_fused_equals_split():
+def test_c5_k100_mcmc_device_rng_fused_equals_split():
     a = _c4_mc("mcmc", "level", "0")
     b = _c4_mc("mcmc", "level", "1")
     assert all(np.isfinite(a[0]))
@@ -188,8 +191,61 @@ def test_c5_mcmc_device_rng_fused_equals_split():
     np.testing.assert_array_equal(a[2], b[2])
 
 
-def test_c5_als_layouts_agree():
+def test_c5_k100_als_layouts_agree():
     a = _c4_mc("als", "level", "0")
     b = _c4_mc("als", "column", "0")
     for x, y in zip(a, b):
         close(x, y, 1e-10)
+
+
+def _sampled(arr, idx):
+    return np.asarray(arr, dtype=np.float64)[np.asarray(idx, dtype=np.int64)]
+
+
+def test_c3_k50_two_iterations_vs_reference():
+    """C3 at its own k = 50 against the reference's fm_learn_vb compiled from its sources and
+    run on the same 1e7-row data set (tests/golden/c3_k50: per-iteration trace at 17 digits,
+    sums and 4096 sampled values of every final parameter array). The device
+    regenerates the data (bit-exact generator) and draws the reference's initial parameters
+    (glibc rand + Leva, seed 3); RMSE, MAE, the train quirk, F, alpha, mu_0', the parameter
+    sums and samples within 1e-9 relative (fm_learn_vb_simultaneous.h:125, 143-222)."""
+    t, a = load_case("c3_k50")
+    m, nums = t["meta"], t["nums"]
+    n, F, S, k = m["n_rows"], m["n_fields"], m["ids_per_field"], int(m["dim"].split(",")[2])
+    D = int(nums["D"])
+    g = vbfm.FMLearnVB(1, 1, k, D, min_target=nums["min_target"], max_target=nums["max_target"])
+    g.init_replay(m["ref_seed"], m["init_stdev"])
+    p0 = g.get_params()
+    for key, name in (("mu_w", "init_mu_w"), ("mu_v", "init_mu_v")):       # the draws: bit-exact
+        np.testing.assert_array_equal(_sampled(p0[key], a[name + "__idx"]), a[name])
+        assert float(np.sum(p0[key])) == t["array_sums"][name][0]
+    g.synth(0, n, F, S, m["seed"], m["xmode"], m["model_seed"])
+    g.synth(1, m["test_rows"], F, S, m["test_seed"], m["xmode"], m["model_seed"])
+    assert g.shape(0) == (n, F * S, n * F)
+    g.init_caches()
+    r = g.rows()
+    for key in ("e", "t"):
+        close(_sampled(r[key], a["init_%s__idx" % key]), a["init_" + key], 1e-12)
+    close(_sampled(g.test_e(), a["init_test_e__idx"]), a["init_test_e"], 1e-12)
+    del r
+    for it in range(m["iter"]):
+        st = g.iterate()
+        ref = t["trace"][it]
+        for got, key in ((st.rmse, "rmse"), (st.mae, "mae"), (st.train_quirk, "train"), (st.alpha, "alpha"),
+                         (st.mu_0_dash, "mu_0_dash"), (st.sigma_0_dash, "sigma_0_dash"),
+                         (st.free_energy, "free_energy")):
+            close([got], [ref[key]])
+        p = g.get_params()
+        close([np.sum(p["mu_w"] ** 2)], [ref["sq_mu_w"]])
+        close([np.sum(p["sigma_w"])], [ref["sum_sigma_w"]])
+        close([np.sum(p["mu_v"] ** 2)], [ref["sq_mu_v"]])
+        close([np.sum(p["sigma_v"])], [ref["sum_sigma_v"]])
+    p = g.get_params()
+    for key in ("mu_w", "sigma_w", "mu_v", "sigma_v", "hyp_sigma_w", "hyp_sigma_v"):
+        name = "final_" + key
+        vals = _sampled(p[key], a[name + "__idx"]) if name + "__idx" in a else np.asarray(p[key])
+        close(vals, a[name])
+        s, s2, size = t["array_sums"][name]
+        assert np.asarray(p[key]).size == size
+        close([np.sum(p[key]), np.sum(np.asarray(p[key]) ** 2)], [s, s2])
+    g.close()

@@ -54,6 +54,7 @@ def test_every_level_vs_reference(case, layout, split, monkeypatch):
     monkeypatch.setenv("VBFM_FORCE_SPLIT", split)
     monkeypatch.setenv("VBFM_DEFER", "0")
     t, a = load_case(case + "/levels")
+    _, s0 = load_case(case + "/steps")
     L = t["meta"]["num_levels"]
     g = _learner(case, layout)
     lv, nl = g.levels()
@@ -61,8 +62,8 @@ def test_every_level_vs_reference(case, layout, split, monkeypatch):
     np.testing.assert_array_equal(lv, a["levels"])
     g.init_caches()
     r = g.rows()
-    np.testing.assert_array_equal(r["e"], a["init_e"])
-    np.testing.assert_array_equal(r["t"], a["init_t"])
+    np.testing.assert_array_equal(r["e"], s0["s0_init_e"])
+    np.testing.assert_array_equal(r["t"], s0["s0_init_t"])
     g.step_w0()
     for key in ("e", "t"):
         close(g.rows()[key], a["l_w0_" + key], "w0 " + key)
