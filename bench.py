@@ -58,52 +58,135 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def cpu_baseline(cfg, sample_rows, sample_factors, seed=1):
-    """Time the reference's own factor sweep (fm_learn_vb.h:409-440: add_main_q + update_v
-    over all features) single-threaded on a bounded sample of the workload: the same
-    field/id shape with sample_rows rows, sample_factors factors timed."""
-    sys.path.insert(0, os.path.join(ROOT, "tests"))
-    import numpy as np
-    import synth
-    ref = os.path.join(ROOT, "oracle", "_ref", "ref_driver")
-    F, S = cfg["fields"], cfg["ids"]
-    tmp = tempfile.mkdtemp(prefix="vbfm_cpu_")
-    rp, f, v, y = synth.generate(sample_rows, F, S, seed, 0)
-    sample = "%d rows x %d fields x %d ids (D=%d), %d factors of the sweep, x=1" % (
-        sample_rows, F, S, F * S, sample_factors)
+def host_cpu_info():
+    """CPU model and the last-level cache one core sees (the sample must not fit in it)."""
+    model, llc = "?", None
     try:
-        if os.path.exists(ref):
-            synth.write_binary(os.path.join(tmp, "train"), F * S, rp, f, v, y)
-            rpt, ft, vt, yt = synth.generate(64, F, S, seed + 1, 0)
-            synth.write_binary(os.path.join(tmp, "test"), F * S, rpt, ft, vt, yt)
-            del rp, f, v, y
-            out = subprocess.run(["taskset", "-c", "0", ref, "sweep", "--train", os.path.join(tmp, "train"),
-                                  "--test", os.path.join(tmp, "test"), "--dim", "1,1,%d" % sample_factors,
-                                  "--seed", "1", "--sweep_factors", str(sample_factors)],
-                                 cwd=tmp, capture_output=True, text=True, check=True, timeout=600).stdout
-            r = json.loads([l for l in out.splitlines() if l.startswith("{")][0])
-            res = {"value": r["nnz_k_per_s"], "unit": "nnz*k/s", "cores": 1, "kind": "reference",
-                   "sample": sample + "; oracle/_ref/ref_driver = the reference's fm_learn_vb compiled "
-                   "from its sources, taskset -c 0 (1 of %d host cores)" % os.cpu_count(),
-                   "seconds": r["sweep_s"], "k0_seconds": r.get("k0_s")}
-            res.update(extrapolate_iteration(cfg, sample_rows, sample_factors, r["sweep_s"], r.get("k0_s")))
-            return res
-        # no reference build on this host: time the oracle restatement (bit-exact port)
-        import oracle_ctypes as oc
-        tr = oc.Data(csr=(sample_rows, rp, f, v, y))
-        vb = oc.VB(1, 1, sample_factors, F * S + 1)
-        vb.init_params(1, 0.1)
-        vb.attach(tr, tr)
-        vb.init_caches()
-        t0 = time.perf_counter()
-        for fk in range(sample_factors):
-            vb.step("add_main_q", fk)
-            vb.step("update_v_all", fk)
-        dt = time.perf_counter() - t0
-        return {"value": len(f) * sample_factors / dt, "unit": "nnz*k/s", "cores": 1, "kind": "port",
-                "sample": sample + "; oracle/liboracle.so (C restatement, single thread)", "seconds": dt}
-    finally:
-        subprocess.run(["rm", "-rf", tmp])
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+        for idx in range(8):
+            d = "/sys/devices/system/cpu/cpu0/cache/index%d" % idx
+            if not os.path.exists(d):
+                break
+            if open(d + "/level").read().strip() == "3":
+                llc = open(d + "/size").read().strip()
+    except OSError:
+        pass
+    return model, llc
+
+
+def write_cpu_sample(vbfm, cfg, rows, base, device):
+    """Rows [0, rows) of the bench's train set (tests/synth.py, seed 1000, x = 1) generated on
+    the device like the bench's own, copied back and written in the reference's binary format
+    (<base>.x/.xt/.y, fmatrix.h:46-52), plus a 64-row test set: the reference loads it with its
+    own Data::load (Data.h:112-171)."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import synth
+    F, S = cfg["fields"], cfg["ids"]
+    g = vbfm.FMLearnVB(1, 1, 1, F * S + 1, min_target=1.0, max_target=5.0, device=device)
+    g.synth(0, rows, F, S, seed=1000, xmode=0)
+    cp, ent, y = g.get_csc(0)
+    g.close()
+    crow, cval = ent["id"], ent["value"]
+    del ent
+    rp, feat, val = synth.field_csr_from_csc(rows, F, S, cp, crow, cval)
+    synth.write_binary_csc(base + "_train", F * S, rp, feat, val, y, cp, crow, cval)
+    del rp, feat, val, cp, crow, cval, y
+    rpt, ft, vt, yt = synth.generate(64, F, S, 1001, 0)
+    synth.write_binary(base + "_test", F * S, rpt, ft, vt, yt)
+
+
+def ref_sweep(base, factors):
+    """The reference's own factor sweep (oracle/_ref/ref_driver sweep: fm_learn_vb.h:409-440,
+    add_main_q + update_v over all features, plus the k = 0 overhead update_w0 + the w sweep)
+    on one core (taskset -c 0)."""
+    ref = os.path.join(ROOT, "oracle", "_ref", "ref_driver")
+    out = subprocess.run(["taskset", "-c", "0", ref, "sweep", "--train", base + "_train", "--test", base + "_test",
+                          "--dim", "1,1,%d" % factors, "--seed", "1", "--sweep_factors", str(factors)],
+                         cwd=os.path.dirname(base), capture_output=True, text=True, check=True, timeout=1200).stdout
+    return json.loads([l for l in out.splitlines() if l.startswith("{")][0])
+
+
+def cpu_baseline_start(vbfm, cfg, device, samples):
+    """Write the samples (device generator, before the timed region) and start the reference's
+    sweep on them in a background thread, so that the CPU leg runs while the GPU steps are
+    timed (one host core; the GPU bench thread uses another). samples: [(rows, factors), ...],
+    the last one reported as `value` -- large enough that its row caches (40 B per row) and
+    per-entry streams exceed the host's last-level cache, as C4's do -- the others beside it.
+    Returns a function that waits and returns the cpu_baseline object."""
+    import threading
+    ref = os.path.join(ROOT, "oracle", "_ref", "ref_driver")
+    if not os.path.exists(ref):
+        return lambda: cpu_baseline_port(cfg, min(samples[0][0], 2_000_000), samples[0][1])
+    tmp = tempfile.mkdtemp(prefix="vbfm_cpu_", dir=os.environ.get("TMPDIR"))
+    bases = []
+    for i, (rows, _) in enumerate(samples):
+        b = os.path.join(tmp, "s%d" % i)
+        write_cpu_sample(vbfm, cfg, rows, b, device)
+        bases.append(b)
+    res = {}
+
+    def work():
+        try:
+            res["runs"] = [ref_sweep(b, f) for b, (_, f) in zip(bases, samples)]
+        except Exception as exc:   # the GPU number stands on its own; report why the CPU leg failed
+            res["error"] = str(exc)
+        finally:
+            subprocess.run(["rm", "-rf", tmp])
+
+    th = threading.Thread(target=work, daemon=True)
+    th.start()
+
+    def finish():
+        th.join()
+        if "error" in res:
+            return {"value": None, "error": res["error"]}
+        model, llc = host_cpu_info()
+        F, S = cfg["fields"], cfg["ids"]
+        out = []
+        for (rows, f), r in zip(samples, res["runs"]):
+            o = {"rows": rows, "factors": f, "nnz": r["nnz"], "value": r["nnz_k_per_s"], "seconds": r["sweep_s"],
+                 "k0_seconds": r.get("k0_s"), "row_cache_bytes": 40 * rows}
+            o.update(extrapolate_iteration(cfg, rows, f, r["sweep_s"], r.get("k0_s")))
+            out.append(o)
+        big = out[-1]
+        return {"value": big["value"], "unit": "nnz*k/s", "cores": 1, "kind": "reference",
+                "sample": "%d rows x %d fields x %d ids (D=%d), %d factor(s) of the sweep, x=1 (rows 0.. of the "
+                          "bench's data set); oracle/_ref/ref_driver = the reference's fm_learn_vb compiled from its "
+                          "sources, taskset -c 0 (1 of %d host cores: %s, last-level cache %s per core complex; the "
+                          "sample's row caches alone are %.1f GB)" % (
+                              big["rows"], F, S, F * S, big["factors"], os.cpu_count(), model, llc,
+                              big["row_cache_bytes"] / 1e9),
+                "seconds": big["seconds"], "k0_seconds": big["k0_seconds"],
+                "extrapolated_iteration_s": big.get("extrapolated_iteration_s"),
+                "extrapolation": big.get("extrapolation"), "cpu_model": model, "llc": llc,
+                "samples": out}
+
+    return finish
+
+
+def cpu_baseline_port(cfg, sample_rows, sample_factors, seed=1):
+    """No reference build on this host: time the oracle restatement (bit-exact port) instead."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import synth
+    import oracle_ctypes as oc
+    F, S = cfg["fields"], cfg["ids"]
+    rp, f, v, y = synth.generate(sample_rows, F, S, seed, 0)
+    tr = oc.Data(csr=(sample_rows, rp, f, v, y))
+    vb = oc.VB(1, 1, sample_factors, F * S + 1)
+    vb.init_params(1, 0.1)
+    vb.attach(tr, tr)
+    vb.init_caches()
+    t0 = time.perf_counter()
+    for fk in range(sample_factors):
+        vb.step("add_main_q", fk)
+        vb.step("update_v_all", fk)
+    dt = time.perf_counter() - t0
+    return {"value": len(f) * sample_factors / dt, "unit": "nnz*k/s", "cores": 1, "kind": "port",
+            "sample": "%d rows x %d fields x %d ids, %d factors; oracle/liboracle.so (C restatement, single thread)"
+                      % (sample_rows, F, S, sample_factors), "seconds": dt}
 
 
 def extrapolate_iteration(cfg, sample_rows, sample_factors, sweep_s, k0_s):
@@ -204,9 +287,14 @@ def main():
     ap.add_argument("--no-launch-events", action="store_true",
                     help="no HIP event pair around every level launch (the roofline then divides the "
                          "sweep phase by the launch count: gaps between launches included)")
+    ap.add_argument("--one-rank-comm", action="store_true",
+                    help="one GPU through a real 1-rank RCCL communicator and the row-shard (split) kernels "
+                         "(VBFM_FORCE_SPLIT / VBFM_FORCE_COMM): the per-rank path of an N-GPU run, minus the "
+                         "other ranks -- for A/B of the per-level exchange on one GPU")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-rows", type=int, default=2_000_000)
-    ap.add_argument("--cpu-factors", type=int, default=2)
+    ap.add_argument("--cpu-rows", type=int, default=20_000_000,
+                    help="rows of the CPU baseline's sample (reported); a 2e6-row, 2-factor sample runs beside it")
+    ap.add_argument("--cpu-factors", type=int, default=1)
     args = ap.parse_args()
 
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
@@ -216,6 +304,11 @@ def main():
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         raise SystemExit("bench.py: --gpus %d but WORLD_SIZE=%d" % (args.gpus, world))
+    if args.one_rank_comm:   # read by vbfm_create / vbfm_comm_init
+        if world != 1:
+            raise SystemExit("--one-rank-comm is a one-rank mode")
+        os.environ["VBFM_FORCE_SPLIT"] = "1"
+        os.environ["VBFM_FORCE_COMM"] = "1"
     cfg = dict(CONFIGS[args.config])
     if args.rows:
         cfg["rows"] = args.rows
@@ -264,6 +357,8 @@ def main():
         if mc:
             raise SystemExit("--shard features is a VB mode")
         fml.set_shard_mode("features")
+    if args.one_rank_comm:
+        fml.comm_init(1, 0, vbfm.FMLearnVB.comm_unique_id())
     if world > 1 and args.transport == "host":
         def host_allreduce(arr, op):
             t = torch.from_numpy(arr.astype(np.float64) if arr.dtype == np.uint32 else arr.copy())
@@ -302,6 +397,16 @@ def main():
     nnz = fml.shape(0)[2]                # this rank's train entries
     log("rank %d: setup %.1f s (N=%d F=%d S=%d features=%d nnz=%d k=%d, %s layout)" % (
         rank, time.time() - t0, N, F, S, NF, nnz, k, layout))
+
+    cpu_leg = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and not mc and not online and not multihot:
+        try:   # the samples written now (device generator); the reference runs during the timed steps
+            rows = min(args.cpu_rows, N)
+            samples = [(min(2_000_000, rows), min(2, k))] if rows > 2_000_000 else []
+            samples.append((rows, min(args.cpu_factors, k)))
+            cpu_leg = cpu_baseline_start(vbfm, cfg, device, samples)
+        except Exception as exc:
+            cpu_leg = (lambda e=str(exc): {"value": None, "error": e})
 
     def rmse_of(st):
         return st.rmse_all if mc else st.rmse
@@ -438,12 +543,8 @@ def main():
              "ms_total"))},
         "cpu_baseline": None,
     }
-    if rank == 0 and world == 1 and not args.no_cpu_baseline and not mc and not online and not multihot:
-        try:
-            rows = min(args.cpu_rows, N)
-            result["cpu_baseline"] = cpu_baseline(cfg, rows, min(args.cpu_factors, k))
-        except Exception as exc:  # the GPU number stands on its own; report why the CPU leg failed
-            result["cpu_baseline"] = {"value": None, "error": str(exc)}
+    if cpu_leg is not None:
+        result["cpu_baseline"] = cpu_leg()
     fml.close()
     if rank == 0:
         print(json.dumps(result), flush=True)

@@ -53,12 +53,11 @@ void allreduce_dev(vbfm_ctx *c, void *buf, size_t n, ncclDataType_t t, ncclRedOp
 uint32_t ar_chunks(vbfm_ctx *c, uint32_t nfeat)
 {
 	if (!c->row_comm()) return 1;
-	static const int env = [] {
-		const char *e = getenv("VBFM_AR_CHUNKS");
-		return e ? atoi(e) : 4;
-	}();
-	// at least 2048 columns per chunk: a smaller launch leaves the chip idle at its tail
-	const uint32_t C = std::min<uint32_t>((uint32_t)std::max(env, 1), nfeat / 2048);
+	// default 4 chunks of at least 2048 columns (a smaller launch leaves the chip idle at its
+	// tail); VBFM_AR_CHUNKS=n asks for n chunks of at least 64 columns (tests, A/B)
+	const char *e = getenv("VBFM_AR_CHUNKS");
+	const uint32_t want = e ? (uint32_t)std::max(atoi(e), 1) : 4u, floor = e ? 64u : 2048u;
+	const uint32_t C = std::min<uint32_t>(want, nfeat / floor);
 	return std::max<uint32_t>(1, std::min<uint32_t>(C, vbfm_ctx::AR_MAX_CHUNKS));
 }
 
@@ -220,8 +219,11 @@ static void build_long_segs(vbfm_ctx *c, const std::vector<uint64_t> &lcp, const
 // the entry its next level sweeps, so a level streams its columns' runs and scatters each
 // record to the row's next slot (k_level_lord<..., ENT>) instead of gathering and writing back
 // rows in place (the column-gather layout: two random touches per entry).
-// Single rank, fused sweeps, no row listing a feature twice (VB and MCMC / ALS); the store must
-// fit in half the free memory. A row without entries parks its record in slot nnz + r.
+// No row listing a feature twice (VB and MCMC / ALS); the store must fit in half the free
+// memory. A row without entries parks its record in slot nnz + r. Row shards (split sweeps): the
+// VB sweep's deferred form reads each slot's previous-entry payload (k_estore_prev: the global
+// level-feature index and x of the row's previous entry) and a posterior table over all level
+// features; VBFM_DEFER=0 and the MCMC / ALS sweep take the two-pass split.
 // Returns false when it does not apply (force: throw instead).
 bool build_estore(vbfm_ctx *c, const std::vector<uint64_t> &lcp, const std::vector<uint8_t> &dup,
                   const std::vector<uint32_t> &feats, bool force)
@@ -233,7 +235,6 @@ bool build_estore(vbfm_ctx *c, const std::vector<uint64_t> &lcp, const std::vect
 	size_t fr = 0, tot = 0;
 	HIPCHK(hipMemGetInfo(&fr, &tot));
 	if (!force && env && env[0] == '0') why = "VBFM_ESTORE=0";
-	else if (c->row_comm() || c->force_split) why = "row shards (split sweeps)";
 	else if (n == 0 || d.nnz == 0) why = "no train entries";
 	else if (d.nnz + n >= 0x80000000ull) why = "more than 2^31 entries and rows";
 	else if ((double)(d.nnz + n) * sizeof(RowRec) > 0.5 * (double)fr) why = "the store does not fit in half the free memory";
@@ -265,6 +266,24 @@ bool build_estore(vbfm_ctx *c, const std::vector<uint64_t> &lcp, const std::vect
 	HIPCHK(hipMemsetAsync(c->rows_alt, 0, (d.nnz + n) * sizeof(RowRec), c->s));
 	HIPCHK(vbk::estore_build(d.row_ptr, d.csr, d.col_ptr, d.csc, lv, c->lcp, n, d.nnz, c->lnext, c->lx, c->lpos0,
 	                         c->s));
+	const char *df = getenv("VBFM_DEFER");
+	if ((c->row_comm() || c->force_split) && !(df && df[0] == '0')) {
+		uint32_t *pidx = dalloc<uint32_t>(d.nnz);
+		float *px = dalloc<float>(d.nnz);
+		HIPCHK(vbk::estore_prev(d.row_ptr, d.csr, d.col_ptr, d.csc, lv, c->lcp, n, pidx, px, c->s));
+		if (c->lx) {
+			c->lpay = dalloc<uint4>(d.nnz);
+			HIPCHK(vbk::lord_pack(c->lx, c->lnext, pidx, px, c->lpay, d.nnz, c->s));
+		} else {   // every x 1: 8 B per entry
+			c->lpay2 = dalloc<uint2>(d.nnz);
+			HIPCHK(vbk::lord_pack2(c->lnext, pidx, c->lpay2, d.nnz, c->s));
+		}
+		c->post_tab = dalloc<PostT>(std::max(nf, 1u));
+		HIPCHK(hipMemsetAsync(c->post_tab, 0, (size_t)std::max(nf, 1u) * sizeof(PostT), c->s));
+		sync(c);
+		dfree(pidx);
+		dfree(px);
+	}
 	sync(c);
 	dfree(lv);
 	c->lord = true;
@@ -806,9 +825,14 @@ void sweep_level(vbfm_ctx *c, uint32_t l, bool is_w, int f)
 			a.lbase = 0;
 			a.dst = c->rows;
 			a.ent = 1;
-			HIPCHK(vbk::lord_level(a, is_w, c->s));
-			prof_end(c, p);
-			return;
+			a.tab_base = c->level_ptr[l];
+			a.lfirst = c->lpos0;
+			a.ent_nnz = c->tr.nnz;
+			if (!c->row_comm() && !c->force_split) {
+				HIPCHK(vbk::lord_level(a, is_w, c->s));
+				prof_end(c, p);
+				return;
+			}
 		}
 		if (!c->row_comm() && !c->force_split) {
 			if (c->long_min) {
@@ -825,10 +849,14 @@ void sweep_level(vbfm_ctx *c, uint32_t l, bool is_w, int f)
 			a.lpay = c->lpay;
 			a.lpay2 = c->lpay2;
 			a.tab = c->post_tab;
-			// level 0 of a v sweep may carry the previous sweep's last correction (vbfm_iterate)
-			const bool carried = l == 0 && c->carry != 0 && !is_w;
-			a.pend_kind = carried ? (c->carry == 3 ? 2 : 1) : 0;
-			c->carry = 0;
+			// level 0 of a v sweep may carry the previous sweep's last correction (vbfm_iterate);
+			// in the entry store the rows' first entries -- which carry it -- lie in every level
+			if (l == 0) {
+				c->carry_in = (c->carry != 0 && !is_w) ? (c->carry == 3 ? 2 : 1) : 0;
+				c->carry = 0;
+			}
+			const bool carried = (l == 0 || c->estore) && c->carry_in != 0;
+			a.pend_kind = carried ? c->carry_in : 0;
 			a.pending = (l > 0 || carried) ? 1 : 0;
 			if (c->tr.n > 50000000u) a.pending |= 2;     // non-temporal record loads (large shards)
 			a.first_prev = l == 1;
@@ -842,7 +870,7 @@ void sweep_level(vbfm_ctx *c, uint32_t l, bool is_w, int f)
 				if (carry_out) {
 					c->carry = is_w ? 3 : 1 + (f & 1);
 				} else {
-					a.dst = c->rows_alt;      // (swapped below)
+					a.dst = c->estore ? c->rows : c->rows_alt;   // (the field store's: swapped below)
 					a.first_prev = l == 0;
 					HIPCHK(vbk::lord_defer_flush(a, is_w, c->tr.n, c->s));
 				}
@@ -851,7 +879,7 @@ void sweep_level(vbfm_ctx *c, uint32_t l, bool is_w, int f)
 			stats_exchange(c, a, [&](const LevelArgs &b) { HIPCHK(vbk::lord_level_stats(b, is_w, c->s)); });
 			HIPCHK(vbk::lord_level_move(a, is_w, c->s));
 		}
-		std::swap(c->rows, c->rows_alt);
+		if (!c->estore) std::swap(c->rows, c->rows_alt);
 		prof_end(c, p);
 		return;
 	}

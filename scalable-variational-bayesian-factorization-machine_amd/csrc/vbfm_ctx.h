@@ -110,6 +110,7 @@ struct vbfm_ctx {
 	std::vector<uint32_t> level_base;   // first id of a level of consecutive feature ids, else ~0u
 	int q_ready[2] = {-1, -1};     // factor whose q-cache each slot holds (-1: none)
 	int qslot = 0;                 // slot reported by vbfm_get_rows
+	int carry_in = 0;              // the pending kind carried into the current sweep (deferred split)
 	// a sweep driven level by level (vbfm_step_w_level / vbfm_step_v_level): kind -1 none, 0 the
 	// w sweep, 1 the v sweep of factor part_f; part_next = the level expected next
 	int part_kind = -1, part_f = 0;

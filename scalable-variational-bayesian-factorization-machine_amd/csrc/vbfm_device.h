@@ -113,6 +113,10 @@ struct LevelArgs {
 	int first_prev;            // the previous level is level 0 (q-cache restart of its entries)
 	int pend_kind;             // level 0 of a v sweep: the pending correction is the previous sweep's last
 	                           // level (1: v of the other q-cache slot, 2: w); 0: this sweep's own
+	uint32_t tab_base;         // the entry store: post writes tab[tab_base + i] (a table over every level
+	                           // feature, tab_base = the level's first), the kernels read tab[global index]
+	const uint32_t *lfirst;    // the entry store's flush: each row's first slot (nnz + r: no entries)
+	uint64_t ent_nnz;          // ... and the number of entry slots
 	// online VB (vbfm_online.hip): natural-gradient steps on a mini-batch; nat == nullptr: VB
 	double2 *nat;              // natural parameters {mu, sigma} of each feature: nat[j * nat_stride]
 	uint32_t nat_stride;       // 1: factor-major (nat_v + f * D), so a level's columns read one run
@@ -234,6 +238,8 @@ hipError_t lord_pack(const float *lx, const uint32_t *lnext, const uint32_t *lpi
 hipError_t estore_build(const uint64_t *row_ptr, const uint2 *csr, const uint64_t *col_ptr, const uint2 *csc,
                         const uint32_t *lvpos, const uint64_t *lcp, uint32_t n, uint64_t nnz, uint32_t *lnext,
                         float *lx, uint32_t *lfirst, hipStream_t s);
+hipError_t estore_prev(const uint64_t *row_ptr, const uint2 *csr, const uint64_t *col_ptr, const uint2 *csc,
+                       const uint32_t *lvpos, const uint64_t *lcp, uint32_t n, uint32_t *lpidx, float *lpx, hipStream_t s);
 hipError_t rows_scatter(RowRec *dst, const RowRec *src, const uint32_t *idx, uint32_t n, hipStream_t s);
 hipError_t mark_first(const uint64_t *row_ptr, const uint2 *csr, const uint64_t *col_ptr, uint2 *csc,
                       uint32_t n, hipStream_t s);

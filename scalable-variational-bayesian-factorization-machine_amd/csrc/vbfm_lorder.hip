@@ -443,7 +443,7 @@ __global__ __launch_bounds__(BLOCK) void k_level_lord_stats(LevelArgs a)
 	if (threadIdx.x == 0) a.stats[blockIdx.x] = make_double2(s1, s2);
 }
 
-template <int BLOCK, bool IS_W, int P, bool NEXT>
+template <int BLOCK, bool IS_W, int P, bool NEXT, bool ENT = false>
 __global__ __launch_bounds__(BLOCK) void k_level_lord_move(LevelArgs a)
 {
 	constexpr uint32_t CAP = BLOCK * 2;
@@ -460,8 +460,8 @@ __global__ __launch_bounds__(BLOCK) void k_level_lord_move(LevelArgs a)
 	const double hyp = (a.hyp_uniform ? a.hyp0 : a.hyp[(size_t)a.attr_group[j] * a.hyp_stride]);
 	op.go = vb_post<IS_W>(st.x, st.y, hyp, a.alpha, op.mo, op.so, op.mu, op.sig, a.counters, threadIdx.x == 0);
 	if (threadIdx.x == 0) a.ms[(size_t)j * a.ms_stride] = make_double2(op.mu, op.sig);
-	lord_move<BLOCK, CAP>(recs, dsts, a.src + (sb - a.lbase), a.lx ? a.lx + sb : nullptr, a.lnext + sb, n, false, a.dst,
-	                      a.first_level != 0, op);
+	lord_move<BLOCK, CAP, VbOp<IS_W, P, NEXT>, ENT>(recs, dsts, a.src + (sb - a.lbase), a.lx ? a.lx + sb : nullptr,
+	                                                a.lnext + sb, n, false, a.dst, a.first_level != 0, op);
 }
 
 // ---- MCMC / ALS on the level-ordered store -----------------------------------------------
@@ -570,6 +570,32 @@ __global__ __launch_bounds__(256) void k_lord_fill(const uint32_t *feats, const 
 	}
 }
 
+// the entry store's deferred payload (row shards): for every slot, the global level-feature
+// index and the x of the row's previous entry (the first entry's previous is the row's last:
+// the correction a sweep leaves pending at its end, carried into the next sweep or flushed)
+__global__ __launch_bounds__(256) void k_estore_prev(const uint64_t *row_ptr, const uint2 *csr, const uint64_t *col_ptr,
+                                                     const uint2 *csc, const uint32_t *lvpos, const uint64_t *lcp,
+                                                     uint32_t n, uint32_t *lpidx, float *lpx)
+{
+	const uint32_t r = blockIdx.x * 256u + threadIdx.x;
+	if (r >= n) return;
+	const uint64_t b = row_ptr[r], e = row_ptr[r + 1];
+	for (uint64_t p = b; p < e; ++p) {
+		const uint32_t j = csr[p].x;
+		uint64_t lo = col_ptr[j], hi = col_ptr[j + 1];   // rows ascending: the row's entry of column j
+		const uint64_t c0 = lo;
+		while (lo < hi) {
+			const uint64_t mid = (lo + hi) >> 1;
+			if ((csc[mid].x & ROW_MASK) < r) lo = mid + 1;
+			else hi = mid;
+		}
+		const uint32_t slot = (uint32_t)(lcp[lvpos[j]] + (lo - c0));
+		const uint2 prev = csr[p == b ? e - 1 : p - 1];
+		lpidx[slot] = lvpos[prev.x];
+		lpx[slot] = ent_x(prev);
+	}
+}
+
 // number of entries whose x is not 1.0f (the level store then keeps x per entry)
 __global__ __launch_bounds__(256) void k_count_x_ne1(const uint2 *csc, uint64_t nnz, uint32_t *cnt)
 {
@@ -661,6 +687,11 @@ void launch_lord(const LevelArgs &a, hipStream_t s)
 template <bool IS_W, int P>
 void launch_lord_move(const LevelArgs &a, hipStream_t s)
 {
+	if (a.ent) {
+		if (a.ms_next) k_level_lord_move<256, IS_W, P, true, true><<<a.nfeat, 256, 0, s>>>(a);
+		else k_level_lord_move<256, IS_W, P, false, true><<<a.nfeat, 256, 0, s>>>(a);
+		return;
+	}
 	if (a.ms_next) k_level_lord_move<256, IS_W, P, true><<<a.nfeat, 256, 0, s>>>(a);
 	else k_level_lord_move<256, IS_W, P, false><<<a.nfeat, 256, 0, s>>>(a);
 }
@@ -719,7 +750,13 @@ DEVI void add_next_q(Rec &v, float x, bool first, double2 nx)
 // PK: which level's correction is pending -- 0: the previous level of this sweep; at level 0 of
 // a v sweep the previous sweep's last level, left unflushed: 1 = v with the other q-cache slot
 // (the previous factor), 2 = w (the w sweep before factor 0)
-template <int BLOCK, int R, bool IS_W, int P, bool NEXT, int PK, bool PAY8>
+// ENT (the entry store under row shards): a row's previous entry sits in any earlier level, so
+// the posteriors live in one table over all level features (tab[global index], written by each
+// level's post kernel at tab_base) and the pending correction is decided per entry: the row's
+// first entry (ENT_FIRST) carries the previous sweep's last correction (PK, or nothing when
+// that sweep was flushed), every other entry the correction of the row's previous entry in
+// this sweep; records move to their rows' next slots in the same store (non-temporal stores)
+template <int BLOCK, int R, bool IS_W, int P, bool NEXT, int PK, bool PAY8, bool ENT = false>
 __global__ __launch_bounds__(BLOCK) void k_lord_defer(LevelArgs a)
 {
 	constexpr uint32_t CAP = BLOCK * R;
@@ -773,20 +810,27 @@ __global__ __launch_bounds__(BLOCK) void k_lord_defer(LevelArgs a)
 			Rec v;
 			lds_get(recs, i, v);
 			const float x = __uint_as_float(q[u].x);
-			if (pending) {
-				if constexpr (PK == 0) apply_pending<IS_W, P>(v, t[u], __uint_as_float(q[u].w));
-				else if constexpr (PK == 1) apply_pending<false, 1 - P>(v, t[u], __uint_as_float(q[u].w));
-				else apply_pending<true, 0>(v, t[u], __uint_as_float(q[u].w));
+			const float px = __uint_as_float(q[u].w);
+			bool fe = first;
+			if constexpr (ENT) {
+				fe = (q[u].y & ENT_FIRST) != 0;
+				if (!fe) apply_pending<IS_W, P>(v, t[u], px);
+				else if constexpr (PK == 1) apply_pending<false, 1 - P>(v, t[u], px);
+				else if constexpr (PK == 2) apply_pending<true, 0>(v, t[u], px);
+			} else if (pending) {
+				if constexpr (PK == 0) apply_pending<IS_W, P>(v, t[u], px);
+				else if constexpr (PK == 1) apply_pending<false, 1 - P>(v, t[u], px);
+				else apply_pending<true, 0>(v, t[u], px);
 			}
-			if constexpr (NEXT) add_next_q<IS_W, P>(v, x, first, nx);
-			if (pending || NEXT) lds_put(recs, i, v);
+			if constexpr (NEXT) add_next_q<IS_W, P>(v, x, fe, nx);
+			if (ENT || pending || NEXT) lds_put(recs, i, v);
 			op.stat(v, x, s1, s2);
-			dsts[i] = q[u].y;
+			dsts[i] = ENT ? q[u].y & ~ENT_FIRST : q[u].y;
 		}
 		__syncthreads();
 		for (uint32_t t = threadIdx.x; t < m * 4; t += BLOCK) {
 			const uint32_t i = t >> 2, c = t & 3;
-			d[(size_t)dsts[i] * 4 + c] = recs[lslot(i, c)];
+			put_piece<ENT>(d, (size_t)dsts[i] * 4 + c, recs[lslot(i, c)]);
 		}
 	}
 	block_sum2<BLOCK>(s1, s2, lds);
@@ -810,7 +854,7 @@ __global__ __launch_bounds__(256) void k_lord_defer_post(LevelArgs a)
 	PostT t;
 	t.mo = msj.x; t.so = msj.y; t.sig = sig;
 	t.mu = go ? mu : __builtin_nan("");
-	a.tab[i] = t;
+	a.tab[a.tab_base + i] = t;
 }
 
 // the last level's correction, in place on the records (level-0 order after the last move)
@@ -832,6 +876,25 @@ __global__ __launch_bounds__(256) void k_lord_defer_flush(LevelArgs a, uint32_t 
 	}
 	__syncthreads();
 	for (uint32_t t = threadIdx.x; t < m * 4; t += 256) r[t] = recs[lslot(t >> 2, t & 3)];
+}
+
+// the entry store's flush: after a sweep every row's record waits in its first slot with the
+// correction of its last entry pending (the first slot's payload names that entry: the cycle)
+template <bool IS_W, int P>
+__global__ __launch_bounds__(256) void k_lord_defer_flush_ent(LevelArgs a, uint32_t n)
+{
+	const uint32_t r = blockIdx.x * 256u + threadIdx.x;
+	if (r >= n) return;
+	const uint32_t s = a.lfirst[r];
+	if (s >= a.ent_nnz) return;   // a row without entries: never swept
+	double2 *p = reinterpret_cast<double2 *>(a.dst + s);
+	Rec v;
+#pragma unroll
+	for (int c = 0; c < 4; ++c) v[c] = p[c];
+	const uint4 q = pay_at(a, s);
+	apply_pending<IS_W, P>(v, a.tab[q.z], __uint_as_float(q.w));
+#pragma unroll
+	for (int c = 0; c < 4; ++c) p[c] = v[c];
 }
 
 // build: prev_i[row] / prev_x[row] = (index within its level, x) of the row's entry in a level
@@ -862,20 +925,27 @@ __global__ __launch_bounds__(256) void k_lord_prev_fill(const uint32_t *feats, c
 }
 
 
+template <bool IS_W, int P, bool NEXT, int PK, bool ENT>
+void launch_defer_shape(const LevelArgs &a, hipStream_t s)
+{
+	if (a.lpay2) {   // every x 1: 8-B payloads
+		if (a.avg_len <= shape_small_max()) k_lord_defer<64, 2, IS_W, P, NEXT, PK, true, ENT><<<a.nfeat, 64, 0, s>>>(a);
+		else if (a.avg_len <= 320) k_lord_defer<256, 1, IS_W, P, NEXT, PK, true, ENT><<<a.nfeat, 256, 0, s>>>(a);
+		else if (a.avg_len <= 640) k_lord_defer<256, 2, IS_W, P, NEXT, PK, true, ENT><<<a.nfeat, 256, 0, s>>>(a);
+		else k_lord_defer<512, 2, IS_W, P, NEXT, PK, true, ENT><<<a.nfeat, 512, 0, s>>>(a);
+		return;
+	}
+	if (a.avg_len <= shape_small_max()) k_lord_defer<64, 2, IS_W, P, NEXT, PK, false, ENT><<<a.nfeat, 64, 0, s>>>(a);
+	else if (a.avg_len <= 320) k_lord_defer<256, 1, IS_W, P, NEXT, PK, false, ENT><<<a.nfeat, 256, 0, s>>>(a);
+	else if (a.avg_len <= 640) k_lord_defer<256, 2, IS_W, P, NEXT, PK, false, ENT><<<a.nfeat, 256, 0, s>>>(a);
+	else k_lord_defer<512, 2, IS_W, P, NEXT, PK, false, ENT><<<a.nfeat, 512, 0, s>>>(a);
+}
+
 template <bool IS_W, int P, bool NEXT, int PK>
 void launch_defer_pk(const LevelArgs &a, hipStream_t s)
 {
-	if (a.lpay2) {   // every x 1: 8-B payloads
-		if (a.avg_len <= shape_small_max()) k_lord_defer<64, 2, IS_W, P, NEXT, PK, true><<<a.nfeat, 64, 0, s>>>(a);
-		else if (a.avg_len <= 320) k_lord_defer<256, 1, IS_W, P, NEXT, PK, true><<<a.nfeat, 256, 0, s>>>(a);
-		else if (a.avg_len <= 640) k_lord_defer<256, 2, IS_W, P, NEXT, PK, true><<<a.nfeat, 256, 0, s>>>(a);
-		else k_lord_defer<512, 2, IS_W, P, NEXT, PK, true><<<a.nfeat, 512, 0, s>>>(a);
-		return;
-	}
-	if (a.avg_len <= shape_small_max()) k_lord_defer<64, 2, IS_W, P, NEXT, PK, false><<<a.nfeat, 64, 0, s>>>(a);
-	else if (a.avg_len <= 320) k_lord_defer<256, 1, IS_W, P, NEXT, PK, false><<<a.nfeat, 256, 0, s>>>(a);
-	else if (a.avg_len <= 640) k_lord_defer<256, 2, IS_W, P, NEXT, PK, false><<<a.nfeat, 256, 0, s>>>(a);
-	else k_lord_defer<512, 2, IS_W, P, NEXT, PK, false><<<a.nfeat, 512, 0, s>>>(a);
+	if (a.ent) launch_defer_shape<IS_W, P, NEXT, PK, true>(a, s);
+	else launch_defer_shape<IS_W, P, NEXT, PK, false>(a, s);
 }
 
 template <bool IS_W, int P, bool NEXT>
@@ -891,7 +961,8 @@ void launch_defer(const LevelArgs &a, hipStream_t s)
 template <bool IS_W, int P, bool NEXT>
 void launch_flush(const LevelArgs &a, uint32_t n, hipStream_t s)
 {
-	k_lord_defer_flush<IS_W, P, NEXT><<<(n + 255) / 256, 256, 0, s>>>(a, n);
+	if (a.ent) k_lord_defer_flush_ent<IS_W, P><<<(n + 255) / 256, 256, 0, s>>>(a, n);
+	else k_lord_defer_flush<IS_W, P, NEXT><<<(n + 255) / 256, 256, 0, s>>>(a, n);
 }
 
 // ---- MCMC / ALS deferred split (row shards) ------------------------------------------------
@@ -1264,6 +1335,14 @@ hipError_t estore_build(const uint64_t *row_ptr, const uint2 *csr, const uint64_
 {
 	if (n == 0) return hipSuccess;
 	k_estore_build<<<(n + 255) / 256, 256, 0, s>>>(row_ptr, csr, col_ptr, csc, lvpos, lcp, n, nnz, lnext, lx, lfirst);
+	return hipGetLastError();
+}
+
+hipError_t estore_prev(const uint64_t *row_ptr, const uint2 *csr, const uint64_t *col_ptr, const uint2 *csc,
+                       const uint32_t *lvpos, const uint64_t *lcp, uint32_t n, uint32_t *lpidx, float *lpx, hipStream_t s)
+{
+	if (n == 0) return hipSuccess;
+	k_estore_prev<<<(n + 255) / 256, 256, 0, s>>>(row_ptr, csr, col_ptr, csc, lvpos, lcp, n, lpidx, lpx);
 	return hipGetLastError();
 }
 

@@ -330,7 +330,12 @@ void mc_sweep(vbfm_ctx *c, bool is_w, int f)
 				a.lbase = 0;
 				a.dst = c->rows;
 				a.ent = 1;
-				HIPCHK(vbk::mc_lord_level(a, 0, is_w, c->s));
+				if (!c->row_comm() && !c->force_split) {
+					HIPCHK(vbk::mc_lord_level(a, 0, is_w, c->s));
+				} else {   // row shards: the two-pass split (statistics, all-reduce, draw + move)
+					stats_exchange(c, a, [&](const McArgs &b) { HIPCHK(vbk::mc_lord_level(b, 1, is_w, c->s)); });
+					HIPCHK(vbk::mc_lord_level(a, 2, is_w, c->s));
+				}
 				prof_end(c, p);
 				continue;
 			}

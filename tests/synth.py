@@ -149,6 +149,50 @@ def write_binary(base, n_feature, row_ptr, feat, val, y):
         fh.write(y.astype("<f4").tobytes())
 
 
+def field_csr_from_csc(n_rows, n_fields, ids_per_field, col_ptr, crow, cval):
+    """The CSR (rows in field order) of one-hot field data from its CSC: row r holds exactly one
+    id of every field, field f's at position r * F + f."""
+    nf = len(col_ptr) - 1
+    col = np.repeat(np.arange(nf, dtype=np.uint32), np.diff(col_ptr.astype(np.int64)))
+    pos = crow.astype(np.int64) * n_fields + col // np.uint32(ids_per_field)
+    feat = np.empty(n_rows * n_fields, dtype=np.uint32)
+    val = np.empty(n_rows * n_fields, dtype=np.float32)
+    feat[pos] = col
+    val[pos] = cval
+    del pos, col
+    return np.arange(n_rows + 1, dtype=np.uint64) * np.uint64(n_fields), feat, val
+
+
+def write_binary_csc(base, n_feature, row_ptr, feat, val, y, col_ptr, crow, cval):
+    """write_binary with the transposed copy given (no sort: large samples)."""
+    N, nnz = len(y), len(feat)
+
+    def write_sparse(path, nrows, ncols, ptr, ids, vals):
+        with open(path, "wb") as fh:
+            hdr = np.zeros(1, dtype=[("id", "<u4"), ("fs", "<u4"), ("nv", "<u8"), ("nr", "<u4"), ("nc", "<u4")])
+            hdr["id"], hdr["fs"], hdr["nv"], hdr["nr"], hdr["nc"] = 2, 4, nnz, nrows, ncols
+            fh.write(hdr.tobytes())
+            ptr64 = ptr.astype(np.int64)
+            for r0 in range(0, nrows, 1 << 20):           # in row blocks: bounded temporaries
+                r1 = min(nrows, r0 + (1 << 20))
+                b, e = int(ptr64[r0]), int(ptr64[r1])
+                sizes = np.diff(ptr64[r0:r1 + 1]).astype(np.uint32)
+                words = np.empty((r1 - r0) + 2 * (e - b), dtype="<u4")
+                row_off = np.arange(r1 - r0, dtype=np.int64) + 2 * (ptr64[r0:r1] - b)
+                words[row_off] = sizes
+                ent_row = np.repeat(np.arange(r1 - r0, dtype=np.int64), sizes.astype(np.int64))
+                ent_off = ent_row + 1 + 2 * np.arange(e - b, dtype=np.int64)
+                words[ent_off] = ids[b:e]
+                words[ent_off + 1] = np.asarray(vals[b:e], dtype="<f4").view("<u4")
+                fh.write(words.tobytes())
+
+    write_sparse(base + ".x", N, n_feature, row_ptr, feat, val)
+    write_sparse(base + ".xt", n_feature, N, col_ptr, crow, cval)
+    with open(base + ".y", "wb") as fh:
+        fh.write(np.array([1, 4, N], dtype="<u4").tobytes())
+        fh.write(y.astype("<f4").tobytes())
+
+
 def generate_multihot(n_rows, n_features, lo, hi, seed, xmode=0, model_seed=MODEL_SEED, row_offset=0):
     """Multi-hot rows without field structure (the device's vbfm_synth_multihot follows this):
 

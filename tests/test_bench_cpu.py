@@ -118,3 +118,28 @@ def test_cpu_baseline_extrapolates_one_iteration():
     assert r["extrapolated_iteration_s"] == pytest.approx(50 * (0.5 + 2.0 * cfg["k"]))
     assert r["extrapolation"].startswith("extrapolated")
     assert bench.extrapolate_iteration(cfg, 2_000_000, 2, sweep_s=4.0, k0_s=None) == {}
+
+
+def test_cpu_sample_files_and_reference_sweep(tmp_path):
+    """The CPU leg's sample in the reference's binary format (sort-free writer, CSR rebuilt from
+    the field CSC) is what the reference's own loader reads, and its sweep reports throughput."""
+    import os
+    import synth
+    import bench
+    rp, f, v, y = synth.generate(5000, 6, 50, 1000, 0)
+    cp, cr, cv = synth.csr_to_csc(5000, 300, rp, f, v)
+    rp2, f2, v2 = synth.field_csr_from_csc(5000, 6, 50, cp, cr, cv)
+    np.testing.assert_array_equal(f2, f)
+    base = str(tmp_path / "s0")
+    synth.write_binary_csc(base + "_train", 300, rp2, f2, v2, y, cp, cr, cv)
+    synth.write_binary(base + "_ref", 300, rp, f, v, y)
+    for ext in (".x", ".xt", ".y"):
+        assert open(base + "_train" + ext, "rb").read() == open(base + "_ref" + ext, "rb").read()
+    rpt, ft, vt, yt = synth.generate(64, 6, 50, 1001, 0)
+    synth.write_binary(base + "_test", 300, rpt, ft, vt, yt)
+    model, llc = bench.host_cpu_info()
+    assert model
+    if not os.path.exists(os.path.join(bench.ROOT, "oracle", "_ref", "ref_driver")):
+        pytest.skip("oracle/_ref/ref_driver not built")
+    r = bench.ref_sweep(base, 2)
+    assert r["nnz"] == 30000 and r["factors"] == 2 and r["nnz_k_per_s"] > 0

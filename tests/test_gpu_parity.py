@@ -145,17 +145,21 @@ def test_trace_synthetic_vs_reference(synth_files, split, layout, monkeypatch):
 
 
 @pytest.mark.parametrize("layout", ["column", "level"])
-@pytest.mark.parametrize("split", ["fused", "split", "rccl"])
+@pytest.mark.parametrize("split", ["fused", "split", "rccl", "rccl_chunks"])
 def test_trace_movielens_split_vs_reference(sa_split, split, layout, monkeypatch):
     """split: the row-sharded kernels on one rank; rccl: the same through a real 1-rank RCCL
-    communicator (every ncclAllReduce of the multi-GPU path runs). Every ML-1M row is one
-    (user, item) pair, so both dependency levels hold every row: the level layout applies."""
+    communicator (every ncclAllReduce of the multi-GPU path runs); rccl_chunks: each level's
+    statistics in 3 chunks whose all-reduces run on the communication stream while the next
+    chunk computes (stats_exchange). Every ML-1M row is one (user, item) pair, so both
+    dependency levels hold every row: the level layout applies."""
     if split != "fused":
         monkeypatch.setenv("VBFM_FORCE_SPLIT", "1")
+    if split == "rccl_chunks":
+        monkeypatch.setenv("VBFM_AR_CHUNKS", "3")
     monkeypatch.setenv("VBFM_LAYOUT", layout)
     t, a = load_case("sa_k8")
     train, test = vbfm.DataSubset.load(sa_split["train"]), vbfm.DataSubset.load(sa_split["test"])
-    if split == "rccl":
+    if split.startswith("rccl"):
         monkeypatch.setenv("VBFM_FORCE_COMM", "1")
         m = t["meta"]
         k0, k1, k = [int(x) for x in m["dim"].split(",")]
@@ -708,3 +712,46 @@ def test_test_prediction_overlap_is_bit_identical(monkeypatch):
         a, b = runs[("1", predict)], runs[("0", predict)]
         assert a[0] == b[0]
         np.testing.assert_array_equal(a[1], b[1])
+
+
+@pytest.mark.parametrize("method", ["vb", "mcmc", "als"])
+@pytest.mark.parametrize("layout", ["level", "column"])
+def test_chunked_exchange_is_bit_identical(method, layout, monkeypatch):
+    """The per-level exchange cut into chunks (VBFM_AR_CHUNKS=4 through a 1-rank RCCL
+    communicator: chunk i's all-reduce on the communication stream while chunk i+1's
+    statistics kernel runs) against the fused single-rank sweep: the same chain bit for bit
+    (every chunk sums exactly its columns' entries; VB and ALS / MCMC with device RNG streams)."""
+    rp, f, v, y = synth.generate(60000, 8, 1500, 17, 1)
+    rpt, ft, vt, yt = synth.generate(3000, 8, 1500, 18, 1)
+    nf = 8 * 1500
+
+    def run(split, chunks):
+        monkeypatch.setenv("VBFM_FORCE_SPLIT", split)
+        monkeypatch.setenv("VBFM_FORCE_COMM", split)
+        if chunks:
+            monkeypatch.setenv("VBFM_AR_CHUNKS", str(chunks))
+        else:
+            monkeypatch.delenv("VBFM_AR_CHUNKS", raising=False)
+        if method == "vb":
+            g = vbfm.FMLearnVB(1, 1, 3, nf + 1, min_target=float(y.min()), max_target=float(y.max()), layout=layout)
+        else:
+            g = vbfm.FMLearnMCMC(1, 1, 3, nf + 1, min_target=float(y.min()), max_target=float(y.max()),
+                                 method=method, layout=layout)
+        if split == "1":
+            g.comm_init(1, 0, vbfm.FMLearnVB.comm_unique_id())
+        if method == "vb":
+            g.init(3, 0.1)
+        else:
+            g.init_device(3, 0.1)
+        g.set_data(vbfm.DataSubset.from_csr(rp, f, v, y, nf), vbfm.DataSubset.from_csr(rpt, ft, vt, yt, nf))
+        g.init_caches()
+        st = [g.iterate() for _ in range(2)]
+        p = g.get_params()
+        g.close()
+        key = "mu_v" if method == "vb" else "v"
+        return [s.rmse if method == "vb" else s.rmse_all for s in st], np.asarray(p[key])
+
+    fused = run("0", 0)
+    chunked = run("1", 4)
+    assert chunked[0] == fused[0]
+    np.testing.assert_array_equal(chunked[1], fused[1])

@@ -113,3 +113,65 @@ def test_entry_store_refused_where_it_cannot_apply(monkeypatch):
     g.synth_multihot(1, 500, 3000, 3, 20, 2, 0)
     g.init_caches()
     assert g.layout() == "column"
+
+
+@pytest.mark.parametrize("xmode", [0, 1])
+@pytest.mark.parametrize("form", ["deferred", "two_pass", "rccl_chunks"])
+def test_entry_store_split_forms_equal_fused(form, xmode, monkeypatch):
+    """The entry store under row shards (VBFM_FORCE_SPLIT=1 on one rank): deferred -- level l's
+    kernel applies each record's pending correction (its row's previous entry, from any earlier
+    level, through a posterior table over all level features; a row's first entry the previous
+    sweep's carried one), reduces, moves; two_pass -- statistics, all-reduce, correction + move
+    (VBFM_DEFER=0); rccl_chunks -- the deferred form through a 1-rank RCCL communicator with
+    each level's exchange in 3 chunks. Every form equals the fused single-rank entry store bit
+    for bit over three iterations (the same per-column order of every sum)."""
+    n, D, lo, hi, k = 20_000, 3000, 3, 40, 4
+
+    def run(split):
+        monkeypatch.setenv("VBFM_FORCE_SPLIT", split)
+        monkeypatch.setenv("VBFM_DEFER", "0" if form == "two_pass" else "1")
+        comm = split == "1" and form == "rccl_chunks"
+        monkeypatch.setenv("VBFM_FORCE_COMM", "1" if comm else "0")
+        monkeypatch.setenv("VBFM_AR_CHUNKS", "3")
+        g = vbfm.FMLearnVB(1, 1, k, D + 1, min_target=1.0, max_target=5.0, layout="entry")
+        if comm:
+            g.comm_init(1, 0, vbfm.FMLearnVB.comm_unique_id())
+        g.init(7, 0.1)
+        g.synth_multihot(0, n, D, lo, hi, 1000, xmode)
+        g.synth_multihot(1, 2000, D, lo, hi, 500000, xmode)
+        g.init_caches()
+        assert g.layout() == "entry"
+        st = [g.iterate() for _ in range(3)]
+        out = ([(s.rmse, s.free_energy, s.alpha, s.mu_0_dash, s.train_quirk) for s in st],
+               g.get_params()["mu_v"], g.rows()["e"])
+        g.close()
+        return out
+
+    fused, split = run("0"), run("1")
+    assert split[0] == fused[0]
+    np.testing.assert_array_equal(split[1], fused[1])
+    np.testing.assert_array_equal(split[2], fused[2])
+
+
+@pytest.mark.parametrize("method", ["als", "mcmc"])
+def test_entry_store_split_mcmc_equals_fused(method, monkeypatch):
+    """MCMC / ALS on the entry store under row shards (the two-pass split: statistics, all-reduce,
+    draw + move) with the device RNG streams: the fused single-rank chain bit for bit."""
+    n, D, lo, hi, k = 15_000, 2500, 3, 30, 3
+
+    def run(split):
+        monkeypatch.setenv("VBFM_FORCE_SPLIT", split)
+        g = vbfm.FMLearnMCMC(1, 1, k, D + 1, min_target=1.0, max_target=5.0, method=method, layout="entry")
+        g.init_device(7, 0.1)
+        g.synth_multihot(0, n, D, lo, hi, 1000, 1)
+        g.synth_multihot(1, 1500, D, lo, hi, 500000, 1)
+        g.init_caches()
+        assert g.layout() == "entry"
+        st = [g.iterate() for _ in range(3)]
+        out = ([s.rmse_all for s in st], g.get_params()["v"])
+        g.close()
+        return out
+
+    fused, split = run("0"), run("1")
+    assert split[0] == fused[0]
+    np.testing.assert_array_equal(split[1], fused[1])

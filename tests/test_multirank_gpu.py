@@ -56,6 +56,10 @@ def _data(kind):
             f[a:b], v[a:b] = f[a:b][order], v[a:b][order]
         rpt, ft, vt, yt = synth.generate(1500, F, S, 22, 1)
         return (rp, f, v, y), (rpt, ft, vt, yt), F * S
+    if kind == "multihot":   # rows of 3..30 distinct ids, no fields: the entry store's levels miss rows
+        tr = synth.generate_multihot(12000, 1500, 3, 30, 5, 1)
+        te = synth.generate_multihot(1500, 1500, 3, 30, 6, 1)
+        return tr, te, 1500
     N, F, S = 16000, 6, 250
     xmode = 0 if kind == "onehot" else 1   # onehot: every x 1 (no x array, 8-B deferred payloads)
     tr = synth.generate(N, F, S, 5, xmode)
@@ -169,17 +173,22 @@ def _rel(a, b):
     return float(np.max(np.abs(a - b)) / max(np.max(np.abs(b)), 1e-300))
 
 
-@pytest.mark.parametrize("world,kind,layout", [(2, "field", "level"), (3, "field", "level"), (2, "onehot", "level"),
-                                               (2, "field", "column"), (2, "ragged", "auto")])
-def test_vb_row_shards_match_one_rank(world, kind, layout):
+@pytest.mark.parametrize("world,kind,layout,chunks", [(2, "field", "level", 0), (3, "field", "level", 0),
+                                                      (2, "onehot", "level", 0), (2, "field", "column", 0),
+                                                      (2, "ragged", "auto", 0), (3, "field", "level", 3),
+                                                      (2, "field", "column", 2), (2, "multihot", "entry", 0),
+                                                      (3, "multihot", "entry", 2)])
+def test_vb_row_shards_match_one_rank(world, kind, layout, chunks, monkeypatch):
     """VB row shards (deferred split kernels on the level-ordered store, stats / correct on the
     column layout) vs the un-sharded data set: RMSE, free energy, alpha per iteration and the
-    final parameters within 1e-9."""
+    final parameters within 1e-9. chunks: each level's exchange cut into that many chunks
+    (VBFM_AR_CHUNKS, inherited by the rank processes)."""
+    if chunks:
+        monkeypatch.setenv("VBFM_AR_CHUNKS", str(chunks))
     s, r = _launch(world, kind, "vb", layout)
-    if kind == "ragged":   # row shards: the column layout; one rank: the entry store (auto)
-        assert s["layout"] == "column" and r["layout"] in ("column", "entry")
-    else:
-        assert s["layout"] == r["layout"]
+    # ragged rows: the levels miss rows (the entry store, or the column layout where a row repeats
+    # an id); every rank decides like the one-rank run (the repeat flags are all-reduced)
+    assert s["layout"] == r["layout"]
     assert s["levels"] == r["levels"]
     for key in ("rmse", "fe", "alpha"):
         for a, b in zip(s[key], r[key]):
@@ -189,7 +198,8 @@ def test_vb_row_shards_match_one_rank(world, kind, layout):
 
 
 @pytest.mark.parametrize("method,layout,kind", [("als", "level", "field"), ("als", "level", "onehot"),
-                                              ("als", "column", "field"), ("mcmc", "level", "field")])
+                                              ("als", "column", "field"), ("mcmc", "level", "field"),
+                                              ("als", "entry", "multihot"), ("mcmc", "entry", "multihot")])
 def test_mcmc_row_shards_match_one_rank(method, layout, kind):
     """MCMC / ALS row shards with the device RNG streams (keyed by seed, iteration, factor and
     attribute, so every rank draws the same numbers) vs one rank: ALS is deterministic
