@@ -1124,13 +1124,12 @@ void launch_mc_lord_ent(const McArgs &a, int is_w, hipStream_t s)
 	}
 }
 
-// the entry store runs the fused form only (one rank)
+// every mode on both stores: the entry store's next slots carry the row's-first-entry flag in
+// bit 31 (ENT_FIRST), which only the ENT kernels strip before the move
 template <int BLOCK, int R, int MODE>
 void launch_mc_lord(const McArgs &a, int is_w, hipStream_t s)
 {
-	if constexpr (MODE == 0) {
-		if (a.ent) return launch_mc_lord_ent<BLOCK, R, MODE, true>(a, is_w, s);
-	}
+	if (a.ent) return launch_mc_lord_ent<BLOCK, R, MODE, true>(a, is_w, s);
 	launch_mc_lord_ent<BLOCK, R, MODE, false>(a, is_w, s);
 }
 
