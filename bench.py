@@ -545,9 +545,11 @@ def main():
     }
     if cpu_leg is not None:
         result["cpu_baseline"] = cpu_leg()
-    fml.close()
-    if rank == 0:
+    if rank == 0:   # the line first: nothing in the teardown can cost it
         print(json.dumps(result), flush=True)
+    log("rank %d: closing" % rank)
+    fml.close()
+    log("rank %d: closed" % rank)
     if world > 1:
         dist.destroy_process_group()
 
