@@ -25,6 +25,7 @@ import pytest
 import oracle_ctypes as oc
 import synth
 import vbfm
+from conftest import load_case
 
 pytestmark = pytest.mark.gpu
 
