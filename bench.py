@@ -299,6 +299,13 @@ def main():
 
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
         sys.exit(spawn_ranks(args.gpus))
+    # stdout carries the JSON line only: native libraries write to fd 1 (RCCL prints a version
+    # banner when a communicator is created), so fd 1 goes to stderr for the whole run (each rank
+    # process does this itself: the launcher above hands its own stdout down) and the
+    # line is written to a saved copy of the real stdout
+    out = os.fdopen(os.dup(1), "w")
+    sys.stdout.flush()
+    os.dup2(2, 1)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
@@ -325,9 +332,10 @@ def main():
     tplan = shard_plan(max(cfg["rows"] // 100, 1000), world, rank, "features" if fshard else args.scaling)
     n_test, trow0 = tplan["rows"], tplan["row_offset"]
     if args.dry_run:
-        print(json.dumps({"rank": rank, "local_rank": local_rank, "world_size": world,
+        out.write(json.dumps({"rank": rank, "local_rank": local_rank, "world_size": world,
                           "master": "%s:%s" % (os.environ.get("MASTER_ADDR"), os.environ.get("MASTER_PORT")),
-                          "train": plan, "test": tplan, "config": args.config, "k": k}), flush=True)
+                          "train": plan, "test": tplan, "config": args.config, "k": k}) + "\n")
+        out.flush()
         return
 
     import numpy as np
@@ -546,7 +554,8 @@ def main():
     if cpu_leg is not None:
         result["cpu_baseline"] = cpu_leg()
     if rank == 0:   # the line first: nothing in the teardown can cost it
-        print(json.dumps(result), flush=True)
+        out.write(json.dumps(result) + "\n")
+        out.flush()
     log("rank %d: closing" % rank)
     fml.close()
     log("rank %d: closed" % rank)
