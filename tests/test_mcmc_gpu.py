@@ -81,8 +81,9 @@ def test_mcmc_als_chain_vs_reference(case, split, layout, synth_files, sa_split,
         expect = "column"
     elif case in COMPLETE:
         expect = "level"
-    else:   # levels that miss rows: the entry store (fused sweeps), unless a row lists a feature twice
-        expect = "column" if case.startswith("tiny_dup") or split == "split" else "entry"
+    else:   # levels that miss rows: the entry store (fused, or the two-pass split under row shards),
+        # unless a row lists a feature twice
+        expect = "column" if case.startswith("tiny_dup") else "entry"
     assert fml.layout() == expect
     for it, st in enumerate(stats):
         ref = t["trace"][it]
