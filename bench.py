@@ -492,7 +492,7 @@ def main():
     if online:
         kernel = "k_ov_lord" if stats[-1].n_lord_batches else "k_ov_v_level"
     elif mc:
-        kernel = "k_mc_level_lord" if layout == "level" else "k_mc_v_level"
+        kernel = {"level": "k_mc_level_lord", "entry": "k_mc_level_lord<ENT> (entry store)"}.get(layout, "k_mc_v_level")
     else:
         kernel = {"level": "k_level_lord", "entry": "k_level_lord<ENT> (entry store)"}.get(layout, "k_v_level_fused")
     # row shards (N > 1, or the multi-rank kernels forced on one GPU): a level is the split
@@ -503,7 +503,10 @@ def main():
         kernel = {"k_level_lord": "k_lord_defer + all-reduce + post (per level)",
                   "k_mc_level_lord": "k_mc_lord_defer + all-reduce + post (per level)",
                   "k_v_level_fused": "k_v_level_stats + all-reduce + k_v_level_correct (per level)",
-                  "k_mc_v_level": "k_mc_v_level stats + all-reduce + draw (per level)"}.get(kernel, kernel)
+                  "k_mc_v_level": "k_mc_v_level stats + all-reduce + draw (per level)",
+                  "k_level_lord<ENT> (entry store)": "entry store: statistics + all-reduce + move (per level)",
+                  "k_mc_level_lord<ENT> (entry store)": "entry store: statistics + all-reduce + draw / move "
+                                                        "(per level)"}.get(kernel, kernel)
     tlayout = ("level" if stats[-1].n_lord_batches else "column") if online else layout
     tf = os.path.join(ROOT, "profiles", "traffic_%s_%s%s.json" % (args.config, tlayout,
                                                                    "_" + args.method if mc or online else ""))

@@ -221,9 +221,10 @@ static void build_long_segs(vbfm_ctx *c, const std::vector<uint64_t> &lcp, const
 // rows in place (the column-gather layout: two random touches per entry).
 // No row listing a feature twice (VB and MCMC / ALS); the store must fit in half the free
 // memory. A row without entries parks its record in slot nnz + r. Row shards (split sweeps): the
-// VB sweep's deferred form reads each slot's previous-entry payload (k_estore_prev: the global
+// two-pass split (statistics, all-reduce, correction + move); VBFM_DEFER=1 takes the VB sweep's
+// deferred form, which reads each slot's previous-entry payload (k_estore_prev: the global
 // level-feature index and x of the row's previous entry) and a posterior table over all level
-// features; VBFM_DEFER=0 and the MCMC / ALS sweep take the two-pass split.
+// features.
 // Returns false when it does not apply (force: throw instead).
 bool build_estore(vbfm_ctx *c, const std::vector<uint64_t> &lcp, const std::vector<uint8_t> &dup,
                   const std::vector<uint32_t> &feats, bool force)
@@ -266,8 +267,12 @@ bool build_estore(vbfm_ctx *c, const std::vector<uint64_t> &lcp, const std::vect
 	HIPCHK(hipMemsetAsync(c->rows_alt, 0, (d.nnz + n) * sizeof(RowRec), c->s));
 	HIPCHK(vbk::estore_build(d.row_ptr, d.csr, d.col_ptr, d.csc, lv, c->lcp, n, d.nnz, c->lnext, c->lx, c->lpos0,
 	                         c->s));
+	// the entry store's split is two-pass by default: its short levels' records are still in L2 /
+	// MALL for the second pass, while the deferred form gathers a posterior per record from a
+	// table over all features (one GPU, multi-hot bench: 23.9 vs 26.1 us per level without a
+	// communicator, profiles/r03_multihot_split/); VBFM_DEFER=1 takes the deferred form
 	const char *df = getenv("VBFM_DEFER");
-	if ((c->row_comm() || c->force_split) && !(df && df[0] == '0')) {
+	if ((c->row_comm() || c->force_split) && df && df[0] == '1') {
 		uint32_t *pidx = dalloc<uint32_t>(d.nnz);
 		float *px = dalloc<float>(d.nnz);
 		HIPCHK(vbk::estore_prev(d.row_ptr, d.csr, d.col_ptr, d.csc, lv, c->lcp, n, pidx, px, c->s));
