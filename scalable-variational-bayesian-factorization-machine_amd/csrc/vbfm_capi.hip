@@ -645,15 +645,6 @@ void build_schedule(vbfm_ctx *c)
 		for (uint32_t i = c->level_ptr[l]; i < c->level_ptr[l + 1]; i++) z += cp[feats[i] + 1] - cp[feats[i]];
 		const uint32_t nfl = c->level_ptr[l + 1] - c->level_ptr[l];
 		c->level_avg[l] = nfl ? (uint32_t)std::min<uint64_t>(z / nfl, 0xFFFFFFFFu) : 0;
-		// VBFM_SHAPE_ROUNDS=1 (A/B): a level whose workgroups would not all be resident at once
-		// with the 256 x 2 shape (34 KB of LDS each: ~4 per CU) but would with 256 x 1 (~9 per
-		// CU) takes 256 x 1 -- one round of workgroups instead of a second, mostly idle one. The
-		// shape is a function of the level's avg_len, the same for every kernel and layout
-		const char *sr = getenv("VBFM_SHAPE_ROUNDS");
-		if (sr && sr[0] == '1') {
-			const uint32_t a = c->level_avg[l];
-			if (a > 320 && a <= 640 && nfl > 4u * 256u && nfl <= 9u * 256u) c->level_avg[l] = 320;
-		}
 	}
 	uint32_t maxlev = 0;
 	for (uint32_t l = 0; l < L; l++) maxlev = std::max(maxlev, c->level_ptr[l + 1] - c->level_ptr[l]);
