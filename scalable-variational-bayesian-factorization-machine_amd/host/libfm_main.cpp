@@ -203,12 +203,22 @@ struct Rank {
 		uint32_t lo, hi;
 		range(h.num_rows, &lo, &hi);
 		s.cp.assign((size_t)h.num_feature + 1, 0);
-		for (uint32_t j = 0; j < h.num_feature; j++) {
+		auto run = [&](uint32_t j, const vbfm_entry **a, const vbfm_entry **z) {
 			const vbfm_entry *b = h.col_ent + h.col_ptr[j], *e = h.col_ent + h.col_ptr[j + 1];
-			const vbfm_entry *a = std::lower_bound(b, e, lo, [](const vbfm_entry &x, uint32_t r) { return x.id < r; });
-			const vbfm_entry *z = std::lower_bound(a, e, hi, [](const vbfm_entry &x, uint32_t r) { return x.id < r; });
-			for (const vbfm_entry *p = a; p < z; p++) s.ent.push_back(vbfm_entry{p->id - lo, p->value});
-			s.cp[j + 1] = s.ent.size();
+			*a = std::lower_bound(b, e, lo, [](const vbfm_entry &x, uint32_t r) { return x.id < r; });
+			*z = std::lower_bound(*a, e, hi, [](const vbfm_entry &x, uint32_t r) { return x.id < r; });
+		};
+		for (uint32_t j = 0; j < h.num_feature; j++) {   // the slice's column pointers, then its entries
+			const vbfm_entry *a, *z;
+			run(j, &a, &z);
+			s.cp[j + 1] = s.cp[j] + (uint64_t)(z - a);
+		}
+		s.ent.resize(s.cp[h.num_feature]);
+		for (uint32_t j = 0; j < h.num_feature; j++) {
+			const vbfm_entry *a, *z;
+			run(j, &a, &z);
+			vbfm_entry *o = s.ent.data() + s.cp[j];
+			for (const vbfm_entry *p = a; p < z; p++) *o++ = vbfm_entry{p->id - lo, p->value};
 		}
 		s.y.assign(h.target + lo, h.target + hi);
 		s.csc = vbfm_csc{hi - lo, h.num_feature, (uint64_t)s.ent.size(), s.cp.data(), s.ent.data(), s.y.data()};
