@@ -1,5 +1,6 @@
 #!/usr/bin/env python3
-"""Generate tests/golden/c3_k50/ from the COMPILED REFERENCE at BASELINE config 3's own size.
+"""Generate tests/golden/c3_k50/ (and c4_k100_r1e7/) from the COMPILED REFERENCE at the
+BASELINE configs' own sizes.
 
 C3: 1e7 train rows x 40 one-hot fields x 25,000 ids (D = 1e6 + 1), nnz 4e8,
 k = 50; test = 1e5 rows. Data: tests/synth.py `generate` (train seed 1000, test seed 500000,
@@ -18,7 +19,12 @@ item 2), the sum and sum of squares of every array, all hyper parameters, and th
 initial test prediction). The GPU test (tests/test_configs_gpu.py) regenerates the same data on
 the device (bit-exact generator) and compares.
 
-Usage: python tests/golden/make_c3_k50.py [--iter 2] [--ref oracle/_ref/ref_driver]
+Case c4_k100_r1e7: config 4's feature space and k (40 one-hot fields x 125,000 ids, D = 5e6 + 1,
+k = 100) on the first 1e7 rows of the bench's own C4 data set (train seed 1000, x = 1; test: the
+first 1e5 rows of its test set, seed 500000) -- the full 1e8 rows need more memory than the
+build container has and ~9 h per reference iteration; one iteration here takes ~2.5 h.
+
+Usage: python tests/golden/make_c3_k50.py [--case c3_k50|c4_k100_r1e7] [--iter 2] [--ref ...]
 """
 import argparse
 import json
@@ -36,9 +42,15 @@ sys.path.insert(0, os.path.dirname(HERE))
 import synth  # noqa: E402
 from make_golden import parse_vb  # noqa: E402
 
-SPEC = {"n_rows": 10_000_000, "n_fields": 40, "ids_per_field": 25_000, "seed": 1000, "xmode": 1,
-        "test_rows": 100_000, "test_seed": 500000, "model_seed": synth.MODEL_SEED,
-        "dim": "1,1,50", "init_stdev": 0.1, "ref_seed": 3}
+CASES = {
+    "c3_k50": {"n_rows": 10_000_000, "n_fields": 40, "ids_per_field": 25_000, "seed": 1000, "xmode": 1,
+               "test_rows": 100_000, "test_seed": 500000, "model_seed": synth.MODEL_SEED,
+               "dim": "1,1,50", "init_stdev": 0.1, "ref_seed": 3},
+    "c4_k100_r1e7": {"n_rows": 10_000_000, "n_fields": 40, "ids_per_field": 125_000, "seed": 1000, "xmode": 0,
+                     "test_rows": 100_000, "test_seed": 500000, "model_seed": synth.MODEL_SEED,
+                     "dim": "1,1,100", "init_stdev": 0.1, "ref_seed": 3},
+}
+SPEC = CASES["c3_k50"]
 N_SAMPLE = 4096
 
 
@@ -51,12 +63,13 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--ref", default=os.path.join(HERE, "..", "..", "oracle", "_ref", "ref_driver"))
     ap.add_argument("--iter", type=int, default=2)
+    ap.add_argument("--case", default="c3_k50", choices=sorted(CASES))
     ap.add_argument("--tmp", default="")
     args = ap.parse_args()
     ref = os.path.abspath(args.ref)
     tmp = args.tmp or tempfile.mkdtemp(prefix="c3k50_")
     os.makedirs(tmp, exist_ok=True)
-    s = SPEC
+    s = CASES[args.case]
     F, S = s["n_fields"], s["ids_per_field"]
     t0 = time.time()
     if not os.path.exists(os.path.join(tmp, "train.y")):
@@ -95,11 +108,11 @@ def main():
             samples[name] = a[idx]
         else:
             samples[name] = a
-    out = os.path.join(HERE, "c3_k50")
+    out = os.path.join(HERE, args.case)
     os.makedirs(out, exist_ok=True)
     with open(os.path.join(out, "trace.json"), "w") as fh:
         json.dump({"nums": nums, "trace": trace, "array_sums": sums,
-                   "meta": dict(SPEC, iter=args.iter, ref_seconds=ref_s,
+                   "meta": dict(s, iter=args.iter, ref_seconds=ref_s,
                                 generator="tests/golden/make_c3_k50.py")}, fh, indent=1)
     np.savez_compressed(os.path.join(out, "arrays.npz"), **samples)
     print("fixture written under", out, flush=True)
