@@ -243,7 +243,18 @@ def test_c3_k50_two_iterations_vs_reference():
     regenerates the data (bit-exact generator) and draws the reference's initial parameters
     (glibc rand + Leva, seed 3); RMSE, MAE, the train quirk, F, alpha, mu_0', the parameter
     sums and samples within 1e-9 relative (fm_learn_vb_simultaneous.h:125, 143-222)."""
-    t, a = load_case("c3_k50")
+    _vs_reference("c3_k50")
+
+
+def test_c4_k100_first_1e7_rows_vs_reference():
+    """C4's feature space (40 x 125,000 ids, D = 5e6 + 1) and k = 100 on the first 1e7 rows of
+    the bench's C4 data set, one iteration against the compiled reference
+    (tests/golden/c4_k100_r1e7, same checks as C3 above)."""
+    _vs_reference("c4_k100_r1e7")
+
+
+def _vs_reference(case):
+    t, a = load_case(case)
     m, nums = t["meta"], t["nums"]
     n, F, S, k = m["n_rows"], m["n_fields"], m["ids_per_field"], int(m["dim"].split(",")[2])
     D = int(nums["D"])
