@@ -813,10 +813,10 @@ static int launch(const Job &job, Data &train, Data &test, Rank proto, const std
 		if (!ok && failed < 0) {
 			failed = (int)(it - pids.begin());
 			status_failed = status;
-			for (pid_t q : pids)
-				if (q != pid) kill(q, SIGKILL);
+			for (pid_t q : pids)   // the ranks still running; a reaped one is 0 (never kill(-1 or 0, ...))
+				if (q > 0 && q != pid) kill(q, SIGKILL);
 		}
-		*it = -1;
+		*it = 0;
 	}
 	pthread_barrier_destroy(&shm->bar);
 	munmap(mem, bytes);
