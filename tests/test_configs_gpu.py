@@ -10,6 +10,9 @@
 * C4 (1e8 x 40 x 125,000 ids) at its own k = 100: two iterations on every kernel form the
   sizes select -- level and column layouts, fused and deferred-split (row-shard) kernels --
   agree to summation order; the split form is the fused one bit for bit; F finite, RMSE falls.
+  C4's feature space and k = 100 on the first 1e7 rows of that data set: one iteration against
+  the compiled reference (tests/golden/c4_k100_r1e7, make_c3_k50.py --case c4_k100_r1e7; the
+  reference ran 2.4 h on one core here).
 * C5: the MCMC Gibbs sweep with device RNG streams at C4 size, k = 100: the fused and the
   row-shard split kernels draw the same chain bit for bit; ALS (no sampling) on the level
   and column layouts agrees to summation order.
