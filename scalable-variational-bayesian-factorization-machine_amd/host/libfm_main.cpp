@@ -11,7 +11,7 @@
 //   * -method sgd/sgda/... and -task c are rejected with an error instead of running
 //     other learners; -relation is not supported;
 //   * extra flags: -device (HIP ordinal), -vfile 0 (skip writing v_file.txt), -save_state /
-//     -resume (checkpoints), and the multi-GPU launch: -devices N | o0,o1,..., -shard
+//     -resume (checkpoints), -parity_log (17-digit JSON lines per iteration), and the multi-GPU launch: -devices N | o0,o1,..., -shard
 //     rows|features, -transport rccl|host, -plan 1 (print the ranks' shard plan, no GPU).
 //
 // Multi-GPU (-devices): the reference is one process on one core. Here this process parses the
@@ -126,6 +126,54 @@ private:
 	std::ostream *out;
 	std::vector<std::string> header;
 	std::map<std::string, double> value;
+};
+
+// -parity_log FILE ("Metrics / logging"): one JSON line per iteration from rank 0 with
+// the values the reference prints, at 17 significant digits (its test_rmse_* / free_energy_*
+// files carry 6, too few for a 1e-6 comparison), the device time of the phases, and the factor
+// sweep's throughput: nnz*k per second of ms_v over the whole job and, per GPU, the fraction of
+// the 8 TB/s HBM roofline by SURVEY §8d's bytes model (VB B = 128 nnz + 24 N + 32 D per factor,
+// MCMC / ALS 72 nnz + 8 N + 16 D). Non-finite values are written as null.
+class ParityLog {
+public:
+	ParityLog(const std::string &path, bool lead)
+	{
+		if (path.empty() || !lead) return;
+		f = fopen(path.c_str(), "w");
+		if (!f) throw std::string("Unable to open file " + path);
+	}
+	~ParityLog() { if (f) fclose(f); }
+	ParityLog(const ParityLog &) = delete;
+	ParityLog &operator=(const ParityLog &) = delete;
+	bool on() const { return f != nullptr; }
+	void begin(const char *method, uint32_t it)
+	{
+		line = std::string("\"method\": \"") + method + "\"";
+		num("iter", (double)it);
+	}
+	void num(const char *key, double v)
+	{
+		char b[48];
+		if (std::isfinite(v)) snprintf(b, sizeof(b), "%.17g", v);
+		else snprintf(b, sizeof(b), "null");
+		line += std::string(", \"") + key + "\": " + b;
+	}
+	// the factor sweep of one iteration: ms_v of rank 0, the whole job's nnz, rows and features
+	void sweep(double ms_v, int k, uint64_t nnz, uint32_t rows, uint32_t nf, int ranks, bool mcmc)
+	{
+		const double s = ms_v * 1e-3;
+		const double bytes = mcmc ? 72.0 * nnz + 8.0 * rows + 16.0 * nf : 128.0 * nnz + 24.0 * rows + 32.0 * nf;
+		num("sweep_nnz_k_per_s", s > 0 ? (double)nnz * k / s : NAN);
+		num("hbm_frac_per_gpu", s > 0 ? bytes * k / ranks / s / 8e12 : NAN);
+	}
+	void end()
+	{
+		fprintf(f, "{%s}\n", line.c_str());
+		fflush(f);
+	}
+private:
+	FILE *f = nullptr;
+	std::string line;
 };
 
 double usertime()
@@ -304,7 +352,7 @@ struct McmcRun {
 	uint32_t G, D;
 	int k0, k1, k;
 	bool vfile;
-	std::string rlog_file, out_file;
+	std::string rlog_file, out_file, parity_file;
 };
 
 static void run_mcmc(const McmcRun &r, Data &train, Data &test, const Rank &rk)
@@ -360,6 +408,7 @@ static void run_mcmc(const McmcRun &r, Data &train, Data &test, const Rank &rk)
 		tag << r.k0 << r.k1 << r.k;
 		const std::string f_rmse = "test_rmse_" + tag.str() + "_mcmc";
 		if (rk.lead()) { std::ofstream a(f_rmse.c_str()); }   // truncate (:52-62)
+		ParityLog plog(r.parity_file, rk.lead());
 		for (uint32_t it = 0; it < r.num_iter; it++) {
 			const double t_user = usertime();
 			const clock_t t_clock = clock();
@@ -399,6 +448,18 @@ static void run_mcmc(const McmcRun &r, Data &train, Data &test, const Rank &rk)
 			}
 			std::cout << "#Iter=" << std::setw(3) << it << "\tTrain=" << st.train_rmse << "\tTest=" << st.rmse_all
 			          << std::endl;
+			if (plog.on()) {
+				plog.begin(r.sample ? "mcmc" : "als", it);
+				const double vals[] = {st.train_rmse, st.rmse_all, st.mae_all, st.rmse_this, st.mae_this, st.alpha, st.w0,
+				                       st.ms_hyper, st.ms_w, st.ms_v, st.ms_predict, st.ms_total};
+				const char *keys[] = {"train", "test_rmse", "test_mae", "test_rmse_this", "test_mae_this", "alpha", "w0",
+				                      "ms_hyper", "ms_w", "ms_v", "ms_predict", "ms_total"};
+				for (size_t i = 0; i < sizeof(vals) / sizeof(vals[0]); i++) plog.num(keys[i], vals[i]);
+				plog.num("levels", st.num_levels);
+				plog.num("rng_skipped", st.rng_skipped);
+				plog.sweep(st.ms_v, r.k, train.h.nnz, train.h.num_rows, train.h.num_feature, rk.nranks, true);
+				plog.end();
+			}
 			if (rk.lead()) {
 				std::ofstream fr(f_rmse.c_str(), std::ios_base::app);
 				fr << st.rmse_all << "\n";
@@ -459,7 +520,7 @@ struct OnlineRun {
 	uint32_t G, D;
 	int k0, k1, k;
 	bool vfile;
-	std::string rlog_file, out_file;
+	std::string rlog_file, out_file, parity_file;
 };
 
 static void run_online(const OnlineRun &r, Data &train, Data &test, const Rank &rk)
@@ -508,6 +569,7 @@ static void run_online(const OnlineRun &r, Data &train, Data &test, const Rank &
 		// free energies are appended to free_energy_..._vb (fm_learn_vb_online.h:636-662)
 		const std::string f_rmse = "test_rmse_" + tag.str() + "_vb_online", f_fe = "free_energy_" + tag.str() + "_vb";
 		{ std::ofstream a(f_rmse.c_str()); std::ofstream b(("free_energy_" + tag.str() + "_vb_online").c_str()); }
+		ParityLog plog(r.parity_file, true);
 		for (uint32_t it = 0; it < r.num_iter; it++) {
 			const double t_user = usertime();
 			const clock_t t_clock = clock();
@@ -535,6 +597,20 @@ static void run_online(const OnlineRun &r, Data &train, Data &test, const Rank &
 			std::ofstream fr(f_rmse.c_str(), std::ios_base::app);
 			fr << st.rmse << "\n";
 			std::cout << "#Iter=" << std::setw(3) << it << "\tTest=" << st.rmse << std::endl;
+			if (plog.on()) {
+				plog.begin("vb_online", it);
+				const double vals[] = {st.rmse, st.mae, st.free_energy_first, st.free_energy_last, st.alpha, st.sigma_0,
+				                       st.mu_0_dash, st.sigma_0_dash, st.ms_regroup, st.ms_predict, st.ms_w0, st.ms_w,
+				                       st.ms_v, st.ms_hyper, st.ms_test, st.ms_total};
+				const char *keys[] = {"test_rmse", "test_mae", "free_energy_first", "free_energy_last", "alpha", "sigma_0",
+				                      "mu_0_dash", "sigma_0_dash", "ms_regroup", "ms_predict", "ms_w0", "ms_w", "ms_v",
+				                      "ms_hyper", "ms_test", "ms_total"};
+				for (size_t i = 0; i < sizeof(vals) / sizeof(vals[0]); i++) plog.num(keys[i], vals[i]);
+				plog.num("levels", st.num_levels);
+				plog.num("level_launches", st.n_vlevel_launches);
+				plog.num("sweep_nnz_k_per_s", st.ms_v > 0 ? (double)train.h.nnz * r.k / (st.ms_v * 1e-3) : NAN);
+				plog.end();
+			}
 		}
 		std::cout << "after learn" << std::endl;                              // libfm.cpp:507
 		std::cout << "Final\tTrain=" << NAN << "\tTest=" << NAN << std::endl;   // evaluate() is NaN (:17)
@@ -562,7 +638,7 @@ struct VbRun {
 	uint32_t G, D;
 	int k0, k1, k;
 	bool vfile;
-	std::string rlog_file, out_file, save_file, resume_file;
+	std::string rlog_file, out_file, save_file, resume_file, parity_file;
 };
 
 static void run_vb(const VbRun &r, Data &train, Data &test, const Rank &rk)
@@ -637,6 +713,7 @@ static void run_vb(const VbRun &r, Data &train, Data &test, const Rank &rk)
 		tag << r.k0 << r.k1 << k;
 		const std::string f_rmse = "test_rmse_" + tag.str() + "_vb", f_fe = "free_energy_" + tag.str() + "_vb";
 		if (!resume && rk.lead()) { std::ofstream a(f_rmse.c_str()); std::ofstream b(f_fe.c_str()); }   // truncate (:58-73); a resumed run appends
+		ParityLog plog(r.parity_file, rk.lead());
 		for (uint32_t it = it0; it < it0 + r.num_iter; it++) {
 			time_t now = time(0);
 			std::cout << ctime(&now) << std::endl;
@@ -666,6 +743,23 @@ static void run_vb(const VbRun &r, Data &train, Data &test, const Rank &rk)
 				fr << st.rmse << "\n";
 			}
 			std::cout << "#Iter=" << std::setw(3) << it << "\tTrain=" << st.train_quirk << "\tTest=" << st.rmse << std::endl;
+			if (plog.on()) {
+				plog.begin("vb", it);
+				const double vals[] = {st.train_quirk, st.rmse, st.mae, st.free_energy_valid ? st.free_energy : NAN, st.alpha,
+				                       st.sigma_0, st.mu_0_dash, st.sigma_0_dash, st.ms_w0, st.ms_w, st.ms_qcache, st.ms_v,
+				                       st.ms_hyper, st.ms_test, st.ms_total};
+				const char *keys[] = {"train", "test_rmse", "test_mae", "free_energy", "alpha", "sigma_0", "mu_0_dash",
+				                      "sigma_0_dash", "ms_w0", "ms_w", "ms_qcache", "ms_v", "ms_hyper", "ms_test", "ms_total"};
+				for (size_t i = 0; i < sizeof(vals) / sizeof(vals[0]); i++) plog.num(keys[i], vals[i]);
+				const uint32_t nans[] = {st.nan_mu_w, st.nan_sigma_w, st.inf_mu_w, st.nan_mu_v, st.nan_sigma_v, st.inf_mu_v,
+				                         st.nan_alpha, st.inf_alpha};
+				const char *nkeys[] = {"nan_mu_w", "nan_sigma_w", "inf_mu_w", "nan_mu_v", "nan_sigma_v", "inf_mu_v",
+				                       "nan_alpha", "inf_alpha"};
+				for (size_t i = 0; i < sizeof(nans) / sizeof(nans[0]); i++) plog.num(nkeys[i], nans[i]);
+				plog.num("levels", st.num_levels);
+				plog.sweep(st.ms_v, k, train.h.nnz, train.h.num_rows, train.h.num_feature, rk.nranks, false);
+				plog.end();
+			}
 		}
 		if (!r.save_file.empty())
 			check(vbfm_save_state(ctx, rk.rank_file(r.save_file).c_str(), it0 + r.num_iter), ctx);
@@ -869,6 +963,7 @@ int main(int argc, char **argv)
 		const std::string p_plan = cmd.reg("plan", "1: every rank prints its launch and shard plan as JSON and exits (no GPU)");
 		const std::string p_vfile = cmd.reg("vfile", "write v_file.txt like the reference (1) or not (0); default=1");
 		const std::string p_save = cmd.reg("save_state", "vb: write the learner's state to this file after the last iteration (.<rank> per rank with -devices)");
+		const std::string p_plog = cmd.reg("parity_log", "one JSON line per iteration: the printed values at 17 digits, phase times, sweep nnz*k/s and HBM roofline fraction; default=''");
 		const std::string p_resume = cmd.reg("resume", "vb: continue from a -save_state file (same data and -dim) instead of the initial draws");
 		if (cmd.has(p_help) || argc == 1) { cmd.print_help(); return 0; }
 		cmd.check();
@@ -947,17 +1042,19 @@ int main(int argc, char **argv)
 		const bool vfile = cmd.geti(p_vfile, 1) != 0;
 		const std::string rlog = cmd.has(p_rlog) ? cmd.get(p_rlog) : std::string();
 		const std::string out = cmd.has(p_out) ? cmd.get(p_out) : std::string();
+		const std::string plog = cmd.has(p_plog) ? cmd.get(p_plog) : std::string();
 
 		Job job;
 		job.method = method;
 		job.plan = cmd.geti(p_plan, 0) != 0;
 		job.online = OnlineRun{seed, init_stdev, num_iter, (uint32_t)cmd.geti(p_batch, 50), gp, G, D, k0, k1, k, vfile,
-		                       rlog, out};
+		                       rlog, out, plog};
 		std::vector<double> reg;
 		for (const std::string &r : cmd.list(p_reg)) reg.push_back(atof(r.c_str()));
-		job.mc = McmcRun{method == "mcmc", seed, init_stdev, num_iter, reg, gp, G, D, k0, k1, k, vfile, rlog, out};
+		job.mc = McmcRun{method == "mcmc", seed, init_stdev, num_iter, reg, gp, G, D, k0, k1, k, vfile, rlog, out, plog};
 		job.vb = VbRun{seed, init_stdev, num_iter, gp, G, D, k0, k1, k, vfile, rlog, out,
-		               cmd.has(p_save) ? cmd.get(p_save) : std::string(), cmd.has(p_resume) ? cmd.get(p_resume) : std::string()};
+		               cmd.has(p_save) ? cmd.get(p_save) : std::string(), cmd.has(p_resume) ? cmd.get(p_resume) : std::string(),
+		               plog};
 
 		if (proto.nranks == 1) {   // one GPU, this process
 			run_rank(job, train, test, proto);

@@ -24,7 +24,15 @@ k = 100) on the first 1e7 rows of the bench's own C4 data set (train seed 1000, 
 first 1e5 rows of its test set, seed 500000) -- the full 1e8 rows need more memory than the
 build container has and ~9 h per reference iteration; one iteration here takes ~2.5 h.
 
-Usage: python tests/golden/make_c3_k50.py [--case c3_k50|c4_k100_r1e7] [--iter 2] [--ref ...]
+Cases c5_mcmc_k100_r1e7 / c5_als_k100_r1e7 (config 5): the same data as c4_k100_r1e7, run through
+the reference's fm_learn_mcmc_simultaneous (ref_driver mcmc | als, fm_learn_mcmc_simultaneous.h:
+50-305) with k = 100, seed 3, init_stdev 0.1, no -regular, one iteration: the per-iteration
+"#Iter=" trace at 17 digits (train quirk, test RMSE of the averaged prediction), w0 and alpha,
+the sums and 4096 sampled values of the final v, w and hyper-priors (w_mu, w_lambda, v_mu,
+v_lambda).
+
+Usage: python tests/golden/make_c3_k50.py [--case c3_k50|c4_k100_r1e7|c5_mcmc_k100_r1e7|c5_als_k100_r1e7]
+       [--iter 2] [--ref ...] [--tmp DIR (data kept there, shared between cases)]
 """
 import argparse
 import json
@@ -40,7 +48,7 @@ import numpy as np
 HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.dirname(HERE))
 import synth  # noqa: E402
-from make_golden import parse_vb  # noqa: E402
+from make_golden import parse_mcmc, parse_vb  # noqa: E402
 
 CASES = {
     "c3_k50": {"n_rows": 10_000_000, "n_fields": 40, "ids_per_field": 25_000, "seed": 1000, "xmode": 1,
@@ -50,6 +58,12 @@ CASES = {
                      "test_rows": 100_000, "test_seed": 500000, "model_seed": synth.MODEL_SEED,
                      "dim": "1,1,100", "init_stdev": 0.1, "ref_seed": 3},
 }
+for _mode in ("mcmc", "als"):
+    CASES["c5_%s_k100_r1e7" % _mode] = dict(CASES["c4_k100_r1e7"], mode=_mode)
+MCMC_ARRAYS = ("final_fm_v", "final_fm_w", "final_mcmc_scalars", "final_w_mu", "final_w_lambda", "final_v_mu",
+               "final_v_lambda")
+VB_ARRAYS = ("final_mu_w", "final_sigma_w", "final_mu_v", "final_sigma_v", "final_hyp_sigma_w",
+             "final_hyp_sigma_v", "final_scalars", "init_mu_w", "init_mu_v", "init_e", "init_t", "init_test_e")
 SPEC = CASES["c3_k50"]
 N_SAMPLE = 4096
 
@@ -67,7 +81,7 @@ def main():
     ap.add_argument("--tmp", default="")
     args = ap.parse_args()
     ref = os.path.abspath(args.ref)
-    tmp = args.tmp or tempfile.mkdtemp(prefix="c3k50_")
+    tmp = os.path.abspath(args.tmp or tempfile.mkdtemp(prefix="c3k50_"))
     os.makedirs(tmp, exist_ok=True)
     s = CASES[args.case]
     F, S = s["n_fields"], s["ids_per_field"]
@@ -80,26 +94,25 @@ def main():
         synth.write_binary(os.path.join(tmp, "test"), F * S, rp, f, v, y)
         del rp, f, v, y
     print("data written in %.0f s" % (time.time() - t0), flush=True)
-    dump = os.path.join(tmp, "dump")
+    dump = os.path.join(tmp, "dump_" + args.case)
     os.makedirs(dump, exist_ok=True)
     t0 = time.time()
-    cmd = [ref, "vb", "--train", os.path.join(tmp, "train"), "--test", os.path.join(tmp, "test"),
+    mode = s.get("mode", "vb")
+    cmd = [ref, mode, "--train", os.path.join(tmp, "train"), "--test", os.path.join(tmp, "test"),
            "--dim", s["dim"], "--iter", str(args.iter), "--seed", str(s["ref_seed"]),
            "--init_stdev", str(s["init_stdev"]), "--dump", dump]
     res = subprocess.run(cmd, cwd=tmp, capture_output=True, text=True, check=True)
     ref_s = time.time() - t0
     print("reference run %.0f s" % ref_s, flush=True)
-    with open(os.path.join(tmp, "ref_stdout.txt"), "w") as fh:
+    with open(os.path.join(tmp, "ref_stdout_%s.txt" % args.case), "w") as fh:
         fh.write(res.stdout)
-    nums, trace = parse_vb(res.stdout)
+    nums, trace = (parse_vb if mode == "vb" else parse_mcmc)(res.stdout)
 
     def load(name):
         return np.fromfile(os.path.join(dump, name + ".f64"), dtype="<f8")
 
     sums, samples = {}, {}
-    for name in ("final_mu_w", "final_sigma_w", "final_mu_v", "final_sigma_v", "final_hyp_sigma_w",
-                 "final_hyp_sigma_v", "final_scalars", "init_mu_w", "init_mu_v", "init_e", "init_t",
-                 "init_test_e"):
+    for name in (VB_ARRAYS if mode == "vb" else MCMC_ARRAYS):
         a = load(name)
         sums[name] = [float(np.sum(a)), float(np.sum(a * a)), int(a.size)]
         if a.size > N_SAMPLE:

@@ -177,3 +177,30 @@ def test_cli_online_matches_reference(case, init, tmp_path, monkeypatch):
     np.testing.assert_allclose(vf.ravel(), a["init_fm_v"], rtol=1e-5, atol=1e-7)
     np.testing.assert_allclose(np.loadtxt(tmp_path / "pred.txt"), a["final_pred"], rtol=1e-5)
     assert "Final\tTrain=nan\tTest=nan" in stdout
+
+
+@pytest.mark.parametrize("case", ["tiny/vb", "tiny/mcmc", "tiny/als"])
+def test_cli_parity_log_17_digits(case, tmp_path):
+    """-parity_log: one JSON line per iteration with the values the reference prints at 17
+    digits, against the compiled reference's trace at 1e-9 (the 6-digit files cannot carry that),
+    plus the sweep's throughput fields."""
+    import json
+    t, _ = load_case(case)
+    m = t["meta"]
+    d = os.path.join(GOLDEN, case.split("/")[0])
+    method = case.split("/")[1]
+    run_cli(tmp_path, os.path.join(d, "train.libfm"), os.path.join(d, "test.libfm"), m["dim"], m["iter"], m["seed"],
+            ["-init_stdev", str(m["init_stdev"]), "-parity_log", "parity.jsonl", "-vfile", "0"], method=method)
+    lines = [json.loads(x) for x in open(tmp_path / "parity.jsonl")]
+    assert len(lines) == m["iter"]
+    for it, (got, ref) in enumerate(zip(lines, t["trace"])):
+        assert got["iter"] == it and got["method"] == method
+        pairs = [("train", "train")]
+        if method == "vb":
+            pairs += [("test_rmse", "rmse"), ("test_mae", "mae"), ("alpha", "alpha"), ("mu_0_dash", "mu_0_dash"),
+                      ("sigma_0_dash", "sigma_0_dash"), ("free_energy", "free_energy")]
+        else:
+            pairs += [("test_rmse", "rmse_all")]
+        for gk, rk in pairs:
+            assert abs(got[gk] - ref[rk]) <= 1e-9 * max(abs(ref[rk]), 1e-300), (it, gk, got[gk], ref[rk])
+        assert got["ms_v"] > 0 and got["sweep_nnz_k_per_s"] > 0 and 0 < got["hbm_frac_per_gpu"] < 1

@@ -297,3 +297,48 @@ def _vs_reference(case):
         assert np.asarray(p[key]).size == size
         close([np.sum(p[key]), np.sum(np.asarray(p[key]) ** 2)], [s, s2])
     g.close()
+
+
+@pytest.mark.parametrize("method", ["mcmc", "als"])
+def test_c5_k100_first_1e7_rows_vs_reference(method):
+    """Config 5 (-method mcmc, k = 100) on the first 1e7 rows of the bench's C4 data set, one
+    iteration against the compiled reference's fm_learn_mcmc_simultaneous run on the same data
+    (tests/golden/c5_{mcmc,als}_k100_r1e7, make_c3_k50.py). The library takes every random
+    number from the reference's own stream (glibc rand, Leva normals, Marsaglia-Tsang gammas in
+    the reference's order: the initial v draws, w0, every w_j and v_{f,j}, alpha and the
+    hyper-prior draws), so the Gibbs chain follows the reference's; the per-iteration Train= /
+    Test= values, w0, alpha, the sums and 4096 sampled values of v, w and the hyper-priors
+    within 1e-9 relative (fm_learn_mcmc_simultaneous.h:134,152-175; fm_learn_mcmc.h:411-623)."""
+    _mc_vs_reference("c5_%s_k100_r1e7" % method)
+
+
+def _mc_vs_reference(case):
+    t, a = load_case(case)
+    m, nums = t["meta"], t["nums"]
+    n, F, S, k = m["n_rows"], m["n_fields"], m["ids_per_field"], int(m["dim"].split(",")[2])
+    D = int(nums["D"])
+    g = vbfm.FMLearnMCMC(1, 1, k, D, min_target=nums["min_target"], max_target=nums["max_target"],
+                         method=m["mode"])
+    g.init(m["ref_seed"], m["init_stdev"], rng=vbfm.RNG_REFERENCE)
+    g.synth(0, n, F, S, m["seed"], m["xmode"], m["model_seed"])
+    g.synth(1, m["test_rows"], F, S, m["test_seed"], m["xmode"], m["model_seed"])
+    assert g.shape(0) == (n, F * S, n * F)
+    g.init_caches()
+    for it in range(m["iter"]):
+        st = g.iterate()
+        ref = t["trace"][it]
+        assert st.rng_skipped == 0
+        close([st.rmse_all], [ref["rmse_all"]])
+        close([st.train_rmse], [ref["train"]])
+    p = g.get_params()
+    got = {"final_fm_v": p["v"], "final_fm_w": p["w"], "final_mcmc_scalars": [p["w0"], p["alpha"]],
+           "final_w_mu": p["w_mu"], "final_w_lambda": p["w_lambda"], "final_v_mu": p["v_mu"],
+           "final_v_lambda": p["v_lambda"]}
+    for name, arr in got.items():
+        arr = np.ravel(np.asarray(arr, dtype=np.float64))
+        vals = _sampled(arr, a[name + "__idx"]) if name + "__idx" in a else arr
+        close(vals, a[name])
+        s, s2, size = t["array_sums"][name]
+        assert arr.size == size, (name, arr.size, size)
+        close([np.sum(arr), np.sum(arr * arr)], [s, s2])
+    g.close()
