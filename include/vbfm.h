@@ -217,7 +217,12 @@ int vbfm_set_profiling(vbfm_ctx *ctx, int32_t on);   /* on > 1: time every on-th
  * to one file. vbfm_load_state, on a context created with the same configuration, rank and
  * train data (checked: shape and a fingerprint of the train CSC and targets; the test set is
  * free), replaces vbfm_init_caches and the run continues bit for bit. iter: the caller's
- * iteration count, stored and returned. VB learner (vbfm_iterate) only. */
+ * iteration count, stored and returned. An MCMC / ALS context (vbfm_mcmc_init) writes its
+ * chain instead -- the RNG (mode, seed, completed iterations, the reference stream's position),
+ * the parameters, hyper-priors, w0, alpha, the test predictions and their running sum, the
+ * train row caches -- and vbfm_load_state on a context initialised the same way (vbfm_mcmc_init
+ * with the same method and RNG mode; it replaces vbfm_mcmc_init_caches) continues the chain bit
+ * for bit. Not the online learner. */
 int vbfm_save_state(vbfm_ctx *ctx, const char *path, uint32_t iter);
 int vbfm_load_state(vbfm_ctx *ctx, const char *path, uint32_t *iter);
 

@@ -1702,8 +1702,9 @@ int vbfm_get_test_pred(vbfm_ctx *c, double *pred)
 // fm_learn_vb_simultaneous.h:20) and keeps no state on disk. Between two vbfm_iterate calls the
 // VB learner's state is the parameters, the hyper parameters, the four scalars and the train
 // row records (row order; their q-cache slots are rebuilt inside the next sweeps, they are kept
-// only so that a resumed context holds the same bytes).
-namespace {
+// only so that a resumed context holds the same bytes). An MCMC / ALS context writes its own
+// payload behind the same header (vbi::mc_state_*, vbfm_mcmc_capi.hip).
+namespace vbi {
 
 struct StateHeader {
 	char magic[8];        // "VBFMST01"
@@ -1722,6 +1723,7 @@ struct StateHeader {
 };
 static_assert(sizeof(StateHeader) == 104, "checkpoint header layout");
 constexpr char STATE_MAGIC[8] = {'V', 'B', 'F', 'M', 'S', 'T', '0', '1'};
+constexpr char MC_STATE_MAGIC[8] = {'V', 'B', 'F', 'M', 'M', 'C', '0', '1'};   // MCMC / ALS payload
 constexpr size_t IO_CHUNK = (size_t)64 << 20;
 
 uint64_t train_fingerprint(vbfm_ctx *c)
@@ -1767,25 +1769,8 @@ uint64_t state_payload(vbfm_ctx *c)
 	       (uint64_t)c->tr.n * sizeof(RowRec);
 }
 
-struct File {
-	FILE *f;
-	std::string path;
-	File(const char *p, const char *mode) : f(fopen(p, mode)), path(p)
-	{
-		if (!f) throw std::string("cannot open checkpoint file ") + p;
-	}
-	~File() { if (f) fclose(f); }
-	void write(const void *p, size_t n)
-	{
-		if (n && fwrite(p, 1, n, f) != n) throw std::string("short write to ") + path;
-	}
-	void read(void *p, size_t n)
-	{
-		if (n && fread(p, 1, n, f) != n) throw std::string("checkpoint file truncated: ") + path;
-	}
-};
 
-void dev_to_file(vbfm_ctx *c, File &f, const void *d, size_t bytes)
+void dev_to_file(vbfm_ctx *c, CkptFile &f, const void *d, size_t bytes)
 {
 	std::vector<uint8_t> buf(std::min(bytes, IO_CHUNK));
 	for (size_t o = 0; o < bytes; o += IO_CHUNK) {
@@ -1796,7 +1781,7 @@ void dev_to_file(vbfm_ctx *c, File &f, const void *d, size_t bytes)
 	}
 }
 
-void file_to_dev(vbfm_ctx *c, File &f, void *d, size_t bytes)
+void file_to_dev(vbfm_ctx *c, CkptFile &f, void *d, size_t bytes)
 {
 	std::vector<uint8_t> buf(std::min(bytes, IO_CHUNK));
 	for (size_t o = 0; o < bytes; o += IO_CHUNK) {
@@ -1809,11 +1794,11 @@ void file_to_dev(vbfm_ctx *c, File &f, void *d, size_t bytes)
 
 void require_vb_state(vbfm_ctx *c, const char *fn)
 {
-	if (c->mc || c->ov) throw std::string(fn) + ": the VB learner's state only (not MCMC / ALS / online)";
+	if (c->ov) throw std::string(fn) + ": the VB and MCMC / ALS learners' state only (not the online learner)";
 	require_train(c);
 }
 
-}  // namespace
+}  // namespace vbi
 
 extern "C" {
 
@@ -1824,27 +1809,33 @@ int vbfm_save_state(vbfm_ctx *c, const char *path, uint32_t iter)
 		require_vb_state(c, "vbfm_save_state");
 		no_partial(c);
 		StateHeader h = state_header(c, iter);
+		if (c->mc) memcpy(h.magic, MC_STATE_MAGIC, 8);
 		h.level_order = c->rows_lorder ? 1 : 0;
 		rows_row_order(c);
 		// written beside the target and renamed over it once complete and on disk: a failed
 		// or interrupted save never destroys the previous checkpoint (-resume X -save_state X)
 		const std::string tmp = std::string(path) + ".tmp";
 		try {
-			File f(tmp.c_str(), "wb");
+			CkptFile f(tmp.c_str(), "wb");
 			f.write(&h, sizeof(h));
-			dev_to_file(c, f, c->ms_w, (size_t)c->D * sizeof(double2));
-			dev_to_file(c, f, c->ms_v, (size_t)c->k * c->D * sizeof(double2));
-			f.write(c->hyp_w.data(), c->hyp_w.size() * 8);
-			f.write(c->hyp_v.data(), c->hyp_v.size() * 8);
-			const double sc[4] = {c->alpha, c->sigma_0, c->mu0, c->s0d};
-			f.write(sc, sizeof(sc));
-			dev_to_file(c, f, c->rows, (size_t)c->tr.n * sizeof(RowRec));
+			if (c->mc) {
+				mc_state_write(c, f);
+			} else {
+				dev_to_file(c, f, c->ms_w, (size_t)c->D * sizeof(double2));
+				dev_to_file(c, f, c->ms_v, (size_t)c->k * c->D * sizeof(double2));
+				f.write(c->hyp_w.data(), c->hyp_w.size() * 8);
+				f.write(c->hyp_v.data(), c->hyp_v.size() * 8);
+				const double sc[4] = {c->alpha, c->sigma_0, c->mu0, c->s0d};
+				f.write(sc, sizeof(sc));
+				dev_to_file(c, f, c->rows, (size_t)c->tr.n * sizeof(RowRec));
+			}
 			if (fflush(f.f) != 0 || fsync(fileno(f.f)) != 0) throw std::string("short write to ") + tmp;
 			if (fclose(f.f) != 0) { f.f = nullptr; throw std::string("short write to ") + tmp; }
 			f.f = nullptr;
 			if (rename(tmp.c_str(), path) != 0) throw std::string("cannot rename ") + tmp + " to " + path;
 		} catch (...) {
 			unlink(tmp.c_str());
+			if (h.level_order) rows_level_order(c);
 			throw;
 		}
 		if (h.level_order) rows_level_order(c);   // the run goes on exactly as without the save
@@ -1857,11 +1848,15 @@ int vbfm_load_state(vbfm_ctx *c, const char *path, uint32_t *iter)
 	return guarded(c, [&] {
 		require_vb_state(c, "vbfm_load_state");
 		no_partial(c);
-		File f(path, "rb");
+		CkptFile f(path, "rb");
 		StateHeader h;
 		f.read(&h, sizeof(h));
-		if (memcmp(h.magic, STATE_MAGIC, 8) != 0 || h.version != 2)
-			throw std::string("not a libvbfm VB checkpoint (version 2): ") + path;
+		const bool mc_file = memcmp(h.magic, MC_STATE_MAGIC, 8) == 0;
+		if ((!mc_file && memcmp(h.magic, STATE_MAGIC, 8) != 0) || h.version != 2)
+			throw std::string("not a libvbfm checkpoint (version 2): ") + path;
+		if (mc_file != (c->mc != nullptr))
+			throw std::string(mc_file ? "an MCMC / ALS checkpoint: resume it in an MCMC / ALS context"
+			                          : "a VB checkpoint: resume it in a VB context");
 		if (h.k0 != c->k0 || h.k1 != c->k1 || h.k != c->k || h.D != c->D || h.G != c->G)
 			throw std::string("checkpoint of another model configuration (-dim / num_attribute / groups)");
 		if (h.nranks != c->nranks || h.rank != c->rank)
@@ -1872,25 +1867,28 @@ int vbfm_load_state(vbfm_ctx *c, const char *path, uint32_t *iter)
 		if (h.layout != state_layout(c))
 			throw std::string("checkpoint of another row layout or shard mode (the data-set sums would add the rows in "
 			                  "another order): resume with the same VBFM_LAYOUT / vbfm_set_layout and shard mode");
+		if (h.level_order && !c->lord) throw std::string("checkpoint of a level-ordered run: resume with the same row layout");
 		// the whole file is there before any state is replaced
-		if (fseek(f.f, 0, SEEK_END) != 0 || (uint64_t)ftell(f.f) != sizeof(h) + state_payload(c) ||
+		const uint64_t payload = mc_file ? mc_state_payload(c) : state_payload(c);
+		if (fseek(f.f, 0, SEEK_END) != 0 || (uint64_t)ftell(f.f) != sizeof(h) + payload ||
 		    fseek(f.f, (long)sizeof(h), SEEK_SET) != 0)
 			throw std::string("checkpoint file truncated or of another size: ") + path;
 		rows_row_order(c);
-		file_to_dev(c, f, c->ms_w, (size_t)c->D * sizeof(double2));
-		file_to_dev(c, f, c->ms_v, (size_t)c->k * c->D * sizeof(double2));
-		f.read(c->hyp_w.data(), c->hyp_w.size() * 8);
-		f.read(c->hyp_v.data(), c->hyp_v.size() * 8);
-		upload_hyp(c);
-		double sc[4];
-		f.read(sc, sizeof(sc));
-		c->alpha = sc[0]; c->sigma_0 = sc[1]; c->mu0 = sc[2]; c->s0d = sc[3];
-		file_to_dev(c, f, c->rows, (size_t)c->tr.n * sizeof(RowRec));
-		c->rows_lorder = false;
-		if (h.level_order) {
-			if (!c->lord) throw std::string("checkpoint of a level-ordered run: resume with the same row layout");
-			rows_level_order(c);
+		if (mc_file) {
+			mc_state_read(c, f);
+		} else {
+			file_to_dev(c, f, c->ms_w, (size_t)c->D * sizeof(double2));
+			file_to_dev(c, f, c->ms_v, (size_t)c->k * c->D * sizeof(double2));
+			f.read(c->hyp_w.data(), c->hyp_w.size() * 8);
+			f.read(c->hyp_v.data(), c->hyp_v.size() * 8);
+			upload_hyp(c);
+			double sc[4];
+			f.read(sc, sizeof(sc));
+			c->alpha = sc[0]; c->sigma_0 = sc[1]; c->mu0 = sc[2]; c->s0d = sc[3];
+			file_to_dev(c, f, c->rows, (size_t)c->tr.n * sizeof(RowRec));
 		}
+		c->rows_lorder = false;
+		if (h.level_order) rows_level_order(c);
 		c->q_ready[0] = c->q_ready[1] = -1;
 		c->carry = 0;
 		sync(c);

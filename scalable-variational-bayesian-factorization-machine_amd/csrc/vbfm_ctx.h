@@ -7,6 +7,7 @@
 
 #include <rccl/rccl.h>
 #include <rocprofiler-sdk-roctx/roctx.h>
+#include <cstdio>
 #include <cstdlib>
 
 #include <string>
@@ -302,5 +303,32 @@ void lord_release(vbfm_ctx *c, bool keep_rows);
 void rows_level_order(vbfm_ctx *c);   // records in level-0 order before a sweep (no-op without the store)
 void rows_dense(vbfm_ctx *c);         // records N-dense for the data-set sums (row order from the entry store)
 void rows_row_order(vbfm_ctx *c);     // records back in row order (row-indexed kernels, readback)   // level-ordered store freed (rows back to row order)
+
+// checkpoint files (vbfm_save_state / vbfm_load_state, vbfm_capi.hip): whole-buffer I/O that
+// throws on a short read or write, device buffers staged through the host in 64 MB pieces
+struct CkptFile {
+	FILE *f;
+	std::string path;
+	CkptFile(const char *p, const char *mode) : f(fopen(p, mode)), path(p)
+	{
+		if (!f) throw std::string("cannot open checkpoint file ") + p;
+	}
+	~CkptFile() { if (f) fclose(f); }
+	void write(const void *p, size_t n)
+	{
+		if (n && fwrite(p, 1, n, f) != n) throw std::string("short write to ") + path;
+	}
+	void read(void *p, size_t n)
+	{
+		if (n && fread(p, 1, n, f) != n) throw std::string("checkpoint file truncated: ") + path;
+	}
+};
+void dev_to_file(vbfm_ctx *c, CkptFile &f, const void *d, size_t bytes);
+void file_to_dev(vbfm_ctx *c, CkptFile &f, void *d, size_t bytes);
+// the MCMC / ALS learner's part of a checkpoint (vbfm_mcmc_capi.hip): its payload size, and the
+// payload written / read behind the common header (the caller has put the records in row order)
+uint64_t mc_state_payload(vbfm_ctx *c);
+void mc_state_write(vbfm_ctx *c, CkptFile &f);
+void mc_state_read(vbfm_ctx *c, CkptFile &f);
 
 }  // namespace vbi

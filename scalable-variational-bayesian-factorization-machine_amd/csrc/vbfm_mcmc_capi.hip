@@ -725,3 +725,78 @@ int vbfm_mcmc_factor_sweep(vbfm_ctx *c, double *ms_device)
 }
 
 }  // extern "C"
+
+// ---- checkpoint / resume of the MCMC / ALS learner (vbfm_save_state / vbfm_load_state) ------
+// The reference keeps no state on disk (num_complete_iter = 0, fm_learn_mcmc_simultaneous.h:
+// 50-83). Between two vbfm_mcmc_iterate calls the chain's state is: the RNG (mode, seed, the
+// completed iterations, which key the device streams, and the reference stream's 31-word
+// window), the parameters as stored ({value, 0} pairs), the hyper-priors, w0, alpha, reg0, the
+// test predictions of the last iteration and their running sum (pred_this / pred_sum: "Test="
+// is the mean over all iterations, :152-175) and the train row records (e = yhat - y of the
+// last re-prediction; the q-caches are rebuilt inside the next sweep). The RNG block comes
+// first so that a file of another method or RNG mode is refused before any state is replaced.
+namespace vbi {
+
+namespace {
+constexpr size_t MC_RNG_WORDS = 8 + 32;   // {sample, multilevel, rng, seed, iter, 0, 0, 0}, window + pad
+}
+
+uint64_t mc_state_payload(vbfm_ctx *c)
+{
+	const uint64_t D = c->D, kd = (uint64_t)c->k * c->D, G = c->G, gk = G * (uint64_t)c->k;
+	return MC_RNG_WORDS * 4 + D * 16 + kd * 16 + (2 * G + 2 * gk) * 8 + 3 * 8 + 2 * (uint64_t)c->te.n * 8 +
+	       (uint64_t)c->tr.n * sizeof(RowRec);
+}
+
+void mc_state_write(vbfm_ctx *c, CkptFile &f)
+{
+	McState &m = mc(c);
+	if (!m.caches || !m.pred_sum) throw std::string("vbfm_save_state: vbfm_mcmc_init_caches first");
+	uint32_t w[MC_RNG_WORDS] = {};
+	w[0] = (uint32_t)m.sample; w[1] = (uint32_t)m.multilevel; w[2] = (uint32_t)m.rng; w[3] = m.seed; w[4] = m.iter;
+	m.stream.chrono_state(w + 8);
+	f.write(w, sizeof(w));
+	dev_to_file(c, f, c->ms_w, (size_t)c->D * sizeof(double2));
+	dev_to_file(c, f, c->ms_v, (size_t)c->k * c->D * sizeof(double2));
+	f.write(m.w_mu.data(), G_(c) * 8);
+	f.write(m.w_lambda.data(), G_(c) * 8);
+	f.write(m.v_mu.data(), GK(c) * 8);
+	f.write(m.v_lambda.data(), GK(c) * 8);
+	const double sc[3] = {m.w0, m.alpha, m.reg0};
+	f.write(sc, sizeof(sc));
+	dev_to_file(c, f, m.pred_this, (size_t)c->te.n * 8);
+	dev_to_file(c, f, m.pred_sum, (size_t)c->te.n * 8);
+	dev_to_file(c, f, c->rows, (size_t)c->tr.n * sizeof(RowRec));
+}
+
+void mc_state_read(vbfm_ctx *c, CkptFile &f)
+{
+	McState &m = mc(c);
+	uint32_t w[MC_RNG_WORDS];
+	f.read(w, sizeof(w));
+	if (w[0] != (uint32_t)m.sample || w[1] != (uint32_t)m.multilevel)
+		throw std::string("checkpoint of another method (mcmc vs als): resume with the same -method");
+	if (w[2] != (uint32_t)m.rng) throw std::string("checkpoint of another RNG mode (VBFM_RNG_REFERENCE / _DEVICE)");
+	if (c->te.n && !c->e_test) throw std::string("no test data set (vbfm_set_test)");
+	if (!m.pred_sum) require_test(c);
+	if (m.col_nonempty.empty()) scan_columns(c);
+	m.seed = w[3];
+	m.iter = w[4];
+	m.stream.set_chrono_state(w + 8);
+	file_to_dev(c, f, c->ms_w, (size_t)c->D * sizeof(double2));
+	file_to_dev(c, f, c->ms_v, (size_t)c->k * c->D * sizeof(double2));
+	f.read(m.w_mu.data(), G_(c) * 8);
+	f.read(m.w_lambda.data(), G_(c) * 8);
+	f.read(m.v_mu.data(), GK(c) * 8);
+	f.read(m.v_lambda.data(), GK(c) * 8);
+	upload_hyper(c);
+	double sc[3];
+	f.read(sc, sizeof(sc));
+	m.w0 = sc[0]; m.alpha = sc[1]; m.reg0 = sc[2];
+	file_to_dev(c, f, m.pred_this, (size_t)c->te.n * 8);
+	file_to_dev(c, f, m.pred_sum, (size_t)c->te.n * 8);
+	file_to_dev(c, f, c->rows, (size_t)c->tr.n * sizeof(RowRec));
+	m.caches = true;
+}
+
+}  // namespace vbi

@@ -352,7 +352,7 @@ struct McmcRun {
 	uint32_t G, D;
 	int k0, k1, k;
 	bool vfile;
-	std::string rlog_file, out_file, parity_file;
+	std::string rlog_file, out_file, parity_file, save_file, resume_file;
 };
 
 static void run_mcmc(const McmcRun &r, Data &train, Data &test, const Rank &rk)
@@ -373,7 +373,8 @@ static void run_mcmc(const McmcRun &r, Data &train, Data &test, const Rank &rk)
 		const size_t kd = (size_t)r.k * r.D, gk = (size_t)r.G * r.k;
 		std::vector<double> w(r.D), v(kd), wmu(r.G), wl(r.G), vmu(gk), vl(gk);
 		vbfm_mcmc_params p{w.data(), v.data(), wmu.data(), wl.data(), vmu.data(), vl.data(), 0, 0, 0};
-		if (r.vfile && rk.lead()) {   // fm_model.h:98: the initial factors (DMatrix::save, matrix.h:129-152)
+		const bool resume = !r.resume_file.empty();
+		if (r.vfile && rk.lead() && !resume) {   // fm_model.h:98: the initial factors (DMatrix::save, matrix.h:129-152)
 			check(vbfm_mcmc_get_params(ctx, &p), ctx);
 			std::ofstream vf("v_file.txt");
 			for (int f = 0; f < r.k; f++) {
@@ -403,13 +404,21 @@ static void run_mcmc(const McmcRun &r, Data &train, Data &test, const Rank &rk)
 			rlog->init();
 		}
 		std::cout << "in mcmc learn" << std::endl << "preprocess complete" << std::endl;
-		check(vbfm_mcmc_init_caches(ctx), ctx);
+		// -resume: the chain's state from the file instead of the initial caches (the initial
+		// draws above are replaced by the file's parameters and RNG position)
+		uint32_t it0 = 0;
+		if (resume) {
+			check(vbfm_load_state(ctx, rk.rank_file(r.resume_file).c_str(), &it0), ctx);
+			std::cout << "resuming from " << r.resume_file << " after " << it0 << " iterations" << std::endl;
+		} else {
+			check(vbfm_mcmc_init_caches(ctx), ctx);
+		}
 		std::ostringstream tag;
 		tag << r.k0 << r.k1 << r.k;
 		const std::string f_rmse = "test_rmse_" + tag.str() + "_mcmc";
-		if (rk.lead()) { std::ofstream a(f_rmse.c_str()); }   // truncate (:52-62)
+		if (rk.lead() && !resume) { std::ofstream a(f_rmse.c_str()); }   // truncate (:52-62); a resumed run appends
 		ParityLog plog(r.parity_file, rk.lead());
-		for (uint32_t it = 0; it < r.num_iter; it++) {
+		for (uint32_t it = it0; it < it0 + r.num_iter; it++) {
 			const double t_user = usertime();
 			const clock_t t_clock = clock();
 			const double t_wall = (double)time(NULL);
@@ -465,12 +474,14 @@ static void run_mcmc(const McmcRun &r, Data &train, Data &test, const Rank &rk)
 				fr << st.rmse_all << "\n";
 			}
 		}
+		if (!r.save_file.empty())
+			check(vbfm_save_state(ctx, rk.rank_file(r.save_file).c_str(), it0 + r.num_iter), ctx);
 		std::cout << "after learn" << std::endl;   // libfm.cpp:507; no Final line for mcmc (:509)
 		if (!r.out_file.empty()) {                 // libfm.cpp:514-519
 			uint32_t lo, hi;
 			rk.range(test.h.num_rows, &lo, &hi);
 			std::vector<double> pred(hi - lo), all;
-			check(vbfm_mcmc_get_test_pred(ctx, (int32_t)r.num_iter, pred.data()), ctx);
+			check(vbfm_mcmc_get_test_pred(ctx, (int32_t)(it0 + r.num_iter), pred.data()), ctx);
 			gather_test(rk, test, pred, &all);
 			if (rk.lead()) {
 				std::ofstream o(r.out_file.c_str());
@@ -962,9 +973,9 @@ int main(int argc, char **argv)
 		const std::string p_trans = cmd.reg("transport", "rank exchange: rccl (one GPU per rank, default) or host (shared memory; ranks may share a GPU)");
 		const std::string p_plan = cmd.reg("plan", "1: every rank prints its launch and shard plan as JSON and exits (no GPU)");
 		const std::string p_vfile = cmd.reg("vfile", "write v_file.txt like the reference (1) or not (0); default=1");
-		const std::string p_save = cmd.reg("save_state", "vb: write the learner's state to this file after the last iteration (.<rank> per rank with -devices)");
+		const std::string p_save = cmd.reg("save_state", "vb, mcmc, als: write the learner's state to this file after the last iteration (.<rank> per rank with -devices)");
 		const std::string p_plog = cmd.reg("parity_log", "one JSON line per iteration: the printed values at 17 digits, phase times, sweep nnz*k/s and HBM roofline fraction; default=''");
-		const std::string p_resume = cmd.reg("resume", "vb: continue from a -save_state file (same data and -dim) instead of the initial draws");
+		const std::string p_resume = cmd.reg("resume", "vb, mcmc, als: continue from a -save_state file (same data and -dim) instead of the initial draws");
 		if (cmd.has(p_help) || argc == 1) { cmd.print_help(); return 0; }
 		cmd.check();
 
@@ -1051,7 +1062,8 @@ int main(int argc, char **argv)
 		                       rlog, out, plog};
 		std::vector<double> reg;
 		for (const std::string &r : cmd.list(p_reg)) reg.push_back(atof(r.c_str()));
-		job.mc = McmcRun{method == "mcmc", seed, init_stdev, num_iter, reg, gp, G, D, k0, k1, k, vfile, rlog, out, plog};
+		job.mc = McmcRun{method == "mcmc", seed, init_stdev, num_iter, reg, gp, G, D, k0, k1, k, vfile, rlog, out, plog,
+		                 cmd.has(p_save) ? cmd.get(p_save) : std::string(), cmd.has(p_resume) ? cmd.get(p_resume) : std::string()};
 		job.vb = VbRun{seed, init_stdev, num_iter, gp, G, D, k0, k1, k, vfile, rlog, out,
 		               cmd.has(p_save) ? cmd.get(p_save) : std::string(), cmd.has(p_resume) ? cmd.get(p_resume) : std::string(),
 		               plog};

@@ -1,4 +1,4 @@
-"""Checkpoint / resume of the VB learner (include/vbfm.h vbfm_save_state / vbfm_load_state).
+"""Checkpoint / resume of the VB and MCMC / ALS learners (include/vbfm.h vbfm_save_state / vbfm_load_state).
 
 The reference has no counterpart (it always starts from its initial draws,
 fm_learn_vb_simultaneous.h:20): the contract is that a run stopped after i iterations and
@@ -102,7 +102,7 @@ def test_load_refuses_other_model_or_data(tmp_path):
     bad = tmp_path / "bad.state"
     bad.write_bytes(b"\0" * 200)
     h = _learner(tr, te, nf, 3, "auto")
-    with pytest.raises(vbfm.VbfmError, match="not a libvbfm VB checkpoint"):
+    with pytest.raises(vbfm.VbfmError, match="not a libvbfm checkpoint"):
         h.load_state(str(bad))
     h.close()
 
@@ -184,3 +184,124 @@ def test_failed_save_keeps_the_previous_checkpoint(tmp_path):
         g.save_state(path)
     assert open(path, "rb").read() == before
     g.close()
+
+
+def _mc_learner(tr, te, nf, k, method, rng, layout):
+    rp, f, v, y = tr
+    g = vbfm.FMLearnMCMC(1, 1, k, nf + 1, min_target=float(y.min()), max_target=float(y.max()), method=method,
+                         layout=layout)
+    g.init(7, 0.1, rng=rng)
+    g.set_data(vbfm.DataSubset.from_csr(rp, f, v, y, nf), vbfm.DataSubset.from_csr(*te, nf))
+    return g
+
+
+def _mc_trace(stats):
+    return [(s.rmse_all, s.mae_all, s.rmse_this, s.train_rmse, s.alpha, s.w0, s.rng_skipped) for s in stats]
+
+
+MC_CASES = [("mcmc", "reference", "level", "0"), ("mcmc", "device", "level", "0"), ("mcmc", "reference", "level", "1"),
+            ("mcmc", "device", "column", "0"), ("als", "reference", "level", "0"), ("mcmc", "reference", "entry", "0")]
+
+
+@pytest.mark.parametrize("method,rng,layout,split", MC_CASES)
+def test_mcmc_resume_continues_bit_for_bit(method, rng, layout, split, tmp_path, monkeypatch):
+    """The MCMC / ALS chain: 4 iterations in one go against 2 + save, then load into a fresh
+    context + 2. Test= is the running mean over all iterations (fm_learn_mcmc_simultaneous.h:
+    152-175) and the reference stream continues where it stopped, so every later value, the
+    final parameters, the hyper-priors and the averaged test prediction are equal bit for bit
+    (reference glibc stream and device streams; level store, column layout, entry store;
+    fused and split sweeps)."""
+    monkeypatch.setenv("VBFM_FORCE_SPLIT", split)
+    if layout == "entry":
+        tr = synth.generate_multihot(8000, 1500, 3, 30, 41, 1)
+        te = synth.generate_multihot(800, 1500, 3, 30, 42, 1)
+        nf = 1500
+    else:
+        tr, te, nf = _data()
+    r = vbfm.RNG_REFERENCE if rng == "reference" else vbfm.RNG_DEVICE
+    k = 4
+    a = _mc_learner(tr, te, nf, k, method, r, layout)
+    a.init_caches()
+    full = [a.iterate() for _ in range(4)]
+    pa, preda = a.get_params(), a.predict()
+    a.close()
+
+    b = _mc_learner(tr, te, nf, k, method, r, layout)
+    b.init_caches()
+    first = [b.iterate() for _ in range(2)]
+    path = str(tmp_path / "mc.state")
+    b.save_state(path)
+    b.close()
+
+    c = _mc_learner(tr, te, nf, k, method, r, layout)
+    assert c.load_state(path) == 2
+    assert c.layout() == layout
+    rest = [c.iterate() for _ in range(2)]
+    pc, predc = c.get_params(), c.predict()
+    c.close()
+    assert _mc_trace(first + rest) == _mc_trace(full)
+    for key in ("w", "v", "w_mu", "w_lambda", "v_mu", "v_lambda", "w0", "alpha"):
+        np.testing.assert_array_equal(np.asarray(pc[key]), np.asarray(pa[key]), err_msg=key)
+    np.testing.assert_array_equal(predc, preda)
+
+
+def test_mcmc_load_refuses_other_learner_method_or_rng(tmp_path):
+    tr, te, nf = _data(n=5000)
+    g = _mc_learner(tr, te, nf, 3, "mcmc", vbfm.RNG_REFERENCE, "auto")
+    g.init_caches()
+    g.iterate()
+    path = str(tmp_path / "mc.state")
+    g.save_state(path)
+    g.close()
+    h = _learner(tr, te, nf, 3, "auto")   # a VB context
+    with pytest.raises(vbfm.VbfmError, match="MCMC / ALS checkpoint"):
+        h.load_state(path)
+    h.close()
+    h = _mc_learner(tr, te, nf, 3, "als", vbfm.RNG_REFERENCE, "auto")
+    with pytest.raises(vbfm.VbfmError, match="another method"):
+        h.load_state(path)
+    h.close()
+    h = _mc_learner(tr, te, nf, 3, "mcmc", vbfm.RNG_DEVICE, "auto")
+    with pytest.raises(vbfm.VbfmError, match="another RNG mode"):
+        h.load_state(path)
+    h.close()
+    v = _learner(tr, te, nf, 3, "auto")
+    v.init_caches()
+    v.iterate()
+    vpath = str(tmp_path / "vb.state")
+    v.save_state(vpath)
+    v.close()
+    h = _mc_learner(tr, te, nf, 3, "mcmc", vbfm.RNG_REFERENCE, "auto")
+    with pytest.raises(vbfm.VbfmError, match="a VB checkpoint"):
+        h.load_state(vpath)
+    h.close()
+
+
+@pytest.mark.parametrize("method", ["mcmc", "als"])
+def test_cli_mcmc_save_state_and_resume(method, tmp_path):
+    """bin/libFM -method mcmc | als: 3 iterations + -save_state, then -resume for 3 more: the
+    appended test_rmse file, the #Iter lines and -out (the mean of the clipped draws over all 6
+    iterations) equal the 6-iteration run's."""
+    d = os.path.join(GOLDEN, "tiny")
+    import subprocess
+
+    def run(cwd, iters, extra):
+        os.makedirs(cwd, exist_ok=True)
+        out = subprocess.run([CLI, "-task", "r", "-train", os.path.join(d, "train.libfm"), "-test",
+                              os.path.join(d, "test.libfm"), "-method", method, "-dim", "1,1,3", "-iter", str(iters),
+                              "-seed", "5", "-init_stdev", "0.1", "-regular", "0.5,1,2"] + extra,
+                             cwd=str(cwd), capture_output=True, text=True, timeout=300)
+        assert "ERROR" not in out.stderr, out.stderr
+        return out.stdout
+
+    one = tmp_path / "one"
+    s_one = run(one, 6, ["-out", "pred.txt"])
+    two = tmp_path / "two"
+    run(two, 3, ["-save_state", "mc.state"])
+    s_two = run(two, 3, ["-resume", "mc.state", "-out", "pred.txt"])
+    fn = "test_rmse_113_mcmc"
+    assert open(one / fn).read() == open(two / fn).read()
+    assert open(one / "pred.txt").read() == open(two / "pred.txt").read()
+    it_one = re.findall(r"#Iter=\s*(\d+)\tTrain=(\S+)\tTest=(\S+)", s_one)
+    it_two = re.findall(r"#Iter=\s*(\d+)\tTrain=(\S+)\tTest=(\S+)", s_two)
+    assert len(it_one) == 6 and it_two == it_one[3:]
