@@ -332,7 +332,9 @@ def _mc_vs_reference(case):
         ref = t["trace"][it]
         assert st.rng_skipped == 0
         close([st.rmse_all], [ref["rmse_all"]])
-        close([st.train_rmse], [ref["train"]])
+        # ALS without -regular fits the 1e7 train rows almost exactly (5e8 parameters): Train= is
+        # ~1e-8, a difference of residuals of targets ~3, so it is held to 1e-9 of the target scale
+        assert abs(st.train_rmse - ref["train"]) <= REL * max(abs(ref["train"]), 1.0), (st.train_rmse, ref["train"])
     p = g.get_params()
     got = {"final_fm_v": p["v"], "final_fm_w": p["w"], "final_mcmc_scalars": [p["w0"], p["alpha"]],
            "final_w_mu": p["w_mu"], "final_w_lambda": p["w_lambda"], "final_v_mu": p["v_mu"],
