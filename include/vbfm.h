@@ -222,7 +222,8 @@ int vbfm_set_profiling(vbfm_ctx *ctx, int32_t on);   /* on > 1: time every on-th
  * the parameters, hyper-priors, w0, alpha, the test predictions and their running sum, the
  * train row caches -- and vbfm_load_state on a context initialised the same way (vbfm_mcmc_init
  * with the same method and RNG mode; it replaces vbfm_mcmc_init_caches) continues the chain bit
- * for bit. Not the online learner. */
+ * for bit. An online context (vbfm_online_init with the same -batch) saves between epochs:
+ * parameters, natural parameters, step sizes, the rand() stream and the last permutation. */
 int vbfm_save_state(vbfm_ctx *ctx, const char *path, uint32_t iter);
 int vbfm_load_state(vbfm_ctx *ctx, const char *path, uint32_t *iter);
 

@@ -1724,6 +1724,11 @@ struct StateHeader {
 static_assert(sizeof(StateHeader) == 104, "checkpoint header layout");
 constexpr char STATE_MAGIC[8] = {'V', 'B', 'F', 'M', 'S', 'T', '0', '1'};
 constexpr char MC_STATE_MAGIC[8] = {'V', 'B', 'F', 'M', 'M', 'C', '0', '1'};   // MCMC / ALS payload
+constexpr char OV_STATE_MAGIC[8] = {'V', 'B', 'F', 'M', 'O', 'V', '0', '1'};   // online VB payload
+
+// the learner a checkpoint belongs to: 0 VB, 1 MCMC / ALS, 2 online VB
+int state_kind(const vbfm_ctx *c) { return c->mc ? 1 : c->ov ? 2 : 0; }
+const char *state_magic(int kind) { return kind == 1 ? MC_STATE_MAGIC : kind == 2 ? OV_STATE_MAGIC : STATE_MAGIC; }
 constexpr size_t IO_CHUNK = (size_t)64 << 20;
 
 uint64_t train_fingerprint(vbfm_ctx *c)
@@ -1794,7 +1799,7 @@ void file_to_dev(vbfm_ctx *c, CkptFile &f, void *d, size_t bytes)
 
 void require_vb_state(vbfm_ctx *c, const char *fn)
 {
-	if (c->ov) throw std::string(fn) + ": the VB and MCMC / ALS learners' state only (not the online learner)";
+	(void)fn;
 	require_train(c);
 }
 
@@ -1809,7 +1814,7 @@ int vbfm_save_state(vbfm_ctx *c, const char *path, uint32_t iter)
 		require_vb_state(c, "vbfm_save_state");
 		no_partial(c);
 		StateHeader h = state_header(c, iter);
-		if (c->mc) memcpy(h.magic, MC_STATE_MAGIC, 8);
+		memcpy(h.magic, state_magic(state_kind(c)), 8);
 		h.level_order = c->rows_lorder ? 1 : 0;
 		rows_row_order(c);
 		// written beside the target and renamed over it once complete and on disk: a failed
@@ -1820,6 +1825,8 @@ int vbfm_save_state(vbfm_ctx *c, const char *path, uint32_t iter)
 			f.write(&h, sizeof(h));
 			if (c->mc) {
 				mc_state_write(c, f);
+			} else if (c->ov) {
+				ov_state_write(c, f);
 			} else {
 				dev_to_file(c, f, c->ms_w, (size_t)c->D * sizeof(double2));
 				dev_to_file(c, f, c->ms_v, (size_t)c->k * c->D * sizeof(double2));
@@ -1851,12 +1858,14 @@ int vbfm_load_state(vbfm_ctx *c, const char *path, uint32_t *iter)
 		CkptFile f(path, "rb");
 		StateHeader h;
 		f.read(&h, sizeof(h));
-		const bool mc_file = memcmp(h.magic, MC_STATE_MAGIC, 8) == 0;
-		if ((!mc_file && memcmp(h.magic, STATE_MAGIC, 8) != 0) || h.version != 2)
-			throw std::string("not a libvbfm checkpoint (version 2): ") + path;
-		if (mc_file != (c->mc != nullptr))
-			throw std::string(mc_file ? "an MCMC / ALS checkpoint: resume it in an MCMC / ALS context"
-			                          : "a VB checkpoint: resume it in a VB context");
+		int kind = -1;
+		for (int q = 0; q < 3; q++)
+			if (memcmp(h.magic, state_magic(q), 8) == 0) kind = q;
+		if (kind < 0 || h.version != 2) throw std::string("not a libvbfm checkpoint (version 2): ") + path;
+		static const char *const learner[3] = {"a VB checkpoint: resume it in a VB context",
+		                                       "an MCMC / ALS checkpoint: resume it in an MCMC / ALS context",
+		                                       "an online VB checkpoint: resume it in an online VB context"};
+		if (kind != state_kind(c)) throw std::string(learner[kind]);
 		if (h.k0 != c->k0 || h.k1 != c->k1 || h.k != c->k || h.D != c->D || h.G != c->G)
 			throw std::string("checkpoint of another model configuration (-dim / num_attribute / groups)");
 		if (h.nranks != c->nranks || h.rank != c->rank)
@@ -1869,13 +1878,15 @@ int vbfm_load_state(vbfm_ctx *c, const char *path, uint32_t *iter)
 			                  "another order): resume with the same VBFM_LAYOUT / vbfm_set_layout and shard mode");
 		if (h.level_order && !c->lord) throw std::string("checkpoint of a level-ordered run: resume with the same row layout");
 		// the whole file is there before any state is replaced
-		const uint64_t payload = mc_file ? mc_state_payload(c) : state_payload(c);
+		const uint64_t payload = kind == 1 ? mc_state_payload(c) : kind == 2 ? ov_state_payload(c) : state_payload(c);
 		if (fseek(f.f, 0, SEEK_END) != 0 || (uint64_t)ftell(f.f) != sizeof(h) + payload ||
 		    fseek(f.f, (long)sizeof(h), SEEK_SET) != 0)
 			throw std::string("checkpoint file truncated or of another size: ") + path;
 		rows_row_order(c);
-		if (mc_file) {
+		if (kind == 1) {
 			mc_state_read(c, f);
+		} else if (kind == 2) {
+			ov_state_read(c, f);
 		} else {
 			file_to_dev(c, f, c->ms_w, (size_t)c->D * sizeof(double2));
 			file_to_dev(c, f, c->ms_v, (size_t)c->k * c->D * sizeof(double2));

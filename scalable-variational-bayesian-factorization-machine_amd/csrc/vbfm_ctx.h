@@ -330,5 +330,9 @@ void file_to_dev(vbfm_ctx *c, CkptFile &f, void *d, size_t bytes);
 uint64_t mc_state_payload(vbfm_ctx *c);
 void mc_state_write(vbfm_ctx *c, CkptFile &f);
 void mc_state_read(vbfm_ctx *c, CkptFile &f);
+// ... and the online learner's (vbfm_online.hip)
+uint64_t ov_state_payload(vbfm_ctx *c);
+void ov_state_write(vbfm_ctx *c, CkptFile &f);
+void ov_state_read(vbfm_ctx *c, CkptFile &f);
 
 }  // namespace vbi

@@ -1272,3 +1272,84 @@ int vbfm_online_get_state(vbfm_ctx *c, double *nat_mu_w, double *nat_sigma_w, do
 }
 
 }  // extern "C"
+
+// ---- checkpoint / resume of the online learner (vbfm_save_state / vbfm_load_state) ----------
+// Between two epochs the online learner's state is the parameters, the hyper parameters and the
+// four scalars (as VB's), the natural parameters and step sizes of every attribute and of w0
+// (fm_learn_vb_online.h:686-758), and the epoch shuffle's inputs: the reference's rand() stream
+// (its 31-word window) and the last permutation (the reference keeps it across epochs,
+// fm_learn_vb_online_simultaneous.h:58-62). A batch's row caches are predicted afresh from the
+// parameters (:111-139), so no records are kept. The next epoch's permutation, drawn ahead on a
+// host thread, is not saved: the resumed context draws it from the same stream and permutation.
+namespace vbi {
+
+namespace {
+constexpr size_t OV_HEAD_WORDS = 8 + 32;   // {num_batch, n_total, t_w0, 0...}, stream window + pad
+}
+
+uint64_t ov_state_payload(vbfm_ctx *c)
+{
+	const uint64_t D = c->D, kd = (uint64_t)c->k * c->D, G = c->G, gk = G * (uint64_t)c->k;
+	return OV_HEAD_WORDS * 4 + (uint64_t)c->tr.n * 4 + D * 16 + kd * 16 + (G + gk) * 8 + 4 * 8 + D * 16 + kd * 16 +
+	       D * 8 * 2 + D * 4 * 2 + 3 * 8;
+}
+
+void ov_state_write(vbfm_ctx *c, CkptFile &f)
+{
+	OvState &o = *c->ov;
+	o.pre_join();   // the prefetch thread reads the stream and the permutation
+	uint32_t w[OV_HEAD_WORDS] = {};
+	w[0] = o.num_batch; w[1] = o.n_total; w[2] = o.t_w0;
+	o.stream.chrono_state(w + 8);
+	f.write(w, sizeof(w));
+	f.write(o.shuffle.data(), (size_t)o.n_total * 4);
+	const size_t D = c->D, kd = (size_t)c->k * c->D;
+	dev_to_file(c, f, c->ms_w, D * sizeof(double2));
+	dev_to_file(c, f, c->ms_v, kd * sizeof(double2));
+	f.write(c->hyp_w.data(), c->hyp_w.size() * 8);
+	f.write(c->hyp_v.data(), c->hyp_v.size() * 8);
+	const double sc[4] = {c->alpha, c->sigma_0, c->mu0, c->s0d};
+	f.write(sc, sizeof(sc));
+	dev_to_file(c, f, o.nat_w, D * sizeof(double2));
+	dev_to_file(c, f, o.nat_v, kd * sizeof(double2));
+	dev_to_file(c, f, o.new_wj, D * 8);
+	dev_to_file(c, f, o.new_vj, D * 8);
+	dev_to_file(c, f, o.t_wj, D * 4);
+	dev_to_file(c, f, o.t_vj, D * 4);
+	const double os[3] = {o.nat_mu0, o.nat_sig0, o.new_w0};
+	f.write(os, sizeof(os));
+}
+
+void ov_state_read(vbfm_ctx *c, CkptFile &f)
+{
+	OvState &o = *c->ov;
+	uint32_t w[OV_HEAD_WORDS];
+	f.read(w, sizeof(w));
+	if (w[0] != o.num_batch || w[1] != o.n_total)
+		throw std::string("checkpoint of another mini-batch split (-batch): resume with the same num_batch");
+	o.pre_join();   // a permutation drawn ahead from the state being replaced is dropped
+	o.sh_next.clear();
+	f.read(o.shuffle.data(), (size_t)o.n_total * 4);
+	o.stream.set_chrono_state(w + 8);
+	o.t_w0 = w[2];
+	const size_t D = c->D, kd = (size_t)c->k * c->D;
+	file_to_dev(c, f, c->ms_w, D * sizeof(double2));
+	file_to_dev(c, f, c->ms_v, kd * sizeof(double2));
+	f.read(c->hyp_w.data(), c->hyp_w.size() * 8);
+	f.read(c->hyp_v.data(), c->hyp_v.size() * 8);
+	upload_hyp(c);
+	double sc[4];
+	f.read(sc, sizeof(sc));
+	c->alpha = sc[0]; c->sigma_0 = sc[1]; c->mu0 = sc[2]; c->s0d = sc[3];
+	file_to_dev(c, f, o.nat_w, D * sizeof(double2));
+	file_to_dev(c, f, o.nat_v, kd * sizeof(double2));
+	file_to_dev(c, f, o.new_wj, D * 8);
+	file_to_dev(c, f, o.new_vj, D * 8);
+	file_to_dev(c, f, o.t_wj, D * 4);
+	file_to_dev(c, f, o.t_vj, D * 4);
+	double os[3];
+	f.read(os, sizeof(os));
+	o.nat_mu0 = os[0]; o.nat_sig0 = os[1]; o.new_w0 = os[2];
+}
+
+}  // namespace vbi

@@ -531,7 +531,7 @@ struct OnlineRun {
 	uint32_t G, D;
 	int k0, k1, k;
 	bool vfile;
-	std::string rlog_file, out_file, parity_file;
+	std::string rlog_file, out_file, parity_file, save_file, resume_file;
 };
 
 static void run_online(const OnlineRun &r, Data &train, Data &test, const Rank &rk)
@@ -551,7 +551,15 @@ static void run_online(const OnlineRun &r, Data &train, Data &test, const Rank &
 		vbfm_online_config oc{r.num_batch, r.seed, r.init_stdev,
 		                      replay ? VBFM_ONLINE_INIT_REPLAY : VBFM_ONLINE_INIT_HOST, r.vfile ? fm_v.data() : nullptr};
 		check(vbfm_online_init(ctx, &oc), ctx);
-		if (r.vfile) write_vfile(fm_v, r.k, r.D);
+		const bool resume = !r.resume_file.empty();
+		if (r.vfile && !resume) write_vfile(fm_v, r.k, r.D);
+		// -resume: the learner's state (parameters, natural parameters, step sizes, the rand()
+		// stream and the last permutation) from the file instead of the initial draws
+		uint32_t it0 = 0;
+		if (resume) {
+			check(vbfm_load_state(ctx, r.resume_file.c_str(), &it0), ctx);
+			std::cout << "resuming from " << r.resume_file << " after " << it0 << " iterations" << std::endl;
+		}
 		std::ofstream *rlog_out = nullptr;
 		RLog *rlog = nullptr;
 		if (!r.rlog_file.empty()) {   // fm_learn::init + fm_learn_vb_online::init fields (:761-783)
@@ -579,9 +587,9 @@ static void run_online(const OnlineRun &r, Data &train, Data &test, const Rank &
 		// :37-52: the rmse file and an (always empty) free_energy_..._vb_online are truncated; the
 		// free energies are appended to free_energy_..._vb (fm_learn_vb_online.h:636-662)
 		const std::string f_rmse = "test_rmse_" + tag.str() + "_vb_online", f_fe = "free_energy_" + tag.str() + "_vb";
-		{ std::ofstream a(f_rmse.c_str()); std::ofstream b(("free_energy_" + tag.str() + "_vb_online").c_str()); }
+		if (!resume) { std::ofstream a(f_rmse.c_str()); std::ofstream b(("free_energy_" + tag.str() + "_vb_online").c_str()); }
 		ParityLog plog(r.parity_file, true);
-		for (uint32_t it = 0; it < r.num_iter; it++) {
+		for (uint32_t it = it0; it < it0 + r.num_iter; it++) {
 			const double t_user = usertime();
 			const clock_t t_clock = clock();
 			const double t_wall = (double)time(NULL);
@@ -623,6 +631,7 @@ static void run_online(const OnlineRun &r, Data &train, Data &test, const Rank &
 				plog.end();
 			}
 		}
+		if (!r.save_file.empty()) check(vbfm_save_state(ctx, r.save_file.c_str(), it0 + r.num_iter), ctx);
 		std::cout << "after learn" << std::endl;                              // libfm.cpp:507
 		std::cout << "Final\tTrain=" << NAN << "\tTest=" << NAN << std::endl;   // evaluate() is NaN (:17)
 		if (!r.out_file.empty()) {
@@ -973,9 +982,9 @@ int main(int argc, char **argv)
 		const std::string p_trans = cmd.reg("transport", "rank exchange: rccl (one GPU per rank, default) or host (shared memory; ranks may share a GPU)");
 		const std::string p_plan = cmd.reg("plan", "1: every rank prints its launch and shard plan as JSON and exits (no GPU)");
 		const std::string p_vfile = cmd.reg("vfile", "write v_file.txt like the reference (1) or not (0); default=1");
-		const std::string p_save = cmd.reg("save_state", "vb, mcmc, als: write the learner's state to this file after the last iteration (.<rank> per rank with -devices)");
+		const std::string p_save = cmd.reg("save_state", "vb, vb_online, mcmc, als: write the learner's state to this file after the last iteration (.<rank> per rank with -devices)");
 		const std::string p_plog = cmd.reg("parity_log", "one JSON line per iteration: the printed values at 17 digits, phase times, sweep nnz*k/s and HBM roofline fraction; default=''");
-		const std::string p_resume = cmd.reg("resume", "vb, mcmc, als: continue from a -save_state file (same data and -dim) instead of the initial draws");
+		const std::string p_resume = cmd.reg("resume", "vb, vb_online, mcmc, als: continue from a -save_state file (same data and -dim) instead of the initial draws");
 		if (cmd.has(p_help) || argc == 1) { cmd.print_help(); return 0; }
 		cmd.check();
 
@@ -1059,7 +1068,8 @@ int main(int argc, char **argv)
 		job.method = method;
 		job.plan = cmd.geti(p_plan, 0) != 0;
 		job.online = OnlineRun{seed, init_stdev, num_iter, (uint32_t)cmd.geti(p_batch, 50), gp, G, D, k0, k1, k, vfile,
-		                       rlog, out, plog};
+		                       rlog, out, plog, cmd.has(p_save) ? cmd.get(p_save) : std::string(),
+		                       cmd.has(p_resume) ? cmd.get(p_resume) : std::string()};
 		std::vector<double> reg;
 		for (const std::string &r : cmd.list(p_reg)) reg.push_back(atof(r.c_str()));
 		job.mc = McmcRun{method == "mcmc", seed, init_stdev, num_iter, reg, gp, G, D, k0, k1, k, vfile, rlog, out, plog,

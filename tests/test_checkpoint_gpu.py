@@ -305,3 +305,80 @@ def test_cli_mcmc_save_state_and_resume(method, tmp_path):
     it_one = re.findall(r"#Iter=\s*(\d+)\tTrain=(\S+)\tTest=(\S+)", s_one)
     it_two = re.findall(r"#Iter=\s*(\d+)\tTrain=(\S+)\tTest=(\S+)", s_two)
     assert len(it_one) == 6 and it_two == it_one[3:]
+
+
+def _ov_learner(tr, te, nf, k, num_batch=7):
+    rp, f, v, y = tr
+    g = vbfm.FMLearnVBOnline(1, 1, k, nf, min_target=float(y.min()), max_target=float(y.max()))
+    g.set_data(vbfm.DataSubset.from_csr(rp, f, v, y, nf), vbfm.DataSubset.from_csr(*te, nf))
+    g.init(7, 0.1, num_batch)
+    return g
+
+
+def _ov_trace(stats):
+    return [(s.rmse, s.mae, s.free_energy_first, s.free_energy_last, s.alpha, s.mu_0_dash, s.sigma_0_dash)
+            for s in stats]
+
+
+@pytest.mark.parametrize("layout", ["auto", "column"])
+def test_online_resume_continues_bit_for_bit(layout, tmp_path, monkeypatch):
+    """The online learner: 4 epochs against 2 + save, then load into a fresh context + 2. The
+    epoch permutations continue from the saved rand() stream and last permutation (the one the
+    first context drew ahead on its host thread is not saved), the natural parameters and step
+    sizes from the file: every later epoch and the final natural parameters equal bit for bit
+    (per-batch level store and column kernels)."""
+    monkeypatch.setenv("VBFM_LAYOUT", layout)
+    tr, te, nf = _data(n=20000)
+    k = 4
+    a = _ov_learner(tr, te, nf, k)
+    full = [a.epoch() for _ in range(4)]
+    sa, pa = a.online_state(), a.get_params()
+    a.close()
+    b = _ov_learner(tr, te, nf, k)
+    first = [b.epoch() for _ in range(2)]
+    path = str(tmp_path / "ov.state")
+    b.save_state(path)
+    b.close()
+    c = _ov_learner(tr, te, nf, k)
+    assert c.load_state(path) == 2
+    rest = [c.epoch() for _ in range(2)]
+    sc, pc = c.online_state(), c.get_params()
+    c.close()
+    assert _ov_trace(first + rest) == _ov_trace(full)
+    assert (full[-1].n_lord_batches > 0) == (layout == "auto")
+    for key in sa:
+        np.testing.assert_array_equal(sc[key], sa[key], err_msg=key)
+    for key in ("mu_w", "sigma_w", "mu_v", "sigma_v"):
+        np.testing.assert_array_equal(np.asarray(pc[key]), np.asarray(pa[key]), err_msg=key)
+    # another mini-batch split is refused
+    h = _ov_learner(tr, te, nf, k, num_batch=5)
+    with pytest.raises(vbfm.VbfmError, match="another mini-batch split"):
+        h.load_state(path)
+    h.close()
+
+
+def test_cli_online_save_state_and_resume(tmp_path):
+    """bin/libFM -method vb_online: 3 epochs + -save_state, then -resume for 3 more: the test_rmse
+    file, the free energies and the #Iter lines continue the 6-epoch run's."""
+    d = os.path.join(GOLDEN, "tiny")
+    import subprocess
+
+    def run(cwd, iters, extra):
+        os.makedirs(cwd, exist_ok=True)
+        out = subprocess.run([CLI, "-task", "r", "-train", os.path.join(d, "train.libfm"), "-test",
+                              os.path.join(d, "test.libfm"), "-method", "vb_online", "-dim", "1,1,3", "-iter",
+                              str(iters), "-seed", "5", "-init_stdev", "0.1", "-batch", "3"] + extra,
+                             cwd=str(cwd), capture_output=True, text=True, timeout=300)
+        assert "ERROR" not in out.stderr, out.stderr
+        return out.stdout
+
+    one = tmp_path / "one"
+    s_one = run(one, 6, [])
+    two = tmp_path / "two"
+    run(two, 3, ["-save_state", "ov.state"])
+    s_two = run(two, 3, ["-resume", "ov.state"])
+    for fn in ("test_rmse_113_vb_online", "free_energy_113_vb"):
+        assert open(one / fn).read() == open(two / fn).read(), fn
+    it_one = re.findall(r"#Iter=\s*(\d+)\tTest=(\S+)", s_one)
+    it_two = re.findall(r"#Iter=\s*(\d+)\tTest=(\S+)", s_two)
+    assert len(it_one) == 6 and it_two == it_one[3:]
