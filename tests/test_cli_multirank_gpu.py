@@ -144,6 +144,27 @@ def test_checkpoint_per_rank_resume(synth_files, tmp_path):
         assert got[key] == full["files"][key], key
 
 
+@pytest.mark.parametrize("method", ["mcmc", "als"])
+def test_checkpoint_per_rank_resume_mcmc(method, synth_files, tmp_path):
+    """-method mcmc | als, -devices 2: one chain file per rank; 3 + 3 iterations equal 6 in one go
+    (test_rmse file, #Iter= lines and -parity_log values at 17 digits)."""
+    import json
+    tr, te = synth_files["train"], synth_files["test"]
+    ext = ["-vfile", "0", "-devices", "2", "-transport", "host"]
+    full = cli_run(tmp_path, "full", tr, te, "1,1,4", 6, 7, ext + ["-parity_log", "p.jsonl"], method=method)
+    cwd = tmp_path / "half"
+    run(cwd, tr, te, "1,1,4", 3, 7, ext + ["-save_state", str(cwd / "s"), "-parity_log", "p1.jsonl"], method=method)
+    assert (cwd / "s.0").exists() and (cwd / "s.1").exists()
+    out = run(cwd, tr, te, "1,1,4", 3, 7, ext + ["-resume", str(cwd / "s"), "-parity_log", "p2.jsonl"], method=method)
+    assert "resuming" in out.stdout
+    assert files(cwd, "114", method)["rmse"] == full["files"]["rmse"]
+    assert iters_of(out.stdout) == iters_of(full["stdout"])[3:]
+    want = [json.loads(x) for x in open(full["cwd"] / "p.jsonl")]
+    got = [json.loads(x) for x in open(cwd / "p1.jsonl")] + [json.loads(x) for x in open(cwd / "p2.jsonl")]
+    keys = ("iter", "train", "test_rmse", "test_mae", "test_rmse_this", "alpha", "w0")
+    assert [[g[k] for k in keys] for g in got] == [[w[k] for k in keys] for w in want]
+
+
 def test_feature_shards_run(synth_files, tmp_path):
     """-shard features (the north star's column partition, Jacobi across ranks): runs through
     the CLI and fits (test RMSE falls); not the reference's sequential sweep for 2 ranks."""
