@@ -15,7 +15,10 @@
   reference ran 2.4 h on one core here).
 * C5: the MCMC Gibbs sweep with device RNG streams at C4 size, k = 100: the fused and the
   row-shard split kernels draw the same chain bit for bit; ALS (no sampling) on the level
-  and column layouts agrees to summation order.
+  and column layouts agrees to summation order. C5 at k = 100 on the first 1e7 rows of C4's
+  data set, -method mcmc and als: one iteration against the compiled reference
+  (tests/golden/c5_{mcmc,als}_k100_r1e7, make_c3_k50.py --case c5_*; 79 / 81 min of reference),
+  the chain on the reference's own random stream.
 
 The oracle (tests/oracle_ctypes.py, the C restatement pinned to the reference's fixtures) is
 the checker; the tolerance is REL = 1e-9 relative (the north star's gate is 1e-6).
