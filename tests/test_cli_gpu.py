@@ -204,3 +204,24 @@ def test_cli_parity_log_17_digits(case, tmp_path):
         for gk, rk in pairs:
             assert abs(got[gk] - ref[rk]) <= 1e-9 * max(abs(ref[rk]), 1e-300), (it, gk, got[gk], ref[rk])
         assert got["ms_v"] > 0 and got["sweep_nnz_k_per_s"] > 0 and 0 < got["hbm_frac_per_gpu"] < 1
+
+
+def test_cli_parity_log_online(tmp_path):
+    """-parity_log with -method vb_online: test RMSE and the first / last batch's free energy of
+    every epoch at 1e-9 against the compiled reference's trace (tiny/online_b3)."""
+    import json
+    t, _ = load_case("tiny/online_b3")
+    m = t["meta"]
+    d = os.path.join(GOLDEN, "tiny")
+    run_cli(tmp_path, os.path.join(d, "train.libfm"), os.path.join(d, "test.libfm"), m["dim"], m["iter"], m["seed"],
+            ["-init_stdev", str(m["init_stdev"]), "-batch", str(m["batch"]), "-parity_log", "p.jsonl", "-vfile", "0"],
+            method="vb_online")
+    lines = [json.loads(x) for x in open(tmp_path / "p.jsonl")]
+    assert len(lines) == m["iter"]
+    for it, (got, ref) in enumerate(zip(lines, t["trace"])):
+        assert got["iter"] == it and got["method"] == "vb_online"
+        pairs = [(got["test_rmse"], ref["rmse"]), (got["free_energy_first"], ref["free_energy"][0]),
+                 (got["free_energy_last"], ref["free_energy"][-1])]
+        for a, b in pairs:
+            assert abs(a - b) <= 1e-9 * abs(b), (it, a, b)
+        assert got["ms_v"] > 0 and got["sweep_nnz_k_per_s"] > 0
