@@ -53,13 +53,16 @@ void allreduce_dev(vbfm_ctx *c, void *buf, size_t n, ncclDataType_t t, ncclRedOp
 uint32_t ar_chunks(vbfm_ctx *c, uint32_t nfeat)
 {
 	if (!c->row_comm()) return 1;
-	// default 2 chunks of at least 2048 columns: every chunk past the first costs ~13 us (a
-	// kernel boundary, its tail, the cross-stream events: measured at C4's per-rank size on 8
-	// GPUs, profiles/r03_chunks/), about what hiding another part of a 2 MB all-reduce saves, so
-	// the expected optimum is near sqrt(t_allreduce / 13 us) ~ 2; VBFM_AR_CHUNKS=n asks for n
-	// chunks of at least 64 columns (tests, A/B)
+	// default: one all-reduce per level. Cutting a level into chunks whose all-reduces overlap
+	// the next chunk's statistics kernel is bit-identical, but each extra chunk costs a kernel
+	// boundary, a second collective and two cross-stream events: 489 -> 516 -> 530 us per level
+	// for 1 / 2 / 4 chunks at C4's per-rank size on 8 GPUs (one GPU, 1-rank RCCL,
+	// profiles/r03_chunks/n8_shard), while it can hide at most t_ar(2 MB) - t_ar(1 MB) of a
+	// latency-dominated ring all-reduce (~10-20 us on one xGMI node): a net loss there.
+	// VBFM_AR_CHUNKS=n asks for n chunks of at least 64 columns (fabrics with slow collectives;
+	// tests, A/B)
 	const char *e = getenv("VBFM_AR_CHUNKS");
-	const uint32_t want = e ? (uint32_t)std::max(atoi(e), 1) : 2u, floor = e ? 64u : 2048u;
+	const uint32_t want = e ? (uint32_t)std::max(atoi(e), 1) : 1u, floor = e ? 64u : 2048u;
 	const uint32_t C = std::min<uint32_t>(want, nfeat / floor);
 	return std::max<uint32_t>(1, std::min<uint32_t>(C, vbfm_ctx::AR_MAX_CHUNKS));
 }
