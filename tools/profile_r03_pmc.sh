@@ -6,7 +6,7 @@
 # gpurun_out/prof_r03/FETCH_SIZE.txt); a level launch's bytes do not depend on k or the step.
 cd "$GRAFT_REPO_ROOT" || exit 1
 export TMPDIR=/tmp
-out=gpurun_out/prof_r03
+out=gpurun_out/${1:-prof_r03}
 mkdir -p $out
 for c in FETCH_SIZE WRITE_SIZE; do
   echo "pass $c start $(date +%T)" >> $out/progress.txt
