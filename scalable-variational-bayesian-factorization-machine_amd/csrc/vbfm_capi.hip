@@ -1800,11 +1800,6 @@ void file_to_dev(vbfm_ctx *c, CkptFile &f, void *d, size_t bytes)
 	}
 }
 
-void require_vb_state(vbfm_ctx *c, const char *fn)
-{
-	(void)fn;
-	require_train(c);
-}
 
 }  // namespace vbi
 
@@ -1814,7 +1809,7 @@ int vbfm_save_state(vbfm_ctx *c, const char *path, uint32_t iter)
 {
 	if (!c || !path) return fail(c, "null argument");
 	return guarded(c, [&] {
-		require_vb_state(c, "vbfm_save_state");
+		require_train(c);
 		no_partial(c);
 		StateHeader h = state_header(c, iter);
 		memcpy(h.magic, state_magic(state_kind(c)), 8);
@@ -1856,7 +1851,7 @@ int vbfm_load_state(vbfm_ctx *c, const char *path, uint32_t *iter)
 {
 	if (!c || !path) return fail(c, "null argument");
 	return guarded(c, [&] {
-		require_vb_state(c, "vbfm_load_state");
+		require_train(c);
 		no_partial(c);
 		CkptFile f(path, "rb");
 		StateHeader h;
