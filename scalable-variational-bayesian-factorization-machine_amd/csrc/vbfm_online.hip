@@ -1297,7 +1297,8 @@ uint64_t ov_state_payload(vbfm_ctx *c)
 void ov_state_write(vbfm_ctx *c, CkptFile &f)
 {
 	OvState &o = *c->ov;
-	o.pre_join();   // the prefetch thread reads the stream and the permutation
+	// a prefetch thread still drawing the next permutation only reads the stream and the
+	// permutation saved here (it writes sh_next / stream_next): no join, the draw stays usable
 	uint32_t w[OV_HEAD_WORDS] = {};
 	w[0] = o.num_batch; w[1] = o.n_total; w[2] = o.t_w0;
 	o.stream.chrono_state(w + 8);

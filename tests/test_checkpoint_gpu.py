@@ -338,7 +338,9 @@ def test_online_resume_continues_bit_for_bit(layout, tmp_path, monkeypatch):
     first = [b.epoch() for _ in range(2)]
     path = str(tmp_path / "ov.state")
     b.save_state(path)
+    cont = [b.epoch() for _ in range(2)]   # the saving context goes on as if nothing happened
     b.close()
+    assert _ov_trace(first + cont) == _ov_trace(full)
     c = _ov_learner(tr, te, nf, k)
     assert c.load_state(path) == 2
     rest = [c.epoch() for _ in range(2)]
