@@ -64,7 +64,9 @@ def test_resume_continues_bit_for_bit(layout, split, tmp_path, monkeypatch):
     first = [b.iterate() for _ in range(2)]
     path = str(tmp_path / "vb.state")
     b.save_state(path)
+    cont = [b.iterate() for _ in range(2)]   # the saving context goes on as if nothing happened
     b.close()
+    assert _trace(first + cont) == _trace(full)
 
     c = _learner(tr, te, nf, k, layout)
     assert c.load_state(path) == 2
@@ -231,7 +233,9 @@ def test_mcmc_resume_continues_bit_for_bit(method, rng, layout, split, tmp_path,
     first = [b.iterate() for _ in range(2)]
     path = str(tmp_path / "mc.state")
     b.save_state(path)
+    cont = [b.iterate() for _ in range(2)]   # the saving context goes on as if nothing happened
     b.close()
+    assert _mc_trace(first + cont) == _mc_trace(full)
 
     c = _mc_learner(tr, te, nf, k, method, r, layout)
     assert c.load_state(path) == 2
