@@ -98,18 +98,75 @@ def write_cpu_sample(vbfm, cfg, rows, base, device):
     synth.write_binary(base + "_test", F * S, rpt, ft, vt, yt)
 
 
-def ref_sweep(base, factors):
+PROFILER_ENV = ("ROCPROF", "ROCP_", "ROCPROFILER")
+
+
+def profiler_attached(env=None):
+    """True under rocprofv3 (its preloaded library, or its ROCPROF* / ROCP_* variables): a child
+    process would start under the profiler's preload, which the GPU pool forbids."""
+    env = os.environ if env is None else env
+    if "rocprof" in env.get("LD_PRELOAD", ""):
+        return True
+    return any(k.startswith(PROFILER_ENV) for k in env)
+
+
+def cpu_leg_plan(rank, world, args, mc, online, multihot, env=None):
+    """Whether this rank runs the CPU baseline: rank 0 only, at every N (the north star's
+    "alongside ... in the same run" at 1/2/4/8 GPUs), not for MCMC / online / multi-hot (the
+    reference sweep timed is fm_learn_vb's), never under a profiler (the child would inherit its
+    preload) or with --no-cpu-baseline. Returns (run, reason)."""
+    if args.no_cpu_baseline:
+        return False, "--no-cpu-baseline"
+    if mc or online or multihot:
+        return False, "the CPU leg times fm_learn_vb's sweep on field-structured data"
+    if profiler_attached(env):
+        return False, "skipped under a profiler (its preloaded library would be inherited by the reference)"
+    return rank == 0, "rank 0 of %d" % world
+
+
+def cpu_leg_core():
+    """The host core the reference's sweep runs on: the last core this process may use. Every
+    rank keeps its own threads off it (pin_away_from), so the CPU leg and the GPU-driving
+    threads do not share a core."""
+    try:
+        return max(os.sched_getaffinity(0))
+    except (AttributeError, OSError, ValueError):
+        return None
+
+
+def pin_away_from(core):
+    """Move every thread of this process off `core` (no-op when it is the only core allowed)."""
+    if core is None:
+        return
+    try:
+        allowed = os.sched_getaffinity(0) - {core}
+        if not allowed:
+            return
+        for tid in os.listdir("/proc/self/task"):
+            try:
+                os.sched_setaffinity(int(tid), allowed)
+            except OSError:
+                pass
+    except (AttributeError, OSError):
+        pass
+
+
+def ref_sweep(base, factors, core=None):
     """The reference's own factor sweep (oracle/_ref/ref_driver sweep: fm_learn_vb.h:409-440,
     add_main_q + update_v over all features, plus the k = 0 overhead update_w0 + the w sweep)
-    on one core (taskset -c 0)."""
+    on one core: the child pins itself (sched_setaffinity before exec: no launcher process) and
+    starts without any profiler preload in its environment."""
     ref = os.path.join(ROOT, "oracle", "_ref", "ref_driver")
-    out = subprocess.run(["taskset", "-c", "0", ref, "sweep", "--train", base + "_train", "--test", base + "_test",
+    env = {k: v for k, v in os.environ.items() if k != "LD_PRELOAD" and not k.startswith(PROFILER_ENV)}
+    pre = (lambda: os.sched_setaffinity(0, {core})) if core is not None else None
+    out = subprocess.run([ref, "sweep", "--train", base + "_train", "--test", base + "_test",
                           "--dim", "1,1,%d" % factors, "--seed", "1", "--sweep_factors", str(factors)],
-                         cwd=os.path.dirname(base), capture_output=True, text=True, check=True, timeout=1200).stdout
+                         cwd=os.path.dirname(base), capture_output=True, text=True, check=True, timeout=1200,
+                         env=env, preexec_fn=pre).stdout
     return json.loads([l for l in out.splitlines() if l.startswith("{")][0])
 
 
-def cpu_baseline_start(vbfm, cfg, device, samples):
+def cpu_baseline_start(vbfm, cfg, device, samples, core=None, world=1):
     """Write the samples (device generator, before the timed region) and start the reference's
     sweep on them in a background thread, so that the CPU leg runs while the GPU steps are
     timed (one host core; the GPU bench thread uses another). samples: [(rows, factors), ...],
@@ -130,7 +187,7 @@ def cpu_baseline_start(vbfm, cfg, device, samples):
 
     def work():
         try:
-            res["runs"] = [ref_sweep(b, f) for b, (_, f) in zip(bases, samples)]
+            res["runs"] = [ref_sweep(b, f, core) for b, (_, f) in zip(bases, samples)]
         except Exception as exc:   # the GPU number stands on its own; report why the CPU leg failed
             res["error"] = str(exc)
         finally:
@@ -155,10 +212,11 @@ def cpu_baseline_start(vbfm, cfg, device, samples):
         return {"value": big["value"], "unit": "nnz*k/s", "cores": 1, "kind": "reference",
                 "sample": "%d rows x %d fields x %d ids (D=%d), %d factor(s) of the sweep, x=1 (rows 0.. of the "
                           "bench's data set); oracle/_ref/ref_driver = the reference's fm_learn_vb compiled from its "
-                          "sources, taskset -c 0 (1 of %d host cores: %s, last-level cache %s per core complex; the "
-                          "sample's row caches alone are %.1f GB)" % (
-                              big["rows"], F, S, F * S, big["factors"], os.cpu_count(), model, llc,
-                              big["row_cache_bytes"] / 1e9),
+                          "sources, pinned to host core %s (1 of %d host cores: %s, last-level cache %s per core "
+                          "complex; the sample's row caches alone are %.1f GB); run by rank 0 of %d during the timed "
+                          "GPU steps, every rank's threads kept off that core" % (
+                              big["rows"], F, S, F * S, big["factors"], core, os.cpu_count(), model, llc,
+                              big["row_cache_bytes"] / 1e9, world),
                 "seconds": big["seconds"], "k0_seconds": big["k0_seconds"],
                 "extrapolated_iteration_s": big.get("extrapolated_iteration_s"),
                 "extrapolation": big.get("extrapolation"), "cpu_model": model, "llc": llc,
@@ -266,6 +324,7 @@ def main():
     ap.add_argument("--config", default="c4", choices=sorted(CONFIGS))
     ap.add_argument("--rows", type=int, default=0, help="override rows per GPU")
     ap.add_argument("--k", type=int, default=0, help="override factors")
+    ap.add_argument("--ids", type=int, default=0, help="override ids per field (column length = rows / ids)")
     ap.add_argument("--method", default="vb", choices=["vb", "mcmc", "als", "vb_online"],
                     help="vb: the metric (fm_learn_vb); mcmc / als: config 5's Gibbs draw_v path "
                          "(device counter-based RNG streams); vb_online: OVBFM epochs of --batch "
@@ -321,6 +380,8 @@ def main():
         cfg["rows"] = args.rows
     if args.k:
         cfg["k"] = args.k
+    if args.ids:
+        cfg["ids"] = args.ids
     k = cfg["k"]
     multihot = "features" in cfg
     F, S = (0, 0) if multihot else (cfg["fields"], cfg["ids"])
@@ -407,14 +468,21 @@ def main():
         rank, time.time() - t0, N, F, S, NF, nnz, k, layout))
 
     cpu_leg = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline and not mc and not online and not multihot:
+    run_leg, leg_reason = cpu_leg_plan(rank, world, args, mc, online, multihot)
+    leg_any = cpu_leg_plan(0, world, args, mc, online, multihot)[0]   # some rank runs it
+    core = cpu_leg_core() if leg_any else None
+    if leg_any:
+        pin_away_from(core)     # every rank: the GPU-driving threads leave the CPU leg's core
+    if run_leg:
         try:   # the samples written now (device generator); the reference runs during the timed steps
-            rows = min(args.cpu_rows, N)
+            rows = min(args.cpu_rows, n_total)   # rows [0, rows) of the whole data set, at any N
             samples = [(min(2_000_000, rows), min(2, k))] if rows > 2_000_000 else []
             samples.append((rows, min(args.cpu_factors, k)))
-            cpu_leg = cpu_baseline_start(vbfm, cfg, device, samples)
+            cpu_leg = cpu_baseline_start(vbfm, cfg, device, samples, core=core, world=world)
         except Exception as exc:
             cpu_leg = (lambda e=str(exc): {"value": None, "error": e})
+    elif rank == 0:
+        cpu_leg = (lambda r=leg_reason: {"value": None, "skipped": r})
 
     def rmse_of(st):
         return st.rmse_all if mc else st.rmse

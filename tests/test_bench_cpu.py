@@ -143,3 +143,53 @@ def test_cpu_sample_files_and_reference_sweep(tmp_path):
         pytest.skip("oracle/_ref/ref_driver not built")
     r = bench.ref_sweep(base, 2)
     assert r["nnz"] == 30000 and r["factors"] == 2 and r["nnz_k_per_s"] > 0
+
+
+def _bench_module():
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("bench", BENCH)
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+    return bench
+
+
+@pytest.mark.parametrize("world", [1, 2, 4, 8])
+def test_cpu_leg_runs_on_rank_zero_at_every_n(world):
+    """the reference's sweep (the CPU baseline) runs in the same run at
+    every N, on rank 0 only; MCMC / online / multi-hot and --no-cpu-baseline skip it, and so does
+    a run under a profiler (the reference would inherit its preloaded library)."""
+    bench = _bench_module()
+
+    class A:
+        no_cpu_baseline = False
+    clean = {"PATH": "/usr/bin"}
+    runs = [bench.cpu_leg_plan(r, world, A, False, False, False, clean)[0] for r in range(world)]
+    assert runs == [True] + [False] * (world - 1)
+    for mc, online, multihot in ((True, False, False), (False, True, False), (False, False, True)):
+        assert not bench.cpu_leg_plan(0, world, A, mc, online, multihot, clean)[0]
+    prof = dict(clean, LD_PRELOAD="/opt/rocm/lib/rocprofiler-sdk/librocprofiler-sdk-tool.so")
+    run, why = bench.cpu_leg_plan(0, world, A, False, False, False, prof)
+    assert not run and "profiler" in why
+    assert not bench.cpu_leg_plan(0, world, A, False, False, False, dict(clean, ROCPROF_KERNEL_TRACE="1"))[0]
+    A.no_cpu_baseline = True
+    assert not bench.cpu_leg_plan(0, world, A, False, False, False, clean)[0]
+
+
+def test_cpu_leg_core_and_pinning():
+    """The CPU leg's core is one this process may use, and pin_away_from leaves every thread
+    of the process on the other cores (when there are any)."""
+    bench = _bench_module()
+    before = os.sched_getaffinity(0)
+    core = bench.cpu_leg_core()
+    assert core in before
+    try:
+        bench.pin_away_from(core)
+        if len(before) > 1:
+            for tid in os.listdir("/proc/self/task"):
+                assert core not in os.sched_getaffinity(int(tid))
+    finally:
+        for tid in os.listdir("/proc/self/task"):
+            try:
+                os.sched_setaffinity(int(tid), before)
+            except OSError:
+                pass

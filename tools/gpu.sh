@@ -8,6 +8,8 @@
 #   pmc[=<args>]               FETCH_SIZE then WRITE_SIZE, one --pmc pass each, of bench.py <args>
 #   py=<script>[+args]         python -u <script> <args>
 #   exe=<binary>[+args]        a built probe binary
+#   sq=<CTRS>@<kernel re>@<args>  one --pmc pass of SQ counters (tools/sq_summary.py), list: rocprofv3 -L
+#   setenv=NAME=VALUE / unsetenv=NAME   environment of the steps that follow
 # Every step runs under its own timeout; the first failure ends the call.
 cd "$GRAFT_REPO_ROOT" || exit 1
 export TMPDIR=/tmp
@@ -38,6 +40,14 @@ for step in "$@"; do
         timeout -k 10 600 rocprofv3 --pmc $c --kernel-trace -d "$O/pmc_${n}_$c" -o p --output-format csv -- \
           python3 bench.py $args > "$O/pmc_${n}_$c.json" 2> "$O/pmc_${n}_$c.txt" || break
       done ;;
+    sq)
+      # sq=<COUNTER,COUNTER,...>@<kernel regex>@<bench args>: one --pmc pass (at most 8 SQ_ counters)
+      IFS=@ read -r ctrs kre bargs <<< "$arg"
+      timeout -s KILL 300 rocprofv3 --pmc ${ctrs//,/ } --kernel-trace --kernel-include-regex "$kre" -d "$O/sq_$n" -o p \
+        --output-format csv -- python3 bench.py ${bargs//+/ } > "$O/sq_$n.json" 2> "$O/sq_$n.txt" ;;
+    list) timeout -s KILL 60 rocprofv3 -L > "$O/counters.txt" 2>&1 ;;
+    setenv) export "$arg" ;;          # setenv=NAME=VALUE for the steps that follow
+    unsetenv) unset "$arg" ;;
     py) timeout -k 10 900 python -u $args > "$O/py_$n.txt" 2>&1 ;;
     exe) timeout -k 10 600 $args > "$O/exe_$n.txt" 2>&1 ;;
     *) echo "unknown step $step" >> "$O/progress.txt"; exit 2 ;;
