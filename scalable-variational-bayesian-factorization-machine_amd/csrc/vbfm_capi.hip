@@ -360,7 +360,7 @@ void build_lorder(vbfm_ctx *c, const std::vector<uint64_t> &cp, const std::vecto
 	c->lnext = dalloc<uint32_t>(d.nnz);
 	c->lrow0 = dalloc<uint32_t>(n);
 	c->lpos0 = dalloc<uint32_t>(n);
-	c->rows_alt = dalloc<RowRec>(n);
+	c->rows_alt = dalloc_rec<RowRec>(n);
 	uint32_t *tmp = dalloc<uint32_t>(n);
 	auto lev = [&](uint32_t l, uint32_t *&f, uint32_t &nfl, const uint64_t *&lp) {
 		f = c->level_feats + c->level_ptr[l];
@@ -976,6 +976,9 @@ void no_partial(vbfm_ctx *c)
 {
 	if (c->part_kind >= 0)
 		throw std::string("a sweep driven level by level is in progress (finish it with vbfm_step_*_level)");
+	if (c->part_kind == -2)
+		throw std::string("a level of a sweep driven level by level failed: the row caches are undefined "
+		                  "(vbfm_set_train or vbfm_load_state starts again)");
 }
 
 // level l of the w sweep (is_w) or of factor f's v sweep, exactly as the whole sweep runs it;
@@ -989,6 +992,7 @@ void step_level(vbfm_ctx *c, bool is_w, int f, uint32_t l)
 	if (c->deferred()) throw std::string("per-level steps: the deferred split keeps each level's correction pending (VBFM_DEFER=0)");
 	if (l >= L) throw std::string("level out of range");
 	const int kind = is_w ? 0 : 1;
+	if (c->part_kind == -2) no_partial(c);
 	if (c->part_kind < 0 ? l != 0 : (c->part_kind != kind || c->part_f != f || c->part_next != l))
 		throw std::string("per-level steps: levels of a sweep must come in order from level 0");
 	if (l == 0) {
@@ -998,8 +1002,13 @@ void step_level(vbfm_ctx *c, bool is_w, int f, uint32_t l)
 			rows_level_order(c);
 		}
 	}
+	try {
+		sweep_level(c, l, is_w, f);
+	} catch (...) {
+		c->part_kind = -2;   // the records may be half moved: refuse everything until a restart
+		throw;
+	}
 	c->part_kind = kind; c->part_f = f; c->part_next = l + 1;
-	sweep_level(c, l, is_w, f);
 	if (!is_w) c->qslot = f & 1;
 	if (l + 1 < L) return;
 	c->part_kind = -1;   // the sweep is complete: the bookkeeping of step_w / step_v
@@ -1255,7 +1264,7 @@ static void alloc_rows(vbfm_ctx *c)
 	lord_release(c, false);   // a new train set: the old records are discarded
 	dfree(c->rows);
 	dfree(c->scratch_n);
-	c->rows = dalloc<RowRec>(c->tr.n);
+	c->rows = dalloc_rec<RowRec>(c->tr.n);
 	c->scratch_n = dalloc<double>(c->tr.n);
 	HIPCHK(hipMemsetAsync(c->rows, 0, (size_t)std::max(c->tr.n, 1u) * sizeof(RowRec), c->s));
 	uint64_t n = c->tr.n;
@@ -1294,6 +1303,7 @@ int vbfm_set_train(vbfm_ctx *c, const vbfm_csc *in)
 		if (c->tr.n > ROW_MASK) throw std::string("too many rows for one shard (max 2^31-1)");
 		HIPCHK(vbk::mark_first(c->tr.row_ptr, c->tr.csr, c->tr.col_ptr, c->tr.csc, c->tr.n, c->s));
 		alloc_rows(c);
+		c->part_kind = -1;   // new records: no level-by-level sweep in progress
 	});
 }
 
@@ -1750,7 +1760,10 @@ uint64_t train_fingerprint(vbfm_ctx *c)
 
 uint64_t state_layout(vbfm_ctx *c)
 {
-	const int lay = c->estore ? VBFM_LAYOUT_ENTRY : c->lord ? VBFM_LAYOUT_LEVEL : VBFM_LAYOUT_COLUMN;
+	// the online learner: whether its batches run on the per-batch level-ordered store (the
+	// store's data-set sums add a batch's rows in level-0 order)
+	const int lay = c->ov ? (ov_store_on(c) ? VBFM_LAYOUT_LEVEL : VBFM_LAYOUT_COLUMN)
+	                      : c->estore ? VBFM_LAYOUT_ENTRY : c->lord ? VBFM_LAYOUT_LEVEL : VBFM_LAYOUT_COLUMN;
 	return (uint64_t)lay | (uint64_t)c->shard_mode << 8;
 }
 
@@ -1852,7 +1865,7 @@ int vbfm_load_state(vbfm_ctx *c, const char *path, uint32_t *iter)
 	if (!c || !path) return fail(c, "null argument");
 	return guarded(c, [&] {
 		require_train(c);
-		no_partial(c);
+		if (c->part_kind >= 0) no_partial(c);   // (a failed level, -2, is what a restore repairs)
 		CkptFile f(path, "rb");
 		StateHeader h;
 		f.read(&h, sizeof(h));
@@ -1900,6 +1913,7 @@ int vbfm_load_state(vbfm_ctx *c, const char *path, uint32_t *iter)
 		if (h.level_order) rows_level_order(c);
 		c->q_ready[0] = c->q_ready[1] = -1;
 		c->carry = 0;
+		c->part_kind = -1;   // every record restored
 		sync(c);
 		if (iter) *iter = h.iter;
 	});

@@ -57,6 +57,17 @@ template <class T> inline T *dalloc(size_t n)
 	return (T *)p;
 }
 
+// the row-record buffers (RowRec), allocated at least VBFM_REC_ALLOC_MIN bytes (A/B of the
+// allocation's size against the level kernels' scatter rate; default: exactly n records)
+template <class T> inline T *dalloc_rec(size_t n)
+{
+	const char *e = getenv("VBFM_REC_ALLOC_MIN");
+	const size_t want = e ? (size_t)strtoull(e, nullptr, 10) : 0;
+	void *p = nullptr;
+	HIPCHK(hipMalloc(&p, std::max((n ? n : 1) * sizeof(T), want)));
+	return (T *)p;
+}
+
 template <class T> inline void dfree(T *&p)
 {
 	if (p) (void)hipFree((void *)p);
@@ -332,6 +343,8 @@ void mc_state_write(vbfm_ctx *c, CkptFile &f);
 void mc_state_read(vbfm_ctx *c, CkptFile &f);
 // ... and the online learner's (vbfm_online.hip)
 uint64_t ov_state_payload(vbfm_ctx *c);
+// the online learner sweeps its batches on the per-batch level-ordered store (k_ov_lord)
+bool ov_store_on(vbfm_ctx *c);
 void ov_state_write(vbfm_ctx *c, CkptFile &f);
 void ov_state_read(vbfm_ctx *c, CkptFile &f);
 

@@ -123,6 +123,7 @@ struct LevelArgs {
 	double *rho;               // step size of each feature (new_wj / new_vj)
 	const uint32_t *ccount;    // entries of each feature in the whole train set (col_count)
 	uint32_t *tcount;          // w: t_wj (+= batch entries, rho refreshed); v of factor 0: t_vj; else nullptr
+	int x_one;                 // online per-batch store: every train x is 1.0f (no per-entry x load)
 	int hyp_uniform;           // one attribute group: the prior is hyp0 (no per-column lookup)
 	double hyp0;
 	// long columns of the level-ordered store (fused single-rank VB sweep): columns longer than

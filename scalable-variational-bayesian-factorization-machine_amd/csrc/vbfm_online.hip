@@ -472,6 +472,19 @@ __global__ __launch_bounds__(256) void k_ov_lord(LevelArgs a)
 	}
 	const uint32_t o0 = (uint32_t)(cb - wb);   // the column's first record in the run
 	const uint2 *col = a.csc + cb;
+	// x of the lane's first two entries in registers before the barrier (the stats loop then
+	// waits on no CSC load); none at all when every x is 1. `first` is level-uniform on the store.
+	float xr0 = 1.0f, xr1 = 1.0f;
+	if (!a.x_one) {
+		if (lane < n) xr0 = ent_x(col[lane]);
+		if (lane + G < n) xr1 = ent_x(col[lane + G]);
+	}
+	const bool fe_uniform = a.first_level >= 0, fe = a.first_level > 0;   // -1: the per-entry bit (A/B)
+	auto xof = [&](uint32_t i, uint32_t it) -> float {
+		if (a.x_one) return 1.0f;
+		return it == 0 ? xr0 : it == 1 ? xr1 : ent_x(col[i]);
+	};
+	auto fof = [&](uint32_t i) -> bool { return fe_uniform ? fe : (col[i].x & a.first_mask) != 0; };
 	double2 msj = make_double2(0.0, 0.0), natj = make_double2(0.0, 0.0), nx = make_double2(0.0, 0.0);
 	double rho = 0.0, hg = a.hyp0;
 	uint32_t cc = 0, tc = 0;
@@ -509,10 +522,10 @@ __global__ __launch_bounds__(256) void k_ov_lord(LevelArgs a)
 	const double acc = a.alpha * cc;
 	const double rca = rho * cc * a.alpha;
 	double eta1 = 0.0, eta2 = 0.0;
-	for (uint32_t i = lane; i < n; i += G) {
+	for (uint32_t i = lane, it = 0; i < n; i += G, ++it) {
 		Rec r;
 		get(i, r);
-		const float x = ent_x(col[i]);
+		const float x = xof(i, it);
 		if constexpr (IS_W) {
 			const double w_mean = x * (E(r) + x * mo);
 			const double w_sigma_sqr = x * x;   // fp32 product
@@ -561,12 +574,12 @@ __global__ __launch_bounds__(256) void k_ov_lord(LevelArgs a)
 			}
 		}
 	}
-	for (uint32_t i = lane; i < n; i += G) {
+	for (uint32_t i = lane, it = 0; i < n; i += G, ++it) {
 		Rec r;
 		get(i, r);
-		const uint2 e = col[i];
-		if constexpr (IS_W) w_apply<NEXT>(r, ent_x(e), (e.x & a.first_mask) != 0, go, mo, so, mu, sig, nx);
-		else v_apply<P, NEXT>(r, ent_x(e), (e.x & a.first_mask) != 0, go, mo, so, mu, sig, nx);
+		const float x = xof(i, it);
+		if constexpr (IS_W) w_apply<NEXT>(r, x, fof(i), go, mo, so, mu, sig, nx);
+		else v_apply<P, NEXT>(r, x, fof(i), go, mo, so, mu, sig, nx);
 		const uint32_t o = o0 + i;
 		if (o < m) {
 #pragma unroll
@@ -709,6 +722,7 @@ struct OvState {
 	uint32_t launches_v = 0;
 	// the per-batch level-ordered store (k_ov_lord)
 	uint32_t *level_ptr_d = nullptr;   // [L+1] level bounds in level positions
+	bool x_one = false;                // every train x is 1.0f (one-hot): k_ov_lord loads no x
 	uint64_t *lvl_d = nullptr;         // [num_batch * (L+1)] first entry of every level of every batch
 	std::vector<uint64_t> lvl_h;
 	std::vector<uint8_t> batch_lord;   // [num_batch] the batch's levels are complete
@@ -768,6 +782,15 @@ void ov_launch_level(vbfm_ctx *c, LevelArgs &a, uint32_t l, bool is_w)
 	a.dst = o.rows_other;
 	a.lbase = o.lvl_cur[l];
 	a.lnext = o.lnx + (o.lvl_cur[l] - o.lvl_cur[0]);
+	// every level of the store holds each batch row once and a row's features ascend with the
+	// levels: level 0 holds every row's first entry (the ROW_FIRST bit of its CSC entries)
+	a.first_level = l == 0 && a.first_mask != 0;
+	a.x_one = o.x_one;
+	const char *lg = getenv("VBFM_OV_LEGACY");   // A/B: x and the first-entry bit from the CSC per entry
+	if (lg && lg[0] == '1') {
+		a.first_level = -1;
+		a.x_one = 0;
+	}
 	HIPCHK(vbk::ov_lord_level(a, is_w, c->s));
 	std::swap(c->rows, o.rows_other);
 }
@@ -1083,6 +1106,12 @@ int vbfm_online_init(vbfm_ctx *c, const vbfm_online_config *cfg)
 					o.level_ptr_d = dalloc<uint32_t>((size_t)L + 1);
 					HIPCHK(hipMemcpy(o.level_ptr_d, c->level_ptr.data(), ((size_t)L + 1) * 4, hipMemcpyHostToDevice));
 					o.lvl_d = dalloc<uint64_t>((size_t)nb * (L + 1));
+					uint32_t *cnt = dalloc<uint32_t>(1), ne1 = 1;
+					HIPCHK(vbk::count_x_ne1(c->tr.csc, nnz, cnt, c->s));
+					HIPCHK(hipMemcpyAsync(&ne1, cnt, 4, hipMemcpyDeviceToHost, c->s));
+					sync(c);
+					dfree(cnt);
+					o.x_one = ne1 == 0;
 				}
 			}
 			{
@@ -1286,6 +1315,8 @@ namespace vbi {
 namespace {
 constexpr size_t OV_HEAD_WORDS = 8 + 32;   // {num_batch, n_total, t_w0, 0...}, stream window + pad
 }
+
+bool ov_store_on(vbfm_ctx *c) { return c->ov && c->ov->level_ptr_d != nullptr; }
 
 uint64_t ov_state_payload(vbfm_ctx *c)
 {

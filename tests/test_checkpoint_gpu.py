@@ -388,3 +388,25 @@ def test_cli_online_save_state_and_resume(tmp_path):
     it_one = re.findall(r"#Iter=\s*(\d+)\tTest=(\S+)", s_one)
     it_two = re.findall(r"#Iter=\s*(\d+)\tTest=(\S+)", s_two)
     assert len(it_one) == 6 and it_two == it_one[3:]
+
+
+def test_online_checkpoint_refuses_other_store(tmp_path, monkeypatch):
+    """the online learner records whether its batches ran on the per-batch level
+    store in the checkpoint's layout word; resuming under the other layout (whose data-set sums add
+    a batch's rows in another order) is refused before any state is replaced."""
+    tr, te, nf = _data(n=20000)
+    paths = {}
+    for layout in ("auto", "column"):
+        monkeypatch.setenv("VBFM_LAYOUT", layout)
+        a = _ov_learner(tr, te, nf, 4)
+        a.epoch()
+        paths[layout] = str(tmp_path / ("ov_%s.state" % layout))
+        a.save_state(paths[layout])
+        a.close()
+    for layout, other in (("auto", "column"), ("column", "auto")):
+        monkeypatch.setenv("VBFM_LAYOUT", layout)
+        c = _ov_learner(tr, te, nf, 4)
+        with pytest.raises(vbfm.VbfmError, match="another row layout"):
+            c.load_state(paths[other])
+        assert c.load_state(paths[layout]) == 1
+        c.close()

@@ -9,6 +9,7 @@
 #   py=<script>[+args]         python -u <script> <args>
 #   exe=<binary>[+args]        a built probe binary
 #   sq=<CTRS>@<kernel re>@<args>  one --pmc pass of SQ counters (tools/sq_summary.py), list: rocprofv3 -L
+#   pmcpy=<CTRS>@<kernel re>@<script+args>  one --pmc pass of a python script
 #   setenv=NAME=VALUE / unsetenv=NAME   environment of the steps that follow
 # Every step runs under its own timeout; the first failure ends the call.
 cd "$GRAFT_REPO_ROOT" || exit 1
@@ -45,6 +46,11 @@ for step in "$@"; do
       IFS=@ read -r ctrs kre bargs <<< "$arg"
       timeout -s KILL 300 rocprofv3 --pmc ${ctrs//,/ } --kernel-trace --kernel-include-regex "$kre" -d "$O/sq_$n" -o p \
         --output-format csv -- python3 bench.py ${bargs//+/ } > "$O/sq_$n.json" 2> "$O/sq_$n.txt" ;;
+    pmcpy)
+      # pmcpy=<COUNTER,...>@<kernel regex>@<script+args>: one --pmc pass of a python script
+      IFS=@ read -r ctrs kre sargs <<< "$arg"
+      timeout -s KILL 600 rocprofv3 --pmc ${ctrs//,/ } --kernel-trace --kernel-include-regex "$kre" -d "$O/pmcpy_$n" -o p \
+        --output-format csv -- python3 ${sargs//+/ } > "$O/pmcpy_$n.json" 2> "$O/pmcpy_$n.txt" ;;
     list) timeout -s KILL 60 rocprofv3 -L > "$O/counters.txt" 2>&1 ;;
     setenv) export "$arg" ;;          # setenv=NAME=VALUE for the steps that follow
     unsetenv) unset "$arg" ;;
