@@ -63,8 +63,11 @@ template <class T> inline T *dalloc_rec(size_t n)
 {
 	const char *e = getenv("VBFM_REC_ALLOC_MIN");
 	const size_t want = e ? (size_t)strtoull(e, nullptr, 10) : 0;
+	const char *ct = getenv("VBFM_REC_ALLOC_CONTIG");   // A/B: physically contiguous pages
 	void *p = nullptr;
-	HIPCHK(hipMalloc(&p, std::max((n ? n : 1) * sizeof(T), want)));
+	const size_t bytes = std::max((n ? n : 1) * sizeof(T), want);
+	if (ct && ct[0] == '1') HIPCHK(hipExtMallocWithFlags(&p, bytes, hipDeviceMallocContiguous));
+	else HIPCHK(hipMalloc(&p, bytes));
 	return (T *)p;
 }
 

@@ -11,7 +11,9 @@ for i in $(seq 1 30); do
   # not be prepared, back-off)
   notrun=$(python3 -c "import json;d=json.load(open('gpurun_out/.last_call.json'));print(int(d.get('status')=='transient' and not d.get('run_s')))" 2>/dev/null)
   if [ $rc -eq 3 ] || [ "$notrun" = "1" ]; then
-    sleep 90; continue
+    # honour the back-off gpurun asks for ("retry in Ns"), else wait 90 s
+    w=$(grep -o "retry in [0-9]*s" "$log" | tail -1 | grep -o "[0-9]*")
+    sleep $(( ${w:-80} + 10 )); continue
   fi
   exit $rc
 done

@@ -1,13 +1,14 @@
 #!/usr/bin/env python3
 """Summarise a rocprofv3 --pmc pass of SQ counters per kernel (tools/gpu.sh step `sq`).
 
-usage: tools/sq_summary.py <p_counter_collection.csv> [...]
+usage: tools/sq_summary.py <p_counter_collection.csv[.gz]> [...]
 Per kernel: dispatches, mean duration, VGPR / LDS of the dispatch, and every counter's mean per
 dispatch. SQ_WAVE_CYCLES / SQ_WAIT_* / SQ_ACTIVE_INST_* count quad-cycles (MI355X_MICROARCH.md);
 the derived columns are the shares of wave time parked on s_waitcnt / barriers (WAIT_ANY),
 stalled at issue (WAIT_INST_ANY) and issuing (ACTIVE_INST_ANY), and the mean number of resident
 waves per CU (WAVE_CYCLES * 4 / (duration cycles * 256 CUs), at the dispatch's own clock)."""
 import csv
+import gzip
 import sys
 from collections import defaultdict
 
@@ -15,7 +16,7 @@ from collections import defaultdict
 def main():
     for path in sys.argv[1:]:
         k = defaultdict(lambda: {"n": set(), "dur": {}, "c": defaultdict(float), "meta": ""})
-        with open(path) as fh:
+        with (gzip.open(path, "rt") if path.endswith(".gz") else open(path)) as fh:
             for r in csv.DictReader(fh):
                 e = k[r["Kernel_Name"]]
                 did = r["Dispatch_Id"]
@@ -39,8 +40,12 @@ def main():
                          ("SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY") if x in c]
                 print("    shares of wave time: " + ", ".join(parts))
                 if "SQ_BUSY_CYCLES" in c:
-                    # BUSY_CYCLES: cycles the SQs were busy (summed over the SEs / XCDs)
-                    print("    resident waves per busy SQ-cycle: %.1f" % (wc * 4 / c["SQ_BUSY_CYCLES"]))
+                    # BUSY_CYCLES is summed over the 32 shader engines (8 XCDs x 4): / 32 = the
+                    # dispatch's cycles (its ratio to the duration is the clock); WAVE_CYCLES in
+                    # quad-cycles over 256 CUs gives the mean resident waves per CU
+                    cyc = c["SQ_BUSY_CYCLES"] / 32.0
+                    print("    clock %.2f GHz, mean resident waves per CU %.1f" % (
+                        cyc / dur, wc * 4 / (cyc * 256)))
                 if "SQ_WAVES" in c:
                     print("    wave lifetime: %.0f cycles" % (wc * 4 / c["SQ_WAVES"]))
 
