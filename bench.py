@@ -586,6 +586,17 @@ def main():
             tj = json.load(fh)
         traffic = tj.get("bytes_per_launch")
         traffic_source = "%s (earlier PMC profile: %s)" % (os.path.relpath(tf, ROOT), tj.get("source", "?").split(" (")[0])
+    fused_model = None
+    if mc and not split:
+        # the MCMC level kernel also carries the closing train re-prediction of draw_all
+        # (fm_learn_mcmc.h:117-348, a separate pass over every entry in the reference): per factor
+        # and entry the CSC entry (8 B) and the row's running sums (16 B read + 16 B write), on top
+        # of SURVEY's 72 B/nnz draw_v model -- reported beside `roofline`, which keeps SURVEY's
+        # model
+        fb = (112.0 * nnz + 8.0 * N + 16.0 * NF) / max(1, levels)
+        fa = fb / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else 0.0
+        fused_model = {"bytes_per_launch": fb, "achieved": fa, "frac": fa / HBM_PEAK_GBS,
+                       "model": "draw_v 72 B/nnz + fused re-prediction 40 B/nnz per factor"}
     result = {
         "metric": METRIC, "value": value, "unit": "nnz*k/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": elapsed * 1000.0 / args.steps, "higher_is_better": True,
@@ -609,6 +620,7 @@ def main():
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_source,
                      "kernel": kernel, "avg_launch_ms": avg_ms,
                      "launches": n_launch, "bytes_per_launch": bytes_per_launch},
+        "roofline_with_fused_predict": fused_model,
         "factor_sweep_ms_per_step": sweep_ms,
         "factor_sweep_nnz_k_per_s": nnz_total * k / (sweep_ms * 1e-3),
         "test_rmse": rmse_of(stats[-1]),

@@ -360,7 +360,7 @@ void build_lorder(vbfm_ctx *c, const std::vector<uint64_t> &cp, const std::vecto
 	c->lnext = dalloc<uint32_t>(d.nnz);
 	c->lrow0 = dalloc<uint32_t>(n);
 	c->lpos0 = dalloc<uint32_t>(n);
-	c->rows_alt = dalloc_rec<RowRec>(n);
+	c->rows_alt = dalloc<RowRec>(n);
 	uint32_t *tmp = dalloc<uint32_t>(n);
 	auto lev = [&](uint32_t l, uint32_t *&f, uint32_t &nfl, const uint64_t *&lp) {
 		f = c->level_feats + c->level_ptr[l];
@@ -1264,7 +1264,7 @@ static void alloc_rows(vbfm_ctx *c)
 	lord_release(c, false);   // a new train set: the old records are discarded
 	dfree(c->rows);
 	dfree(c->scratch_n);
-	c->rows = dalloc_rec<RowRec>(c->tr.n);
+	c->rows = dalloc<RowRec>(c->tr.n);
 	c->scratch_n = dalloc<double>(c->tr.n);
 	HIPCHK(hipMemsetAsync(c->rows, 0, (size_t)std::max(c->tr.n, 1u) * sizeof(RowRec), c->s));
 	uint64_t n = c->tr.n;

@@ -57,20 +57,6 @@ template <class T> inline T *dalloc(size_t n)
 	return (T *)p;
 }
 
-// the row-record buffers (RowRec), allocated at least VBFM_REC_ALLOC_MIN bytes (A/B of the
-// allocation's size against the level kernels' scatter rate; default: exactly n records)
-template <class T> inline T *dalloc_rec(size_t n)
-{
-	const char *e = getenv("VBFM_REC_ALLOC_MIN");
-	const size_t want = e ? (size_t)strtoull(e, nullptr, 10) : 0;
-	const char *ct = getenv("VBFM_REC_ALLOC_CONTIG");   // A/B: physically contiguous pages
-	void *p = nullptr;
-	const size_t bytes = std::max((n ? n : 1) * sizeof(T), want);
-	if (ct && ct[0] == '1') HIPCHK(hipExtMallocWithFlags(&p, bytes, hipDeviceMallocContiguous));
-	else HIPCHK(hipMalloc(&p, bytes));
-	return (T *)p;
-}
-
 template <class T> inline void dfree(T *&p)
 {
 	if (p) (void)hipFree((void *)p);

@@ -489,7 +489,10 @@ __global__ __launch_bounds__(256) void k_ov_lord(LevelArgs a)
 	double rho = 0.0, hg = a.hyp0;
 	uint32_t cc = 0, tc = 0;
 	const size_t pi = (size_t)j * a.ms_stride;
-	if (n) {   // every per-column load issued here, one dependent step after the feature id
+	// every per-column load issued at once: on field data the feature id is arithmetic
+	// (feat_contig), so these wait for nothing -- not for the column bounds (a column empty in
+	// this batch loads its parameters for nothing)
+	if (live) {
 		msj = a.ms[pi];
 		natj = a.nat[(size_t)j * a.nat_stride];
 		rho = a.rho[j];

@@ -10,6 +10,7 @@
 #   exe=<binary>[+args]        a built probe binary
 #   sq=<CTRS>@<kernel re>@<args>  one --pmc pass of SQ counters (tools/sq_summary.py), list: rocprofv3 -L
 #   pmcpy=<CTRS>@<kernel re>@<script+args>  one --pmc pass of a python script
+#   pmcr=<CTRS>@<kernel re>@<iteration range>@<args>  --pmc pass of bench.py on a dispatch range
 #   setenv=NAME=VALUE / unsetenv=NAME   environment of the steps that follow
 # Every step runs under its own timeout; the first failure ends the call.
 cd "$GRAFT_REPO_ROOT" || exit 1
@@ -51,6 +52,13 @@ for step in "$@"; do
       IFS=@ read -r ctrs kre sargs <<< "$arg"
       timeout -s KILL 600 rocprofv3 --pmc ${ctrs//,/ } --kernel-trace --kernel-include-regex "$kre" -d "$O/pmcpy_$n" -o p \
         --output-format csv -- python3 ${sargs//+/ } > "$O/pmcpy_$n.json" 2> "$O/pmcpy_$n.txt" ;;
+    pmcr)
+      # pmcr=<COUNTER,...>@<kernel regex>@<iteration range>@<bench args>: one --pmc pass of bench.py
+      # counting only the given dispatch iterations of each matching kernel (e.g. [1-400])
+      IFS=@ read -r ctrs kre rng bargs <<< "$arg"
+      timeout -s KILL 900 rocprofv3 --pmc ${ctrs//,/ } --kernel-trace --kernel-include-regex "$kre" \
+        --kernel-iteration-range "$rng" -d "$O/pmcr_$n" -o p --output-format csv -- python3 bench.py ${bargs//+/ } \
+        > "$O/pmcr_$n.json" 2> "$O/pmcr_$n.txt" ;;
     list) timeout -s KILL 60 rocprofv3 -L > "$O/counters.txt" 2>&1 ;;
     setenv) export "$arg" ;;          # setenv=NAME=VALUE for the steps that follow
     unsetenv) unset "$arg" ;;
