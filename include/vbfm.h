@@ -308,6 +308,8 @@ typedef struct {
 	uint32_t n_vlevel_launches;   /* level launches of the factor sweeps */
 	uint64_t nnz_train;
 	uint32_t n_lord_batches;      /* batches swept on their level-ordered store (complete levels) */
+	uint32_t n_pad_batches;       /* ... of which with the padded layout of levels >= 1 (fills the
+	                               * struct's tail padding: its size is unchanged) */
 } vbfm_online_stats;
 
 int vbfm_online_init(vbfm_ctx *ctx, const vbfm_online_config *cfg);

@@ -124,6 +124,9 @@ struct LevelArgs {
 	const uint32_t *ccount;    // entries of each feature in the whole train set (col_count)
 	uint32_t *tcount;          // w: t_wj (+= batch entries, rho refreshed); v of factor 0: t_vj; else nullptr
 	int x_one;                 // online per-batch store: every train x is 1.0f (no per-entry x load)
+	uint32_t pad_cap;          // online per-batch store, levels >= 1: workgroup w's run sits at record
+	                           // w * pad_cap of the level's buffer (no column-bound load before the
+	                           // run's loads); 0: runs packed (positions from the column bounds)
 	int hyp_uniform;           // one attribute group: the prior is hyp0 (no per-column lookup)
 	double hyp0;
 	// long columns of the level-ordered store (fused single-rank VB sweep): columns longer than
@@ -344,6 +347,9 @@ hipError_t unpack_pairs(const double2 *in, double *a, double *b, uint32_t rows, 
 hipError_t ov_level(const LevelArgs &a, int is_w, hipStream_t s);
 // the same on the batch's level-ordered store (a.src / a.dst / a.lnext / a.lbase)
 hipError_t ov_lord_level(const LevelArgs &a, int is_w, hipStream_t s);
+// lanes per column of that kernel for a batch mean column length m; its padded slot size
+uint32_t ov_lord_g(uint32_t m);
+uint32_t ov_pad_cap();
 // MCMC / ALS (vbfm_mcmc.hip); mode 0: fused, 1: statistics only (into a.stats),
 // 2: draw + correction from the (all-reduced) a.stats
 hipError_t mc_v_level(const McArgs &a, int mode, hipStream_t s);

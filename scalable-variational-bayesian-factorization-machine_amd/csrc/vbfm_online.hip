@@ -401,23 +401,71 @@ DEVI uint32_t ov_level_of(const uint64_t *base, uint32_t L, uint64_t g)
 	return lo;
 }
 
+// The padded layout (levels >= 1 of a batch whose every workgroup run fits PAD_CAP records): the
+// run of workgroup w (level columns [w cpw, (w+1) cpw), cpw = 256 / G of the level's kernel) starts
+// at record w * PAD_CAP of the level's buffer, so a level kernel issues its run's loads at once
+// instead of after a load of the run's column bound. Level 0 stays packed (the data-set sums of
+// the batch read its records in level-0 order, n of them).
+struct OvPad {
+	const uint64_t *gp;        // the batch's col_ptr by level position (o.gptr + b * nf)
+	const uint32_t *lptr;      // level_ptr [L+1]
+	const uint32_t *cpw;       // columns per workgroup of each level
+	uint32_t cap;              // PAD_CAP, or 0: every level packed
+	const uint64_t *off;       // [L] start of each level's lnx region (packed: base[l] - base[0])
+};
+
+// position of entry g (level l) in its level's record buffer
+DEVI uint32_t ov_slot_pos(const OvPad &pd, const uint64_t *base, uint32_t l, uint64_t g)
+{
+	if (pd.cap == 0 || l == 0) return (uint32_t)(g - base[l]);
+	uint32_t lo = pd.lptr[l], hi = pd.lptr[l + 1];   // the last column position p with gp[p] <= g
+	while (hi - lo > 1) {
+		const uint32_t mid = (lo + hi) >> 1;
+		if (pd.gp[mid] <= g) lo = mid;
+		else hi = mid;
+	}
+	const uint32_t w = (lo - pd.lptr[l]) / pd.cpw[l];
+	return w * pd.cap + (uint32_t)(g - pd.gp[pd.lptr[l] + w * pd.cpw[l]]);
+}
+
 // pos[l * n + row] = position of the row in level l; base[L+1] = first entry of every level
-__global__ void k_ov_lord_pos(const uint2 *ent, const uint64_t *base, uint32_t L, uint32_t n, uint32_t *pos)
+__global__ void k_ov_lord_pos(const uint2 *ent, const uint64_t *base, uint32_t L, uint32_t n, uint32_t *pos, OvPad pd)
 {
 	const uint64_t g = base[0] + (uint64_t)blockIdx.x * 256u + threadIdx.x;
 	if (g >= base[L]) return;
 	const uint32_t l = ov_level_of(base, L, g);
-	pos[(size_t)l * n + (ent[g].x & ROW_MASK)] = (uint32_t)(g - base[l]);
+	pos[(size_t)l * n + (ent[g].x & ROW_MASK)] = ov_slot_pos(pd, base, l, g);
 }
 
-// lnx[g - base[0]] = the entry's row position in the next level (the last level -> level 0)
+// lnx[off[l] + the entry's position] = the entry's row position in the next level (the last level
+// -> level 0)
 __global__ void k_ov_lord_next(const uint2 *ent, const uint64_t *base, uint32_t L, uint32_t n, const uint32_t *pos,
-                               uint32_t *lnx)
+                               uint32_t *lnx, OvPad pd)
 {
 	const uint64_t g = base[0] + (uint64_t)blockIdx.x * 256u + threadIdx.x;
 	if (g >= base[L]) return;
 	const uint32_t l = ov_level_of(base, L, g), ln = l + 1 == L ? 0 : l + 1;
-	lnx[g - base[0]] = pos[(size_t)ln * n + (ent[g].x & ROW_MASK)];
+	lnx[pd.off[l] + ov_slot_pos(pd, base, l, g)] = pos[(size_t)ln * n + (ent[g].x & ROW_MASK)];
+}
+
+// per batch: does some workgroup run of a level >= 1 exceed PAD_CAP records? (thread per
+// (batch, level position): the positions that start a workgroup's columns)
+__global__ void k_ov_pad_check(const uint64_t *gptr, const uint32_t *lptr, const uint32_t *cpw, uint32_t L,
+                               uint32_t nf, uint32_t nb, uint32_t cap, uint32_t *bad)
+{
+	const uint64_t i = (uint64_t)blockIdx.x * 256u + threadIdx.x;
+	if (i >= (uint64_t)nb * nf) return;
+	const uint32_t b = (uint32_t)(i / nf), p = (uint32_t)(i % nf);
+	uint32_t lo = 0, hi = L;   // the level of position p: lptr[lo] <= p < lptr[lo + 1]
+	while (hi - lo > 1) {
+		const uint32_t mid = (lo + hi) >> 1;
+		if (lptr[mid] <= p) lo = mid;
+		else hi = mid;
+	}
+	if (lo == 0 || (p - lptr[lo]) % cpw[lo] != 0) return;
+	const uint32_t e = min(p + cpw[lo], lptr[lo + 1]);
+	const uint64_t *g = gptr + (size_t)b * nf;
+	if (g[e] - g[p] > cap) bad[b] = 1u;
 }
 
 // One level of the w (IS_W) or v sweep of a mini-batch on the level-ordered store. A workgroup
@@ -432,7 +480,7 @@ constexpr uint32_t OV_CAP = 512;
 
 DEVI uint32_t ov_slot(uint32_t i, uint32_t c) { return i * 4 + (c ^ ((i >> 2) & 3)); }
 
-template <int G, bool IS_W, int P, bool NEXT>
+template <int G, bool IS_W, int P, bool NEXT, bool PAD>
 __global__ __launch_bounds__(256) void k_ov_lord(LevelArgs a)
 {
 	static_assert(G <= 64, "lane groups inside one wave");
@@ -442,6 +490,8 @@ __global__ __launch_bounds__(256) void k_ov_lord(LevelArgs a)
 	const uint32_t c1 = min(c0 + 256 / G, a.nfeat);
 	const uint64_t wb = a.col_ptr[c0], we = a.col_ptr[c1];
 	const uint32_t m = (uint32_t)min<uint64_t>(we - wb, OV_CAP);
+	// the run's first record in the level's buffer: from the column bound, or (PAD) the slot
+	const uint32_t rb = PAD ? blockIdx.x * OV_CAP : (uint32_t)(wb - a.lbase);
 	// the column's id and bounds first: the per-column loads that depend on them then wait
 	// for these only, not for the run's pieces issued in between
 	const uint32_t col_i = c0 + threadIdx.x / G;
@@ -458,17 +508,33 @@ __global__ __launch_bounds__(256) void k_ov_lord(LevelArgs a)
 	const uint32_t ks = (np + 255) / 256, kd = (m + 255) / 256;
 	double2 sv[KS];
 	uint32_t dv[KD];
-	const double2 *s2 = reinterpret_cast<const double2 *>(a.src + (wb - a.lbase));
-	const uint32_t *nx2 = a.lnext + (wb - a.lbase);
+	const double2 *s2 = reinterpret_cast<const double2 *>(a.src + rb);
+	const uint32_t *nx2 = a.lnext + rb;
+	if constexpr (PAD) {
+		// the slot's first KP rounds (320 records: the run is 256 +- 16 at C3's batch shape) and
+		// every next position are loaded at once; the rest only if the run is that long
+		constexpr int KP = 5;
 #pragma unroll
-	for (int k = 0; k < KS; ++k) {
-		sv[k] = make_double2(0.0, 0.0);
-		if (k < (int)ks) sv[k] = s2[min(threadIdx.x + k * 256, np - 1)];
-	}
+		for (int k = 0; k < KS; ++k) {
+			sv[k] = make_double2(0.0, 0.0);
+			if (k < KP) sv[k] = s2[threadIdx.x + k * 256];
+		}
 #pragma unroll
-	for (int k = 0; k < KD; ++k) {
-		dv[k] = 0;
-		if (k < (int)kd) dv[k] = nx2[min(threadIdx.x + k * 256, m - 1)];
+		for (int k = 0; k < KD; ++k) dv[k] = nx2[threadIdx.x + k * 256];
+#pragma unroll
+		for (int k = KP; k < KS; ++k)
+			if (k < (int)ks) sv[k] = s2[threadIdx.x + k * 256];
+	} else {
+#pragma unroll
+		for (int k = 0; k < KS; ++k) {
+			sv[k] = make_double2(0.0, 0.0);
+			if (k < (int)ks) sv[k] = s2[min(threadIdx.x + k * 256, np - 1)];
+		}
+#pragma unroll
+		for (int k = 0; k < KD; ++k) {
+			dv[k] = 0;
+			if (k < (int)kd) dv[k] = nx2[min(threadIdx.x + k * 256, m - 1)];
+		}
 	}
 	const uint32_t o0 = (uint32_t)(cb - wb);   // the column's first record in the run
 	const uint2 *col = a.csc + cb;
@@ -517,7 +583,7 @@ __global__ __launch_bounds__(256) void k_ov_lord(LevelArgs a)
 #pragma unroll
 			for (uint32_t c = 0; c < 4; ++c) r[c] = stage[ov_slot(o, c)];
 		} else {
-			load_rec(a.src, (uint32_t)(wb - a.lbase) + o, r);
+			load_rec(a.src, rb + o, r);
 		}
 	};
 	const double mo = msj.x, so = msj.y;
@@ -588,7 +654,7 @@ __global__ __launch_bounds__(256) void k_ov_lord(LevelArgs a)
 #pragma unroll
 			for (uint32_t c = 0; c < 4; ++c) stage[ov_slot(o, c)] = r[c];
 		} else {
-			store_rec(a.dst, a.lnext[(wb - a.lbase) + o], r);
+			store_rec(a.dst, a.lnext[rb + o], r);
 		}
 	}
 	__syncthreads();
@@ -629,21 +695,28 @@ hipError_t launch_ov(const LevelArgs &a, int is_w, hipStream_t s)
 	return hipGetLastError();
 }
 
-template <int G>
-hipError_t launch_ov_lord(const LevelArgs &a, int is_w, hipStream_t s)
+template <int G, bool PAD>
+void launch_ov_lord_pad(const LevelArgs &a, int is_w, hipStream_t s)
 {
 	const unsigned grid = (a.nfeat + 256 / G - 1) / (256 / G);
 	const bool nx = a.ms_next != nullptr;
 	if (is_w) {
-		if (nx) k_ov_lord<G, true, 0, true><<<grid, 256, 0, s>>>(a);
-		else k_ov_lord<G, true, 0, false><<<grid, 256, 0, s>>>(a);
+		if (nx) k_ov_lord<G, true, 0, true, PAD><<<grid, 256, 0, s>>>(a);
+		else k_ov_lord<G, true, 0, false, PAD><<<grid, 256, 0, s>>>(a);
 	} else if (a.slot == 0) {
-		if (nx) k_ov_lord<G, false, 0, true><<<grid, 256, 0, s>>>(a);
-		else k_ov_lord<G, false, 0, false><<<grid, 256, 0, s>>>(a);
+		if (nx) k_ov_lord<G, false, 0, true, PAD><<<grid, 256, 0, s>>>(a);
+		else k_ov_lord<G, false, 0, false, PAD><<<grid, 256, 0, s>>>(a);
 	} else {
-		if (nx) k_ov_lord<G, false, 1, true><<<grid, 256, 0, s>>>(a);
-		else k_ov_lord<G, false, 1, false><<<grid, 256, 0, s>>>(a);
+		if (nx) k_ov_lord<G, false, 1, true, PAD><<<grid, 256, 0, s>>>(a);
+		else k_ov_lord<G, false, 1, false, PAD><<<grid, 256, 0, s>>>(a);
 	}
+}
+
+template <int G>
+hipError_t launch_ov_lord(const LevelArgs &a, int is_w, hipStream_t s)
+{
+	if (a.pad_cap) launch_ov_lord_pad<G, true>(a, is_w, s);
+	else launch_ov_lord_pad<G, false>(a, is_w, s);
 	return hipGetLastError();
 }
 
@@ -651,13 +724,22 @@ hipError_t launch_ov_lord(const LevelArgs &a, int is_w, hipStream_t s)
 hipError_t ov_lord_level(const LevelArgs &a, int is_w, hipStream_t s)
 {
 	if (a.nfeat == 0) return hipSuccess;
-	const uint32_t m = a.avg_len;
-	if (m <= 6) return launch_ov_lord<4>(a, is_w, s);
-	if (m <= 12) return launch_ov_lord<8>(a, is_w, s);
-	if (m <= 24) return launch_ov_lord<16>(a, is_w, s);
-	if (m <= 48) return launch_ov_lord<32>(a, is_w, s);
-	return launch_ov_lord<64>(a, is_w, s);
+	if (a.pad_cap && a.pad_cap != OV_CAP) return hipErrorInvalidValue;
+	switch (ov_lord_g(a.avg_len)) {
+	case 4: return launch_ov_lord<4>(a, is_w, s);
+	case 8: return launch_ov_lord<8>(a, is_w, s);
+	case 16: return launch_ov_lord<16>(a, is_w, s);
+	case 32: return launch_ov_lord<32>(a, is_w, s);
+	default: return launch_ov_lord<64>(a, is_w, s);
+	}
 }
+
+uint32_t ov_lord_g(uint32_t m)
+{
+	return m <= 6 ? 4 : m <= 12 ? 8 : m <= 24 ? 16 : m <= 48 ? 32 : 64;
+}
+
+uint32_t ov_pad_cap() { return OV_CAP; }
 
 // lanes per column from the batch's mean column length (LevelArgs::avg_len, set by
 // ov_level_args): about one entry per lane
@@ -726,6 +808,16 @@ struct OvState {
 	// the per-batch level-ordered store (k_ov_lord)
 	uint32_t *level_ptr_d = nullptr;   // [L+1] level bounds in level positions
 	bool x_one = false;                // every train x is 1.0f (one-hot): k_ov_lord loads no x
+	// the padded layout of levels >= 1 (OvPad): columns per workgroup of every level, each level's
+	// slot count, the padded levels' lnx prefix (batch-independent), the batches it applies to
+	uint32_t *cpw_d = nullptr, *pad_bad_d = nullptr;
+	uint64_t *lnx_off_d = nullptr;     // [L] lnx region of each level for the current batch
+	std::vector<uint32_t> cpw_h, ngroups_h;
+	std::vector<uint64_t> pad_prefix;  // [L + 1] sum over levels 1..l-1 of ngroups * cap
+	std::vector<uint8_t> batch_pad;    // [num_batch]
+	uint64_t pad_rows = 0;             // records a padded level's buffer needs (max over levels)
+	bool pad_on = false;               // the batch being processed uses the padded layout
+	uint32_t cur_n = 0;                // its rows
 	uint64_t *lvl_d = nullptr;         // [num_batch * (L+1)] first entry of every level of every batch
 	std::vector<uint64_t> lvl_h;
 	std::vector<uint8_t> batch_lord;   // [num_batch] the batch's levels are complete
@@ -750,6 +842,7 @@ void ov_free(vbfm_ctx *c)
 	dfree(o.gptr); dfree(o.lvcp); dfree(o.rstart_d); dfree(o.tmp); dfree(o.rp_b); dfree(o.len_b); dfree(o.csr_b); dfree(o.t_b);
 	dfree(o.rows_b);
 	dfree(o.level_ptr_d); dfree(o.lvl_d); dfree(o.lpos); dfree(o.lnx); dfree(o.rows_b2);
+	dfree(o.cpw_d); dfree(o.pad_bad_d); dfree(o.lnx_off_d);
 	for (hipEvent_t e : o.ev)
 		if (e) (void)hipEventDestroy(e);
 	for (hipEvent_t e : o.bev) (void)hipEventDestroy(e);
@@ -785,6 +878,10 @@ void ov_launch_level(vbfm_ctx *c, LevelArgs &a, uint32_t l, bool is_w)
 	a.dst = o.rows_other;
 	a.lbase = o.lvl_cur[l];
 	a.lnext = o.lnx + (o.lvl_cur[l] - o.lvl_cur[0]);
+	if (o.pad_on && l > 0) {   // the padded layout: slot w of the level's buffer, lnx likewise
+		a.pad_cap = vbk::ov_pad_cap();
+		a.lnext = o.lnx + o.cur_n + o.pad_prefix[l];
+	}
 	// every level of the store holds each batch row once and a row's features ascend with the
 	// levels: level 0 holds every row's first entry (the ROW_FIRST bit of its CSC entries)
 	a.first_level = l == 0 && a.first_mask != 0;
@@ -898,6 +995,18 @@ void ov_regroup(vbfm_ctx *c)
 			for (uint32_t l = 0; l < L && ok; l++) ok = o.lvl_h[(size_t)b * (L + 1) + l + 1] - o.lvl_h[(size_t)b * (L + 1) + l] == n;
 			o.batch_lord[b] = ok;
 		}
+	// the padded layout of levels >= 1: every workgroup run of the batch must fit its slot
+	o.batch_pad.assign(nb, 0);
+	if (o.cpw_d && L > 1) {
+		HIPCHK(hipMemsetAsync(o.pad_bad_d, 0, (size_t)nb * 4, c->s));
+		k_ov_pad_check<<<grid_of((uint64_t)nb * nf), 256, 0, c->s>>>(o.gptr, o.level_ptr_d, o.cpw_d, L, nf, nb,
+		                                                          vbk::ov_pad_cap(), o.pad_bad_d);
+		HIPCHK(hipGetLastError());
+		std::vector<uint32_t> bad(nb);
+		HIPCHK(hipMemcpyAsync(bad.data(), o.pad_bad_d, (size_t)nb * 4, hipMemcpyDeviceToHost, c->s));
+		sync(c);
+		for (uint32_t b = 0; b < nb; b++) o.batch_pad[b] = o.batch_lord[b] && !bad[b];
+	}
 }
 
 // the per-batch store: positions of the batch's rows in every level and every entry's
@@ -909,19 +1018,34 @@ void ov_lord_begin(vbfm_ctx *c, uint32_t b, uint32_t n, uint64_t nnz)
 	if (n > o.lord_cap_rows) {
 		dfree(o.lpos); dfree(o.rows_b2);
 		o.lpos = dalloc<uint32_t>((size_t)L * n);
-		o.rows_b2 = dalloc<RowRec>(n);
+		o.rows_b2 = dalloc<RowRec>(std::max<uint64_t>(n, o.pad_rows));
 		o.lord_cap_rows = n;
 	}
-	if (nnz > o.lord_cap_nnz) {
+	const bool pad = !o.batch_pad.empty() && o.batch_pad[b];
+	const uint64_t lnx_need = pad ? n + o.pad_prefix[L] : nnz;
+	if (lnx_need > o.lord_cap_nnz) {
 		dfree(o.lnx);
-		o.lnx = dalloc<uint32_t>(nnz);
-		o.lord_cap_nnz = nnz;
+		o.lnx = dalloc<uint32_t>(lnx_need);
+		o.lord_cap_nnz = lnx_need;
 	}
 	const uint64_t *base = o.lvl_d + (size_t)b * (L + 1);
-	k_ov_lord_pos<<<grid_of(nnz), 256, 0, c->s>>>(o.ent_sorted, base, L, n, o.lpos);
+	OvPad pd = {o.gptr + (size_t)b * c->tr.nf, o.level_ptr_d, o.cpw_d, 0u, o.lnx_off_d};
+	{
+		// each level's lnx region: packed (base[l] - base[0]) or, padded, level 0's n entries and
+		// then every level's slots
+		std::vector<uint64_t> off(L);
+		for (uint32_t l = 0; l < L; l++)
+			off[l] = pad ? (l == 0 ? 0 : n + o.pad_prefix[l]) : o.lvl_h[(size_t)b * (L + 1) + l] - o.lvl_h[(size_t)b * (L + 1)];
+		HIPCHK(hipMemcpyAsync(o.lnx_off_d, off.data(), (size_t)L * 8, hipMemcpyHostToDevice, c->s));
+		sync(c);   // (off is a host temporary)
+		if (pad) pd.cap = vbk::ov_pad_cap();
+	}
+	k_ov_lord_pos<<<grid_of(nnz), 256, 0, c->s>>>(o.ent_sorted, base, L, n, o.lpos, pd);
 	HIPCHK(hipGetLastError());
-	k_ov_lord_next<<<grid_of(nnz), 256, 0, c->s>>>(o.ent_sorted, base, L, n, o.lpos, o.lnx);
+	k_ov_lord_next<<<grid_of(nnz), 256, 0, c->s>>>(o.ent_sorted, base, L, n, o.lpos, o.lnx, pd);
 	HIPCHK(hipGetLastError());
+	o.pad_on = pad;
+	o.cur_n = n;
 	HIPCHK(vbk::rows_scatter(o.rows_b2, c->rows, o.lpos, n, c->s));   // row r -> its level-0 position
 	o.rows_other = c->rows;
 	c->rows = o.rows_b2;
@@ -937,7 +1061,8 @@ void ov_batch_capacity(vbfm_ctx *c, uint32_t n, uint64_t nnz)
 		o.rp_b = dalloc<uint64_t>((size_t)n + 1);
 		o.len_b = dalloc<uint64_t>((size_t)n + 1);
 		o.t_b = dalloc<float>(n);
-		o.rows_b = dalloc<RowRec>(n);
+		// also a padded level's buffer (ping-pong partner of rows_b2)
+		o.rows_b = dalloc<RowRec>(std::max<uint64_t>(n, o.pad_rows));
 		o.cap_rows = n;
 	}
 	if (nnz > o.cap_nnz) {
@@ -1115,6 +1240,28 @@ int vbfm_online_init(vbfm_ctx *c, const vbfm_online_config *cfg)
 					sync(c);
 					dfree(cnt);
 					o.x_one = ne1 == 0;
+					// the padded layout (VBFM_OV_PAD=0: packed runs at every level); the lanes per
+					// column of a level's kernel follow its mean batch column (ov_level_args)
+					const char *pe = getenv("VBFM_OV_PAD");
+					if (!(pe && pe[0] == '0') && L > 1) {
+						const uint32_t cap = vbk::ov_pad_cap();
+						o.cpw_h.assign(L, 0);
+						o.ngroups_h.assign(L, 0);
+						o.pad_prefix.assign((size_t)L + 1, 0);
+						for (uint32_t l = 0; l < L; l++) {
+							const uint32_t nfl = c->level_ptr[l + 1] - c->level_ptr[l];
+							o.cpw_h[l] = 256 / vbk::ov_lord_g(c->level_avg[l] / std::max(nb, 1u));
+							o.ngroups_h[l] = (nfl + o.cpw_h[l] - 1) / o.cpw_h[l];
+						}
+						for (uint32_t l = 1; l < L; l++) {
+							o.pad_prefix[l + 1] = o.pad_prefix[l] + (uint64_t)o.ngroups_h[l] * cap;
+							o.pad_rows = std::max<uint64_t>(o.pad_rows, (uint64_t)o.ngroups_h[l] * cap);
+						}
+						o.cpw_d = dalloc<uint32_t>(L);
+						HIPCHK(hipMemcpy(o.cpw_d, o.cpw_h.data(), (size_t)L * 4, hipMemcpyHostToDevice));
+						o.pad_bad_d = dalloc<uint32_t>(nb);
+					}
+					o.lnx_off_d = dalloc<uint64_t>(L);
 				}
 			}
 			{
@@ -1163,6 +1310,7 @@ int vbfm_online_epoch(vbfm_ctx *c, vbfm_online_stats *out)
 		const uint64_t n_global_full = c->n_global;
 		auto restore = [&] {
 			o.lord_on = false;
+			o.pad_on = false;
 			c->tr = full;
 			c->rows = rows_full;
 			c->n_global = n_global_full;
@@ -1204,9 +1352,11 @@ int vbfm_online_epoch(vbfm_ctx *c, vbfm_online_stats *out)
 				HIPCHK(vbk::predict_et(c->tr.row_ptr, c->tr.csr, c->ms_v, c->ms_w, c->k, c->k1, c->k0, c->mu0, c->s0d,
 				                       c->tr.target, c->scratch_n, c->rows, n, bl, c->s));
 				o.lord_on = false;
+				o.pad_on = false;
 				if (o.batch_lord[b]) {
 					ov_lord_begin(c, b, n, nnz);
 					st.n_lord_batches++;
+					if (o.pad_on) st.n_pad_batches++;
 				}
 				// update_all(train1, train.num_cases) (fm_learn_vb_online.h:354-469)
 				HIPCHK(hipEventRecord(bev[1], c->s));

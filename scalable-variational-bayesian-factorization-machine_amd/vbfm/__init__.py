@@ -128,7 +128,8 @@ class OnlineStats(C.Structure):
                 + [("num_levels", C.c_int32), ("ms_regroup", C.c_double), ("ms_batches", C.c_double),
                    ("ms_test", C.c_double), ("ms_total", C.c_double), ("ms_predict", C.c_double),
                    ("ms_w0", C.c_double), ("ms_w", C.c_double), ("ms_v", C.c_double), ("ms_hyper", C.c_double),
-                   ("n_vlevel_launches", C.c_uint32), ("nnz_train", C.c_uint64), ("n_lord_batches", C.c_uint32)])
+                   ("n_vlevel_launches", C.c_uint32), ("nnz_train", C.c_uint64), ("n_lord_batches", C.c_uint32),
+                   ("n_pad_batches", C.c_uint32)])
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}

@@ -138,3 +138,31 @@ def test_online_deterministic(synth_files, sa_split):
         runs.append(([s.rmse for s in st], f.get_params()["mu_v"]))
     assert runs[0][0] == runs[1][0]
     np.testing.assert_array_equal(runs[0][1], runs[1][1])
+
+
+@pytest.mark.parametrize("xmode", [0, 1])
+def test_online_padded_store_bit_identical(xmode, monkeypatch):
+    """The per-batch store's padded layout (levels >= 1: workgroup w's run at slot w * 512, so a
+    level kernel loads its run before the column bounds arrive) moves the same records through the
+    same lanes: epochs and parameters equal the packed layout (VBFM_OV_PAD=0) bit for bit, one-hot
+    (no x loads) and with stored x."""
+    import synth
+    n, F, S, k, nb = 40000, 6, 100, 3, 10
+    rp, f, v, y = synth.generate(n, F, S, 51, xmode)
+    te = synth.generate(1000, F, S, 52, xmode)
+    res = {}
+    for pad in ("1", "0"):
+        monkeypatch.setenv("VBFM_OV_PAD", pad)
+        g = vbfm.FMLearnVBOnline(1, 1, k, F * S, min_target=float(y.min()), max_target=float(y.max()))
+        g.set_data(vbfm.DataSubset.from_csr(rp, f, v, y, F * S), vbfm.DataSubset.from_csr(*te, F * S))
+        g.init(7, 0.1, nb)
+        st = [g.epoch() for _ in range(3)]
+        assert st[-1].n_lord_batches == nb
+        assert st[-1].n_pad_batches == (nb if pad == "1" else 0)
+        p = g.get_params()
+        res[pad] = ([(s.rmse, s.mae, s.free_energy_first, s.free_energy_last, s.alpha) for s in st],
+                    {key: np.asarray(p[key]) for key in ("mu_w", "sigma_w", "mu_v", "sigma_v")})
+        g.close()
+    assert res["1"][0] == res["0"][0]
+    for key in res["0"][1]:
+        np.testing.assert_array_equal(res["1"][1][key], res["0"][1][key], err_msg=key)
