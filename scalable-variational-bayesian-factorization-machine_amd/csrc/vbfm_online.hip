@@ -414,38 +414,51 @@ struct OvPad {
 	const uint64_t *off;       // [L] start of each level's lnx region (packed: base[l] - base[0])
 };
 
-// position of entry g (level l) in its level's record buffer
-DEVI uint32_t ov_slot_pos(const OvPad &pd, const uint64_t *base, uint32_t l, uint64_t g)
+// level of level position p (lptr[l] <= p < lptr[l + 1])
+DEVI uint32_t ov_level_of_pos(const uint32_t *lptr, uint32_t L, uint32_t p)
 {
-	if (pd.cap == 0 || l == 0) return (uint32_t)(g - base[l]);
-	uint32_t lo = pd.lptr[l], hi = pd.lptr[l + 1];   // the last column position p with gp[p] <= g
+	uint32_t lo = 0, hi = L;
 	while (hi - lo > 1) {
 		const uint32_t mid = (lo + hi) >> 1;
-		if (pd.gp[mid] <= g) lo = mid;
+		if (lptr[mid] <= p) lo = mid;
 		else hi = mid;
 	}
-	const uint32_t w = (lo - pd.lptr[l]) / pd.cpw[l];
-	return w * pd.cap + (uint32_t)(g - pd.gp[pd.lptr[l] + w * pd.cpw[l]]);
+	return lo;
 }
 
-// pos[l * n + row] = position of the row in level l; base[L+1] = first entry of every level
-__global__ void k_ov_lord_pos(const uint2 *ent, const uint64_t *base, uint32_t L, uint32_t n, uint32_t *pos, OvPad pd)
+// one thread per column (level position p) of the batch: its entries g in [gp[p], gp[p+1]) sit at
+// position g - first in the level's buffer, first = the level's first entry (packed) or, padded
+// (levels >= 1), first = the start of the workgroup run that holds column p minus its slot w * cap
+DEVI uint64_t ov_col_first(const OvPad &pd, const uint64_t *base, uint32_t l, uint32_t p)
 {
-	const uint64_t g = base[0] + (uint64_t)blockIdx.x * 256u + threadIdx.x;
-	if (g >= base[L]) return;
-	const uint32_t l = ov_level_of(base, L, g);
-	pos[(size_t)l * n + (ent[g].x & ROW_MASK)] = ov_slot_pos(pd, base, l, g);
+	if (pd.cap == 0 || l == 0) return base[l];
+	const uint32_t w = (p - pd.lptr[l]) / pd.cpw[l];
+	return pd.gp[pd.lptr[l] + w * pd.cpw[l]] - (uint64_t)w * pd.cap;
+}
+
+// pos[l * n + row] = position of the row in level l
+__global__ void k_ov_lord_pos(const uint2 *ent, const uint64_t *base, uint32_t L, uint32_t nf, uint32_t n, uint32_t *pos,
+                              OvPad pd)
+{
+	const uint32_t p = blockIdx.x * 256u + threadIdx.x;
+	if (p >= nf) return;
+	const uint32_t l = ov_level_of_pos(pd.lptr, L, p);
+	const uint64_t first = ov_col_first(pd, base, l, p);
+	for (uint64_t g = pd.gp[p]; g < pd.gp[p + 1]; ++g) pos[(size_t)l * n + (ent[g].x & ROW_MASK)] = (uint32_t)(g - first);
 }
 
 // lnx[off[l] + the entry's position] = the entry's row position in the next level (the last level
 // -> level 0)
-__global__ void k_ov_lord_next(const uint2 *ent, const uint64_t *base, uint32_t L, uint32_t n, const uint32_t *pos,
-                               uint32_t *lnx, OvPad pd)
+__global__ void k_ov_lord_next(const uint2 *ent, const uint64_t *base, uint32_t L, uint32_t nf, uint32_t n,
+                               const uint32_t *pos, uint32_t *lnx, OvPad pd)
 {
-	const uint64_t g = base[0] + (uint64_t)blockIdx.x * 256u + threadIdx.x;
-	if (g >= base[L]) return;
-	const uint32_t l = ov_level_of(base, L, g), ln = l + 1 == L ? 0 : l + 1;
-	lnx[pd.off[l] + ov_slot_pos(pd, base, l, g)] = pos[(size_t)ln * n + (ent[g].x & ROW_MASK)];
+	const uint32_t p = blockIdx.x * 256u + threadIdx.x;
+	if (p >= nf) return;
+	const uint32_t l = ov_level_of_pos(pd.lptr, L, p), ln = l + 1 == L ? 0 : l + 1;
+	const uint64_t first = ov_col_first(pd, base, l, p);
+	uint32_t *dst = lnx + pd.off[l];
+	for (uint64_t g = pd.gp[p]; g < pd.gp[p + 1]; ++g)
+		dst[g - first] = pos[(size_t)ln * n + (ent[g].x & ROW_MASK)];
 }
 
 // per batch: does some workgroup run of a level >= 1 exceed PAD_CAP records? (thread per
@@ -1040,9 +1053,10 @@ void ov_lord_begin(vbfm_ctx *c, uint32_t b, uint32_t n, uint64_t nnz)
 		sync(c);   // (off is a host temporary)
 		if (pad) pd.cap = vbk::ov_pad_cap();
 	}
-	k_ov_lord_pos<<<grid_of(nnz), 256, 0, c->s>>>(o.ent_sorted, base, L, n, o.lpos, pd);
+	const uint32_t nf = c->tr.nf;
+	k_ov_lord_pos<<<grid_of(nf), 256, 0, c->s>>>(o.ent_sorted, base, L, nf, n, o.lpos, pd);
 	HIPCHK(hipGetLastError());
-	k_ov_lord_next<<<grid_of(nnz), 256, 0, c->s>>>(o.ent_sorted, base, L, n, o.lpos, o.lnx, pd);
+	k_ov_lord_next<<<grid_of(nf), 256, 0, c->s>>>(o.ent_sorted, base, L, nf, n, o.lpos, o.lnx, pd);
 	HIPCHK(hipGetLastError());
 	o.pad_on = pad;
 	o.cur_n = n;
