@@ -414,51 +414,50 @@ struct OvPad {
 	const uint64_t *off;       // [L] start of each level's lnx region (packed: base[l] - base[0])
 };
 
-// level of level position p (lptr[l] <= p < lptr[l + 1])
-DEVI uint32_t ov_level_of_pos(const uint32_t *lptr, uint32_t L, uint32_t p)
+// pos[l * n + row] = position of the row in level l; base[L+1] = first entry of every level
+// (packed layout: one thread per entry)
+__global__ void k_ov_lord_pos(const uint2 *ent, const uint64_t *base, uint32_t L, uint32_t n, uint32_t *pos)
 {
-	uint32_t lo = 0, hi = L;
+	const uint64_t g = base[0] + (uint64_t)blockIdx.x * 256u + threadIdx.x;
+	if (g >= base[L]) return;
+	const uint32_t l = ov_level_of(base, L, g);
+	pos[(size_t)l * n + (ent[g].x & ROW_MASK)] = (uint32_t)(g - base[l]);
+}
+
+// lnx[g - base[0]] = the entry's row position in the next level (the last level -> level 0)
+__global__ void k_ov_lord_next(const uint2 *ent, const uint64_t *base, uint32_t L, uint32_t n, const uint32_t *pos,
+                               uint32_t *lnx)
+{
+	const uint64_t g = base[0] + (uint64_t)blockIdx.x * 256u + threadIdx.x;
+	if (g >= base[L]) return;
+	const uint32_t l = ov_level_of(base, L, g), ln = l + 1 == L ? 0 : l + 1;
+	lnx[g - base[0]] = pos[(size_t)ln * n + (ent[g].x & ROW_MASK)];
+}
+
+// the padded layout: one workgroup per workgroup run (level l, group w; gbase[l] = the groups of
+// the levels before l), its entries [gs, ge) coalesced; level 0 packed (position g - gp[0]),
+// levels >= 1 at w * cap + (g - gs). NEXT: lnx[off[l] + position] = the row's position in the next
+// level (the last level -> level 0); else pos[l * n + row] = position.
+template <bool NEXT>
+__global__ __launch_bounds__(256) void k_ov_pad_pos(const uint2 *ent, OvPad pd, const uint32_t *gbase, uint32_t L,
+                                                    uint32_t n, uint32_t *pos, uint32_t *lnx)
+{
+	uint32_t lo = 0, hi = L;   // the level of this group: gbase[lo] <= blockIdx.x < gbase[lo + 1]
 	while (hi - lo > 1) {
 		const uint32_t mid = (lo + hi) >> 1;
-		if (lptr[mid] <= p) lo = mid;
+		if (gbase[mid] <= blockIdx.x) lo = mid;
 		else hi = mid;
 	}
-	return lo;
-}
-
-// one thread per column (level position p) of the batch: its entries g in [gp[p], gp[p+1]) sit at
-// position g - first in the level's buffer, first = the level's first entry (packed) or, padded
-// (levels >= 1), first = the start of the workgroup run that holds column p minus its slot w * cap
-DEVI uint64_t ov_col_first(const OvPad &pd, const uint64_t *base, uint32_t l, uint32_t p)
-{
-	if (pd.cap == 0 || l == 0) return base[l];
-	const uint32_t w = (p - pd.lptr[l]) / pd.cpw[l];
-	return pd.gp[pd.lptr[l] + w * pd.cpw[l]] - (uint64_t)w * pd.cap;
-}
-
-// pos[l * n + row] = position of the row in level l
-__global__ void k_ov_lord_pos(const uint2 *ent, const uint64_t *base, uint32_t L, uint32_t nf, uint32_t n, uint32_t *pos,
-                              OvPad pd)
-{
-	const uint32_t p = blockIdx.x * 256u + threadIdx.x;
-	if (p >= nf) return;
-	const uint32_t l = ov_level_of_pos(pd.lptr, L, p);
-	const uint64_t first = ov_col_first(pd, base, l, p);
-	for (uint64_t g = pd.gp[p]; g < pd.gp[p + 1]; ++g) pos[(size_t)l * n + (ent[g].x & ROW_MASK)] = (uint32_t)(g - first);
-}
-
-// lnx[off[l] + the entry's position] = the entry's row position in the next level (the last level
-// -> level 0)
-__global__ void k_ov_lord_next(const uint2 *ent, const uint64_t *base, uint32_t L, uint32_t nf, uint32_t n,
-                               const uint32_t *pos, uint32_t *lnx, OvPad pd)
-{
-	const uint32_t p = blockIdx.x * 256u + threadIdx.x;
-	if (p >= nf) return;
-	const uint32_t l = ov_level_of_pos(pd.lptr, L, p), ln = l + 1 == L ? 0 : l + 1;
-	const uint64_t first = ov_col_first(pd, base, l, p);
-	uint32_t *dst = lnx + pd.off[l];
-	for (uint64_t g = pd.gp[p]; g < pd.gp[p + 1]; ++g)
-		dst[g - first] = pos[(size_t)ln * n + (ent[g].x & ROW_MASK)];
+	const uint32_t l = lo, w = blockIdx.x - gbase[l];
+	const uint32_t p0 = pd.lptr[l] + w * pd.cpw[l], p1 = min(p0 + pd.cpw[l], pd.lptr[l + 1]);
+	const uint64_t gs = pd.gp[p0], ge = pd.gp[p1];
+	const uint64_t first = l == 0 ? pd.gp[0] : gs - (uint64_t)w * pd.cap;
+	const uint32_t ln = l + 1 == L ? 0 : l + 1;
+	for (uint64_t g = gs + threadIdx.x; g < ge; g += 256) {
+		const uint32_t row = ent[g].x & ROW_MASK, at = (uint32_t)(g - first);
+		if constexpr (NEXT) lnx[pd.off[l] + at] = pos[(size_t)ln * n + row];
+		else pos[(size_t)l * n + row] = at;
+	}
 }
 
 // per batch: does some workgroup run of a level >= 1 exceed PAD_CAP records? (thread per
@@ -825,7 +824,8 @@ struct OvState {
 	// slot count, the padded levels' lnx prefix (batch-independent), the batches it applies to
 	uint32_t *cpw_d = nullptr, *pad_bad_d = nullptr;
 	uint64_t *lnx_off_d = nullptr;     // [L] lnx region of each level for the current batch
-	std::vector<uint32_t> cpw_h, ngroups_h;
+	std::vector<uint32_t> cpw_h, ngroups_h, gbase_h;   // gbase: groups of the levels before l [L + 1]
+	uint32_t *gbase_d = nullptr;
 	std::vector<uint64_t> pad_prefix;  // [L + 1] sum over levels 1..l-1 of ngroups * cap
 	std::vector<uint8_t> batch_pad;    // [num_batch]
 	uint64_t pad_rows = 0;             // records a padded level's buffer needs (max over levels)
@@ -855,7 +855,7 @@ void ov_free(vbfm_ctx *c)
 	dfree(o.gptr); dfree(o.lvcp); dfree(o.rstart_d); dfree(o.tmp); dfree(o.rp_b); dfree(o.len_b); dfree(o.csr_b); dfree(o.t_b);
 	dfree(o.rows_b);
 	dfree(o.level_ptr_d); dfree(o.lvl_d); dfree(o.lpos); dfree(o.lnx); dfree(o.rows_b2);
-	dfree(o.cpw_d); dfree(o.pad_bad_d); dfree(o.lnx_off_d);
+	dfree(o.cpw_d); dfree(o.pad_bad_d); dfree(o.lnx_off_d); dfree(o.gbase_d);
 	for (hipEvent_t e : o.ev)
 		if (e) (void)hipEventDestroy(e);
 	for (hipEvent_t e : o.bev) (void)hipEventDestroy(e);
@@ -1053,10 +1053,16 @@ void ov_lord_begin(vbfm_ctx *c, uint32_t b, uint32_t n, uint64_t nnz)
 		sync(c);   // (off is a host temporary)
 		if (pad) pd.cap = vbk::ov_pad_cap();
 	}
-	const uint32_t nf = c->tr.nf;
-	k_ov_lord_pos<<<grid_of(nf), 256, 0, c->s>>>(o.ent_sorted, base, L, nf, n, o.lpos, pd);
-	HIPCHK(hipGetLastError());
-	k_ov_lord_next<<<grid_of(nf), 256, 0, c->s>>>(o.ent_sorted, base, L, nf, n, o.lpos, o.lnx, pd);
+	if (pad) {
+		const uint32_t groups = o.gbase_h[L];
+		k_ov_pad_pos<false><<<groups, 256, 0, c->s>>>(o.ent_sorted, pd, o.gbase_d, L, n, o.lpos, o.lnx);
+		HIPCHK(hipGetLastError());
+		k_ov_pad_pos<true><<<groups, 256, 0, c->s>>>(o.ent_sorted, pd, o.gbase_d, L, n, o.lpos, o.lnx);
+	} else {
+		k_ov_lord_pos<<<grid_of(nnz), 256, 0, c->s>>>(o.ent_sorted, base, L, n, o.lpos);
+		HIPCHK(hipGetLastError());
+		k_ov_lord_next<<<grid_of(nnz), 256, 0, c->s>>>(o.ent_sorted, base, L, n, o.lpos, o.lnx);
+	}
 	HIPCHK(hipGetLastError());
 	o.pad_on = pad;
 	o.cur_n = n;
@@ -1271,8 +1277,12 @@ int vbfm_online_init(vbfm_ctx *c, const vbfm_online_config *cfg)
 							o.pad_prefix[l + 1] = o.pad_prefix[l] + (uint64_t)o.ngroups_h[l] * cap;
 							o.pad_rows = std::max<uint64_t>(o.pad_rows, (uint64_t)o.ngroups_h[l] * cap);
 						}
+						o.gbase_h.assign((size_t)L + 1, 0);
+						for (uint32_t l = 0; l < L; l++) o.gbase_h[l + 1] = o.gbase_h[l] + o.ngroups_h[l];
 						o.cpw_d = dalloc<uint32_t>(L);
 						HIPCHK(hipMemcpy(o.cpw_d, o.cpw_h.data(), (size_t)L * 4, hipMemcpyHostToDevice));
+						o.gbase_d = dalloc<uint32_t>((size_t)L + 1);
+						HIPCHK(hipMemcpy(o.gbase_d, o.gbase_h.data(), ((size_t)L + 1) * 4, hipMemcpyHostToDevice));
 						o.pad_bad_d = dalloc<uint32_t>(nb);
 					}
 					o.lnx_off_d = dalloc<uint64_t>(L);
