@@ -5,6 +5,7 @@
 #   smoke                      __graft_entry__.smoke()
 #   bench[=<args>]             python bench.py <args> > bench.json (args: '+' separates words)
 #   prof[=<args>]              rocprofv3 --kernel-trace --stats of bench.py <args>
+#   profstat[=<args>]          prof, keeping only the --stats summary
 #   pmc[=<args>]               FETCH_SIZE then WRITE_SIZE, one --pmc pass each, of bench.py <args>
 #   py=<script>[+args]         python -u <script> <args>
 #   exe=<binary>[+args]        a built probe binary
@@ -37,6 +38,11 @@ for step in "$@"; do
     prof)
       timeout -k 10 900 rocprofv3 --kernel-trace --stats -d "$O/prof_$n" -o kt --output-format csv -- \
         python3 bench.py $args > "$O/prof_$n.json" 2> "$O/prof_$n.txt" ;;
+    profstat)
+      # as prof, keeping only the summary (the per-dispatch trace of a many-launch run is large)
+      timeout -k 10 900 rocprofv3 --kernel-trace --stats -d "$O/profstat_$n" -o kt --output-format csv -- \
+        python3 bench.py $args > "$O/profstat_$n.json" 2> "$O/profstat_$n.txt"
+      rc0=$?; rm -f "$O/profstat_$n/kt_kernel_trace.csv"; (exit $rc0) ;;
     pmc)
       for c in FETCH_SIZE WRITE_SIZE; do
         timeout -k 10 600 rocprofv3 --pmc $c --kernel-trace -d "$O/pmc_${n}_$c" -o p --output-format csv -- \
