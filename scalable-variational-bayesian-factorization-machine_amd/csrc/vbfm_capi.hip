@@ -303,6 +303,74 @@ bool build_estore(vbfm_ctx *c, const std::vector<uint64_t> &lcp, const std::vect
 	return true;
 }
 
+// Placement of the store's two record buffers (VBFM_PLACE, default 1). The level kernel's
+// scattered whole-record writes run up to ~20 % faster or slower depending on where the driver
+// placed the two buffers, persistently per allocation, while streaming copies do not change
+// (tools/probe_place.hip, profiles/r04_short_columns/). So the current pair and up to
+// VBFM_PLACE_TRIES - 1 freshly allocated pairs are timed on level 0's real pattern in both
+// directions (k_place_move, no arithmetic) and the fastest pair is kept; the records move with it.
+// Only where a launch is long enough to time (>= 2e6 rows) and the candidates fit in half of the
+// free memory. The results do not depend on the buffers (bit for bit).
+static void tune_placement(vbfm_ctx *c)
+{
+	const uint32_t n = c->tr.n, L = nlevels(c);
+	const char *pe = getenv("VBFM_PLACE");
+	if ((pe && pe[0] == '0') || n < 2000000u || L < 2 || !c->lnext) return;
+	const char *te = getenv("VBFM_PLACE_TRIES");
+	const int tries = te ? std::max(1, atoi(te)) : 4;
+	const size_t bytes = (size_t)n * sizeof(RowRec);
+	size_t fr = 0, tot = 0;
+	HIPCHK(hipMemGetInfo(&fr, &tot));
+	const int extra = (int)std::min<size_t>((size_t)tries - 1, fr / 2 / (2 * bytes + 1));
+	if (extra < 1) return;
+	const uint64_t *lp = c->lcp + c->level_ptr[0];
+	const uint32_t nfl = c->level_ptr[1] - c->level_ptr[0];
+	hipEvent_t e0, e1;
+	HIPCHK(hipEventCreate(&e0));
+	HIPCHK(hipEventCreate(&e1));
+	auto time_pair = [&](RowRec *a, RowRec *b) {
+		HIPCHK(vbk::place_move(a, b, lp, c->lnext, nfl, c->s));   // warm-up
+		HIPCHK(hipEventRecord(e0, c->s));
+		for (int r = 0; r < 2; r++) {
+			HIPCHK(vbk::place_move(a, b, lp, c->lnext, nfl, c->s));
+			HIPCHK(vbk::place_move(b, a, lp, c->lnext, nfl, c->s));
+		}
+		HIPCHK(hipEventRecord(e1, c->s));
+		HIPCHK(hipEventSynchronize(e1));
+		float ms = 0.f;
+		HIPCHK(hipEventElapsedTime(&ms, e0, e1));
+		return ms;
+	};
+	// the records (if any) wait in a spare buffer while every pair is overwritten
+	RowRec *keep = dalloc<RowRec>(n);
+	HIPCHK(hipMemcpyAsync(keep, c->rows, bytes, hipMemcpyDeviceToDevice, c->s));
+	std::vector<std::pair<RowRec *, RowRec *>> pairs = {{c->rows, c->rows_alt}};
+	for (int i = 0; i < extra; i++) pairs.push_back({dalloc<RowRec>(n), dalloc<RowRec>(n)});
+	std::vector<float> ms(pairs.size());
+	size_t best = 0;
+	for (size_t i = 0; i < pairs.size(); i++) {
+		ms[i] = time_pair(pairs[i].first, pairs[i].second);
+		if (ms[i] < ms[best]) best = i;
+	}
+	for (size_t i = 0; i < pairs.size(); i++)
+		if (i != best) { dfree(pairs[i].first); dfree(pairs[i].second); }
+	c->rows = pairs[best].first;
+	c->rows_alt = pairs[best].second;
+	HIPCHK(hipMemcpyAsync(c->rows, keep, bytes, hipMemcpyDeviceToDevice, c->s));
+	sync(c);
+	dfree(keep);
+	(void)hipEventDestroy(e0);
+	(void)hipEventDestroy(e1);
+	c->place_ms.assign(ms.begin(), ms.end());
+	c->place_pick = (int)best;
+	const char *lg = getenv("VBFM_PLACE_LOG");
+	if (lg && lg[0] == '1') {
+		fprintf(stderr, "vbfm placement: %u rows, level-0 pattern x4 per pair:", n);
+		for (size_t i = 0; i < ms.size(); i++) fprintf(stderr, " %.3f%s", ms[i], i == best ? "*" : "");
+		fprintf(stderr, " ms\n");
+	}
+}
+
 // Level-ordered store of the train set when every level holds each row exactly once (no
 // repeated feature in a row): per level l, positions [l*n, (l+1)*n) list the level's
 // columns in ascending feature order, rows ascending within a column.
@@ -380,6 +448,7 @@ void build_lorder(vbfm_ctx *c, const std::vector<uint64_t> &cp, const std::vecto
 		                      l == 0 ? c->lrow0 : nullptr, c->s));
 		if (l > 0) HIPCHK(vbk::lord_pos(f, nfl, lp, (uint64_t)l * n, d.col_ptr, d.csc, tmp, c->s));
 	}
+	tune_placement(c);
 	// split form (row shards): each entry's previous-level feature and x, for the deferred
 	// correction (VBFM_DEFER=0 keeps the two-pass split)
 	const char *df = getenv("VBFM_DEFER");

@@ -245,6 +245,10 @@ hipError_t estore_build(const uint64_t *row_ptr, const uint2 *csr, const uint64_
 hipError_t estore_prev(const uint64_t *row_ptr, const uint2 *csr, const uint64_t *col_ptr, const uint2 *csc,
                        const uint32_t *lvpos, const uint64_t *lcp, uint32_t n, uint32_t *lpidx, float *lpx, hipStream_t s);
 hipError_t rows_scatter(RowRec *dst, const RowRec *src, const uint32_t *idx, uint32_t n, hipStream_t s);
+// the level pattern without arithmetic: level 0's runs (lcp, nfeat columns) moved whole to their
+// level-1 slots (lnext), src -> dst (placement probe of a record-buffer pair)
+hipError_t place_move(const RowRec *src, RowRec *dst, const uint64_t *lcp, const uint32_t *lnext, uint32_t nfeat,
+                      hipStream_t s);
 hipError_t mark_first(const uint64_t *row_ptr, const uint2 *csr, const uint64_t *col_ptr, uint2 *csc,
                       uint32_t n, hipStream_t s);
 // blocked = 0: the reference's summation order (bit-exact); 1: factors in blocks of 8

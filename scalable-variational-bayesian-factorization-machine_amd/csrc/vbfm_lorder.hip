@@ -702,6 +702,41 @@ __global__ __launch_bounds__(BLOCK) void k_mc_level_lord(McArgs a)
 	}
 }
 
+// ---- placement probe ---------------------------------------------------------------------
+// The level kernel's memory pattern without its arithmetic: level 0's runs (one workgroup per
+// column, LDS-staged in chunks of 512 records) moved whole to their slots of level 1 (lnext).
+// Used to time a pair of record buffers before the store adopts it: the scattered-write rate of
+// the pattern depends on where the buffers were placed by up to ~20 %, persistently per
+// allocation (tools/probe_place.hip); the copy rate does not.
+__global__ __launch_bounds__(256) void k_place_move(const RowRec *src, RowRec *dst, const uint64_t *lcp,
+                                                    const uint32_t *lnext)
+{
+	constexpr uint32_t CAP = 512;
+	__shared__ double2 recs[CAP * 4];
+	__shared__ uint32_t dsts[CAP];
+	const uint64_t sb = lcp[blockIdx.x];
+	const uint32_t n = (uint32_t)(lcp[blockIdx.x + 1] - sb);
+	const double2 *s = reinterpret_cast<const double2 *>(src + sb);
+	double2 *d = reinterpret_cast<double2 *>(dst);
+	for (uint32_t base = 0; base < n; base += CAP) {
+		const uint32_t m = min(CAP, n - base);
+		if (base) __syncthreads();
+		double2 v[8];
+		uint32_t nr[2];
+#pragma unroll
+		for (int u = 0; u < 2; ++u) nr[u] = lnext[sb + base + min(threadIdx.x + u * 256, m - 1)];
+		stage_load<256, 2, false>(v, s + (size_t)base * 4, m);
+		stage_store<256, 2>(recs, v);
+#pragma unroll
+		for (int u = 0; u < 2; ++u) dsts[threadIdx.x + u * 256] = nr[u];
+		__syncthreads();
+		for (uint32_t t = threadIdx.x; t < m * 4; t += 256) {
+			const uint32_t i = t >> 2, c = t & 3;
+			d[(size_t)dsts[i] * 4 + c] = recs[lslot(i, c)];
+		}
+	}
+}
+
 // ---- build -------------------------------------------------------------------------------
 __global__ void k_lord_pack(const float *lx, const uint32_t *lnext, const uint32_t *lpidx, const float *lpx, uint4 *lpay,
                             uint64_t nnz)
@@ -1646,6 +1681,14 @@ hipError_t estore_prev(const uint64_t *row_ptr, const uint2 *csr, const uint64_t
 {
 	if (n == 0) return hipSuccess;
 	k_estore_prev<<<(n + 255) / 256, 256, 0, s>>>(row_ptr, csr, col_ptr, csc, lvpos, lcp, n, lpidx, lpx);
+	return hipGetLastError();
+}
+
+hipError_t place_move(const RowRec *src, RowRec *dst, const uint64_t *lcp, const uint32_t *lnext, uint32_t nfeat,
+                      hipStream_t s)
+{
+	if (nfeat == 0) return hipSuccess;
+	k_place_move<<<nfeat, 256, 0, s>>>(src, dst, lcp, lnext);
 	return hipGetLastError();
 }
 
