@@ -488,6 +488,7 @@ def main():
         return st.rmse_all if mc else st.rmse
 
     n_ranks_seen, _, transport = fml.comm_info()
+    place_ms, place_kept = fml.placement()
     rccl_libs = loaded_libs("librccl")
     if len(rccl_libs) > 1:
         raise SystemExit("more than one RCCL loaded: %s" % rccl_libs)
@@ -621,6 +622,9 @@ def main():
                      "kernel": kernel, "avg_launch_ms": avg_ms,
                      "launches": n_launch, "bytes_per_launch": bytes_per_launch},
         "roofline_with_fused_predict": fused_model,
+        # the level store's record buffers: probe time of each candidate pair (level 0's pattern,
+        # 4 passes), the first allocated first, and the pair kept (VBFM_PLACE)
+        "placement": {"pair_ms": [round(x, 4) for x in place_ms], "kept": place_kept} if place_ms else None,
         "factor_sweep_ms_per_step": sweep_ms,
         "factor_sweep_nnz_k_per_s": nnz_total * k / (sweep_ms * 1e-3),
         "test_rmse": rmse_of(stats[-1]),

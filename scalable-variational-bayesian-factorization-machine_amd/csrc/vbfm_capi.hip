@@ -317,7 +317,7 @@ static void tune_placement(vbfm_ctx *c)
 	const char *pe = getenv("VBFM_PLACE");
 	if ((pe && pe[0] == '0') || n < 2000000u || L < 2 || !c->lnext) return;
 	const char *te = getenv("VBFM_PLACE_TRIES");
-	const int tries = te ? std::max(1, atoi(te)) : 4;
+	const int tries = te ? std::max(1, atoi(te)) : 5;
 	const size_t bytes = (size_t)n * sizeof(RowRec);
 	size_t fr = 0, tot = 0;
 	HIPCHK(hipMemGetInfo(&fr, &tot));
@@ -344,8 +344,20 @@ static void tune_placement(vbfm_ctx *c)
 	// the records (if any) wait in a spare buffer while every pair is overwritten
 	RowRec *keep = dalloc<RowRec>(n);
 	HIPCHK(hipMemcpyAsync(keep, c->rows, bytes, hipMemcpyDeviceToDevice, c->s));
+	// candidates: plain allocations, and (every other one) physically contiguous ones
+	// (hipDeviceMallocContiguous) when the driver grants them
+	auto alloc_one = [&](bool contig) -> RowRec * {
+		void *q = nullptr;
+		if (contig && hipExtMallocWithFlags(&q, bytes, hipDeviceMallocContiguous) == hipSuccess) return (RowRec *)q;
+		(void)hipGetLastError();
+		return dalloc<RowRec>(n);
+	};
 	std::vector<std::pair<RowRec *, RowRec *>> pairs = {{c->rows, c->rows_alt}};
-	for (int i = 0; i < extra; i++) pairs.push_back({dalloc<RowRec>(n), dalloc<RowRec>(n)});
+	for (int i = 0; i < extra; i++) {
+		const bool contig = (i & 1) != 0;
+		RowRec *a = alloc_one(contig);
+		pairs.push_back({a, alloc_one(contig)});
+	}
 	std::vector<float> ms(pairs.size());
 	size_t best = 0;
 	for (size_t i = 0; i < pairs.size(); i++) {
@@ -2175,6 +2187,17 @@ int vbfm_comm_init(vbfm_ctx *c, int32_t nranks, int32_t rank, const uint8_t uid[
 		NCCLCHK(ncclCommInitRank(&c->comm, nranks, id, rank));
 		c->nranks = nranks;
 		c->rank = rank;
+	});
+}
+
+int vbfm_placement_info(vbfm_ctx *c, float *ms, int32_t *count, int32_t *kept)
+{
+	if (!c || !count || !kept) return fail(c, "null argument");
+	return guarded(c, [&] {
+		const int32_t cap = *count;
+		*count = (int32_t)c->place_ms.size();
+		*kept = c->place_pick;
+		for (int32_t i = 0; ms && i < std::min(cap, *count); i++) ms[i] = c->place_ms[(size_t)i];
 	});
 }
 

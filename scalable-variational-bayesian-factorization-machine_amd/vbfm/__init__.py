@@ -149,7 +149,7 @@ EXPORTS = ["vbfm_abi_version", "vbfm_last_error", "vbfm_create", "vbfm_destroy",
            "vbfm_step_v_level", "vbfm_step_hyper", "vbfm_device_count",
            "vbfm_free_energy", "vbfm_get_rows", "vbfm_get_test_e", "vbfm_factor_sweep", "vbfm_set_profiling",
            "vbfm_set_layout", "vbfm_get_layout", "vbfm_set_shard_mode",
-           "vbfm_comm_unique_id", "vbfm_comm_init", "vbfm_comm_init_host", "vbfm_comm_info", "vbfm_load_data", "vbfm_free_host_data", "vbfm_save_data",
+           "vbfm_comm_unique_id", "vbfm_comm_init", "vbfm_comm_init_host", "vbfm_comm_info", "vbfm_placement_info", "vbfm_load_data", "vbfm_free_host_data", "vbfm_save_data",
            "vbfm_init_params_host", "vbfm_mcmc_init", "vbfm_mcmc_set_params", "vbfm_mcmc_get_params",
            "vbfm_mcmc_init_caches", "vbfm_mcmc_iterate", "vbfm_mcmc_get_test_pred", "vbfm_mcmc_factor_sweep",
            "vbfm_online_init", "vbfm_online_epoch", "vbfm_online_get_state", "vbfm_save_state", "vbfm_load_state"]
@@ -213,6 +213,7 @@ def lib():
         L.vbfm_comm_init.argtypes = [V, C.c_int32, C.c_int32, C.POINTER(C.c_uint8)]
         L.vbfm_comm_init_host.argtypes = [V, C.c_int32, C.c_int32, EXCHANGE_FN, V]
         L.vbfm_comm_info.argtypes = [V, C.POINTER(C.c_int32), C.POINTER(C.c_int32), C.POINTER(C.c_int32)]
+        L.vbfm_placement_info.argtypes = [V, C.POINTER(C.c_float), C.POINTER(C.c_int32), C.POINTER(C.c_int32)]
         L.vbfm_load_data.argtypes = [C.c_char_p, C.POINTER(HostData)]
         L.vbfm_free_host_data.argtypes = [C.POINTER(HostData)]
         L.vbfm_save_data.argtypes = [C.c_char_p, C.POINTER(HostData)]
@@ -597,6 +598,14 @@ class FMLearnVB:
         n, r, t = C.c_int32(), C.c_int32(), C.c_int32()
         _check(lib().vbfm_comm_info(self._ctx, C.byref(n), C.byref(r), C.byref(t)), self._ctx)
         return n.value, r.value, {0: "none", 1: "rccl", 2: "host"}[t.value]
+
+    def placement(self):
+        """(probe ms of each candidate record-buffer pair, index kept) of the level store's
+        placement tuning (vbfm_placement_info); ([], -1) when none ran."""
+        buf = (C.c_float * 32)()
+        n, k = C.c_int32(32), C.c_int32()
+        _check(lib().vbfm_placement_info(self._ctx, buf, C.byref(n), C.byref(k)), self._ctx)
+        return [float(buf[i]) for i in range(min(n.value, 32))], k.value
 
     def close(self):
         if self._ctx:
