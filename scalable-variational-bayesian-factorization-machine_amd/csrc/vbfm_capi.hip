@@ -344,19 +344,12 @@ static void tune_placement(vbfm_ctx *c)
 	// the records (if any) wait in a spare buffer while every pair is overwritten
 	RowRec *keep = dalloc<RowRec>(n);
 	HIPCHK(hipMemcpyAsync(keep, c->rows, bytes, hipMemcpyDeviceToDevice, c->s));
-	// candidates: plain allocations, and (every other one) physically contiguous ones
-	// (hipDeviceMallocContiguous) when the driver grants them
-	auto alloc_one = [&](bool contig) -> RowRec * {
-		void *q = nullptr;
-		if (contig && hipExtMallocWithFlags(&q, bytes, hipDeviceMallocContiguous) == hipSuccess) return (RowRec *)q;
-		(void)hipGetLastError();
-		return dalloc<RowRec>(n);
-	};
+	// candidates: plain allocations (physically contiguous ones, hipDeviceMallocContiguous, probed
+	// 14.1 ms against 11.5-11.8 ms for plain ones at C4 and no better at C3: not tried)
 	std::vector<std::pair<RowRec *, RowRec *>> pairs = {{c->rows, c->rows_alt}};
 	for (int i = 0; i < extra; i++) {
-		const bool contig = (i & 1) != 0;
-		RowRec *a = alloc_one(contig);
-		pairs.push_back({a, alloc_one(contig)});
+		RowRec *a = dalloc<RowRec>(n);
+		pairs.push_back({a, dalloc<RowRec>(n)});
 	}
 	std::vector<float> ms(pairs.size());
 	size_t best = 0;
