@@ -346,10 +346,18 @@ static void tune_placement(vbfm_ctx *c)
 	HIPCHK(hipMemcpyAsync(keep, c->rows, bytes, hipMemcpyDeviceToDevice, c->s));
 	// candidates: plain allocations (physically contiguous ones, hipDeviceMallocContiguous, probed
 	// 14.1 ms against 11.5-11.8 ms for plain ones at C4 and no better at C3: not tried)
+	// every other candidate of a store under 2 GB is allocated 4 GB large (its first n records used;
+	// the pointer stays the allocation's base): another part of the address space
+	auto alloc_one = [&](bool big) -> RowRec * {
+		void *q = nullptr;
+		HIPCHK(hipMalloc(&q, big ? std::max<size_t>(bytes, (size_t)4 << 30) : bytes));
+		return (RowRec *)q;
+	};
 	std::vector<std::pair<RowRec *, RowRec *>> pairs = {{c->rows, c->rows_alt}};
 	for (int i = 0; i < extra; i++) {
-		RowRec *a = dalloc<RowRec>(n);
-		pairs.push_back({a, dalloc<RowRec>(n)});
+		const bool big = (i & 1) != 0 && bytes < ((size_t)2 << 30) && fr / 2 > (size_t)(extra + 1) * (8ull << 30);
+		RowRec *a = alloc_one(big);
+		pairs.push_back({a, alloc_one(big)});
 	}
 	std::vector<float> ms(pairs.size());
 	size_t best = 0;
