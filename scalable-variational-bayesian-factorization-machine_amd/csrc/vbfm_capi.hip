@@ -317,7 +317,7 @@ static void tune_placement(vbfm_ctx *c)
 	const char *pe = getenv("VBFM_PLACE");
 	if ((pe && pe[0] == '0') || n < 2000000u || L < 2 || !c->lnext) return;
 	const char *te = getenv("VBFM_PLACE_TRIES");
-	const int tries = te ? std::max(1, atoi(te)) : 5;
+	const int tries = te ? std::max(1, atoi(te)) : 8;
 	const size_t bytes = (size_t)n * sizeof(RowRec);
 	size_t fr = 0, tot = 0;
 	HIPCHK(hipMemGetInfo(&fr, &tot));

@@ -60,10 +60,43 @@ static float time_pair(dv2 *a, dv2 *b, const uint32_t *np, uint32_t n, hipEvent_
 	return ms / 6 * 1e9f / n;   // ps per record
 }
 
+// mode 1 (argv[3] = 1): allocation strategies instead of plain pairs -- plain, one allocation of
+// 2n records split in two, a 4x oversized allocation used from its middle, hipMallocAsync from the
+// default pool, and plain after a 100 GB allocation was made and freed
+static int strategies(uint32_t n, const uint32_t *np, hipEvent_t e0, hipEvent_t e1)
+{
+	const size_t B = (size_t)n * 64;
+	const char *names[] = {"plain", "plain", "one 2n block", "4x block, middle", "hipMallocAsync", "plain after 100 GB"};
+	for (int sidx = 0; sidx < 6; ++sidx) {
+		void *pa = nullptr, *pb = nullptr;
+		dv2 *a = nullptr, *b = nullptr;
+		if (sidx <= 1) { CK(hipMalloc(&pa, B)); CK(hipMalloc(&pb, B)); a = (dv2 *)pa; b = (dv2 *)pb; }
+		else if (sidx == 2) { CK(hipMalloc(&pa, 2 * B)); a = (dv2 *)pa; b = (dv2 *)((char *)pa + B); }
+		else if (sidx == 3) { CK(hipMalloc(&pa, 4 * B)); a = (dv2 *)((char *)pa + B); b = (dv2 *)((char *)pa + 2 * B); }
+		else if (sidx == 4) { CK(hipMallocAsync(&pa, B, 0)); CK(hipMallocAsync(&pb, B, 0)); CK(hipDeviceSynchronize()); a = (dv2 *)pa; b = (dv2 *)pb; }
+		else {
+			void *big = nullptr;
+			CK(hipMalloc(&big, (size_t)100 << 30));
+			CK(hipMemset(big, 0, (size_t)1 << 30));
+			CK(hipFree(big));
+			CK(hipMalloc(&pa, B)); CK(hipMalloc(&pb, B)); a = (dv2 *)pa; b = (dv2 *)pb;
+		}
+		CK(hipMemset(a, 0, B));
+		CK(hipMemset(b, 0, B));
+		const float t1 = time_pair(a, b, np, n, e0, e1), t2 = time_pair(a, b, np, n, e0, e1);
+		printf("%-20s a=%p b=%p  %.2f %.2f ps/rec\n", names[sidx], (void *)a, (void *)b, t1, t2);
+		fflush(stdout);
+		if (sidx == 4) { CK(hipFreeAsync(pa, 0)); CK(hipFreeAsync(pb, 0)); CK(hipDeviceSynchronize()); }
+		else { CK(hipFree(pa)); if (pb) CK(hipFree(pb)); }
+	}
+	return 0;
+}
+
 int main(int argc, char **argv)
 {
 	const uint32_t n = argc > 1 ? (uint32_t)atol(argv[1]) : 10000000u;
 	const int pairs = argc > 2 ? atoi(argv[2]) : 6;
+	const int mode = argc > 3 ? atoi(argv[3]) : 0;
 	std::vector<uint32_t> hp(n);
 	for (uint32_t i = 0; i < n; i++) hp[i] = i;
 	std::mt19937_64 g(7);
@@ -74,6 +107,7 @@ int main(int argc, char **argv)
 	hipEvent_t e0, e1;
 	CK(hipEventCreate(&e0));
 	CK(hipEventCreate(&e1));
+	if (mode == 1) return strategies(n, np, e0, e1);
 	std::vector<dv2 *> A(pairs), B(pairs);
 	std::vector<float> t1(pairs), t2(pairs), t3(pairs);
 	for (int p = 0; p < pairs; ++p) {
