@@ -605,7 +605,8 @@ def main():
         "data": "synthetic field-structured one-hot libfm data generated in HBM (tests/synth.py spec: "
                 "planted bias + rank-2 interaction shared by train, test and all shards), "
                 "device random init of mu (0.1*N(0,1))",
-        "config": {"workload": cfg["desc"], "rows_total": n_total, "rows_per_gpu": N, "fields": F,
+        "config": {"workload": cfg["desc"].replace("-method vb", "-method " + args.method),
+                   "rows_total": n_total, "rows_per_gpu": N, "fields": F,
                    "ids_per_field": S, "features": NF, "k": k, "nnz_total": nnz_total, "nnz_per_gpu": nnz,
                    "test_rows_per_gpu": n_test,
                    "levels": levels, "method": args.method,
