@@ -625,7 +625,7 @@ def main():
         "roofline_with_fused_predict": fused_model,
         # the level store's record buffers: probe time of each candidate pair (level 0's pattern,
         # 4 passes), the first allocated first, and the pair kept (VBFM_PLACE)
-        "placement": {"pair_ms": [round(x, 4) for x in place_ms], "kept": place_kept} if place_ms else None,
+        "placement": {"buffer_ms": [round(x, 4) for x in place_ms], "kept": place_kept} if place_ms else None,
         "factor_sweep_ms_per_step": sweep_ms,
         "factor_sweep_nnz_k_per_s": nnz_total * k / (sweep_ms * 1e-3),
         "test_rmse": rmse_of(stats[-1]),

@@ -253,9 +253,10 @@ int vbfm_comm_init_host(vbfm_ctx *ctx, int32_t nranks, int32_t rank, vbfm_exchan
 /* The communicator as RCCL reports it (ncclCommCount / ncclCommUserRank): transport 0 = none
  * (one rank), 1 = RCCL, 2 = host exchange (nranks / rank as given to vbfm_comm_init_host). */
 int vbfm_comm_info(vbfm_ctx *ctx, int32_t *nranks, int32_t *rank, int32_t *transport);
-/* The level store's record-buffer placement (VBFM_PLACE): the probe time (ms) of each candidate
- * pair of record buffers, the first being the pair allocated first, and the index of the pair
- * kept. *count = 0 when no placement was tuned. ms holds up to *count on entry (in: capacity). */
+/* The level store's record-buffer placement (VBFM_PLACE): the score (ms, level 0's pattern to and
+ * from a reference buffer) of each candidate record buffer, [0] and [1] being the pair allocated
+ * first, and in kept[0], kept[1] the indices of the two buffers kept (records, alternate).
+ * *count = 0 when no placement was tuned. ms holds up to *count on entry (in: capacity). */
 int vbfm_placement_info(vbfm_ctx *ctx, float *ms, int32_t *count, int32_t *kept);
 
 /* Partition of the VB sweep over ranks (set before vbfm_set_train).

@@ -306,34 +306,44 @@ bool build_estore(vbfm_ctx *c, const std::vector<uint64_t> &lcp, const std::vect
 // Placement of the store's two record buffers (VBFM_PLACE, default 1). The level kernel's
 // scattered whole-record writes run up to ~20 % faster or slower depending on where the driver
 // placed the two buffers, persistently per allocation, while streaming copies do not change
-// (tools/probe_place.hip, profiles/r04_short_columns/). So the current pair and up to
-// VBFM_PLACE_TRIES - 1 freshly allocated pairs are timed on level 0's real pattern in both
-// directions (k_place_move, no arithmetic) and the fastest pair is kept; the records move with it.
-// Only where a launch is long enough to time (>= 2e6 rows) and the candidates fit in half of the
-// free memory. The results do not depend on the buffers (bit for bit).
+// (tools/probe_place.hip, profiles/r04_short_columns/). A pair's time is close to the
+// sum of a per-buffer part for each side (a slow source with a fast destination lands in between),
+// so buffers are scored one at a time: the store's two buffers and up to VBFM_PLACE_TRIES - 2 fresh
+// allocations, each moved to and from one reference buffer on level 0's real pattern (k_place_move,
+// no arithmetic); the two best are kept (the records move with them), the rest freed. Only where a
+// launch is long enough to time (>= 2e6 rows) and the candidates fit in half of the free memory.
+// The results do not depend on the buffers (bit for bit).
 static void tune_placement(vbfm_ctx *c)
 {
 	const uint32_t n = c->tr.n, L = nlevels(c);
 	const char *pe = getenv("VBFM_PLACE");
 	if ((pe && pe[0] == '0') || n < 2000000u || L < 2 || !c->lnext) return;
 	const char *te = getenv("VBFM_PLACE_TRIES");
-	const int tries = te ? std::max(1, atoi(te)) : 8;
 	const size_t bytes = (size_t)n * sizeof(RowRec);
+	// stores under 2 GB (C3, one rank of N = 4 or 8) try 64 buffers, larger ones 16: the fast
+	// allocations come in clusters along the allocation sequence and a few tries miss them on some
+	// boxes (profiles/r04_short_columns/placement_tries/)
+	const int tries = te ? std::max(2, atoi(te)) : bytes < ((size_t)2 << 30) ? 64 : 16;
 	size_t fr = 0, tot = 0;
 	HIPCHK(hipMemGetInfo(&fr, &tot));
-	const int extra = (int)std::min<size_t>((size_t)tries - 1, fr / 2 / (2 * bytes + 1));
+	// the stash of the records and the reference buffer come out of the same half
+	const size_t room = fr / 2 > 2 * bytes ? fr / 2 - 2 * bytes : 0;
+	const int extra = (int)std::min<size_t>((size_t)tries - 2, room / (bytes + 1));
 	if (extra < 1) return;
 	const uint64_t *lp = c->lcp + c->level_ptr[0];
 	const uint32_t nfl = c->level_ptr[1] - c->level_ptr[0];
+	// the records wait in a stash while every candidate is overwritten
+	RowRec *keep = dalloc<RowRec>(n), *ref = dalloc<RowRec>(n);
+	HIPCHK(hipMemcpyAsync(keep, c->rows, bytes, hipMemcpyDeviceToDevice, c->s));
 	hipEvent_t e0, e1;
 	HIPCHK(hipEventCreate(&e0));
 	HIPCHK(hipEventCreate(&e1));
-	auto time_pair = [&](RowRec *a, RowRec *b) {
-		HIPCHK(vbk::place_move(a, b, lp, c->lnext, nfl, c->s));   // warm-up
+	auto score = [&](RowRec *x) {
+		HIPCHK(vbk::place_move(ref, x, lp, c->lnext, nfl, c->s));   // warm-up
 		HIPCHK(hipEventRecord(e0, c->s));
 		for (int r = 0; r < 2; r++) {
-			HIPCHK(vbk::place_move(a, b, lp, c->lnext, nfl, c->s));
-			HIPCHK(vbk::place_move(b, a, lp, c->lnext, nfl, c->s));
+			HIPCHK(vbk::place_move(ref, x, lp, c->lnext, nfl, c->s));
+			HIPCHK(vbk::place_move(x, ref, lp, c->lnext, nfl, c->s));
 		}
 		HIPCHK(hipEventRecord(e1, c->s));
 		HIPCHK(hipEventSynchronize(e1));
@@ -341,45 +351,32 @@ static void tune_placement(vbfm_ctx *c)
 		HIPCHK(hipEventElapsedTime(&ms, e0, e1));
 		return ms;
 	};
-	// the records (if any) wait in a spare buffer while every pair is overwritten
-	RowRec *keep = dalloc<RowRec>(n);
-	HIPCHK(hipMemcpyAsync(keep, c->rows, bytes, hipMemcpyDeviceToDevice, c->s));
 	// candidates: plain allocations (physically contiguous ones, hipDeviceMallocContiguous, probed
 	// 14.1 ms against 11.5-11.8 ms for plain ones at C4 and no better at C3: not tried)
-	// every other candidate of a store under 2 GB is allocated 4 GB large (its first n records used;
-	// the pointer stays the allocation's base): another part of the address space
-	auto alloc_one = [&](bool big) -> RowRec * {
-		void *q = nullptr;
-		HIPCHK(hipMalloc(&q, big ? std::max<size_t>(bytes, (size_t)4 << 30) : bytes));
-		return (RowRec *)q;
-	};
-	std::vector<std::pair<RowRec *, RowRec *>> pairs = {{c->rows, c->rows_alt}};
-	for (int i = 0; i < extra; i++) {
-		const bool big = (i & 1) != 0 && bytes < ((size_t)2 << 30) && fr / 2 > (size_t)(extra + 1) * (8ull << 30);
-		RowRec *a = alloc_one(big);
-		pairs.push_back({a, alloc_one(big)});
-	}
-	std::vector<float> ms(pairs.size());
-	size_t best = 0;
-	for (size_t i = 0; i < pairs.size(); i++) {
-		ms[i] = time_pair(pairs[i].first, pairs[i].second);
-		if (ms[i] < ms[best]) best = i;
-	}
-	for (size_t i = 0; i < pairs.size(); i++)
-		if (i != best) { dfree(pairs[i].first); dfree(pairs[i].second); }
-	c->rows = pairs[best].first;
-	c->rows_alt = pairs[best].second;
+	std::vector<RowRec *> cand = {c->rows, c->rows_alt};
+	for (int i = 0; i < extra; i++) cand.push_back(dalloc<RowRec>(n));
+	std::vector<float> ms(cand.size());
+	for (size_t i = 0; i < cand.size(); i++) ms[i] = score(cand[i]);
+	std::vector<size_t> order(cand.size());
+	for (size_t i = 0; i < order.size(); i++) order[i] = i;
+	std::stable_sort(order.begin(), order.end(), [&](size_t x, size_t y) { return ms[x] < ms[y]; });
+	for (size_t j = 2; j < order.size(); j++) dfree(cand[order[j]]);
+	c->rows = cand[order[0]];
+	c->rows_alt = cand[order[1]];
 	HIPCHK(hipMemcpyAsync(c->rows, keep, bytes, hipMemcpyDeviceToDevice, c->s));
 	sync(c);
 	dfree(keep);
+	dfree(ref);
 	(void)hipEventDestroy(e0);
 	(void)hipEventDestroy(e1);
 	c->place_ms.assign(ms.begin(), ms.end());
-	c->place_pick = (int)best;
+	c->place_pick[0] = (int)order[0];
+	c->place_pick[1] = (int)order[1];
 	const char *lg = getenv("VBFM_PLACE_LOG");
 	if (lg && lg[0] == '1') {
-		fprintf(stderr, "vbfm placement: %u rows, level-0 pattern x4 per pair:", n);
-		for (size_t i = 0; i < ms.size(); i++) fprintf(stderr, " %.3f%s", ms[i], i == best ? "*" : "");
+		fprintf(stderr, "vbfm placement: %u rows, level-0 pattern to and from a reference buffer x2:", n);
+		for (size_t i = 0; i < ms.size(); i++)
+			fprintf(stderr, " %.3f%s", ms[i], (i == order[0] || i == order[1]) ? "*" : "");
 		fprintf(stderr, " ms\n");
 	}
 }
@@ -2197,7 +2194,8 @@ int vbfm_placement_info(vbfm_ctx *c, float *ms, int32_t *count, int32_t *kept)
 	return guarded(c, [&] {
 		const int32_t cap = *count;
 		*count = (int32_t)c->place_ms.size();
-		*kept = c->place_pick;
+		kept[0] = c->place_pick[0];
+		kept[1] = c->place_pick[1];
 		for (int32_t i = 0; ms && i < std::min(cap, *count); i++) ms[i] = c->place_ms[(size_t)i];
 	});
 }

@@ -115,8 +115,8 @@ struct vbfm_ctx {
 	// a sweep driven level by level (vbfm_step_w_level / vbfm_step_v_level): kind -1 none, 0 the
 	// w sweep, 1 the v sweep of factor part_f; part_next = the level expected next
 	int part_kind = -1, part_f = 0;
-	std::vector<float> place_ms;    // tune_placement: each candidate pair's probe time (ms), [0] = first
-	int place_pick = -1;            // ... and the pair kept
+	std::vector<float> place_ms;    // tune_placement: each candidate buffer's score (ms), [0], [1] = the first pair
+	int place_pick[2] = {-1, -1};   // ... and the two kept (records, alternate)
 	uint32_t part_next = 0;
 	uint32_t *level_feats = nullptr;
 	uint8_t *dup = nullptr;

@@ -600,12 +600,13 @@ class FMLearnVB:
         return n.value, r.value, {0: "none", 1: "rccl", 2: "host"}[t.value]
 
     def placement(self):
-        """(probe ms of each candidate record-buffer pair, index kept) of the level store's
-        placement tuning (vbfm_placement_info); ([], -1) when none ran."""
-        buf = (C.c_float * 32)()
-        n, k = C.c_int32(32), C.c_int32()
-        _check(lib().vbfm_placement_info(self._ctx, buf, C.byref(n), C.byref(k)), self._ctx)
-        return [float(buf[i]) for i in range(min(n.value, 32))], k.value
+        """(score in ms of each candidate record buffer, [indices of the two kept]) of the level
+        store's placement tuning (vbfm_placement_info); ([], [-1, -1]) when none ran."""
+        cap = 256
+        buf = (C.c_float * cap)()
+        n, k = C.c_int32(cap), (C.c_int32 * 2)()
+        _check(lib().vbfm_placement_info(self._ctx, buf, C.byref(n), k), self._ctx)
+        return [float(buf[i]) for i in range(min(n.value, cap))], [k[0], k[1]]
 
     def close(self):
         if self._ctx:
