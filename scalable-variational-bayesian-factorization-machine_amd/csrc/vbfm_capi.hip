@@ -326,8 +326,10 @@ static void tune_placement(vbfm_ctx *c)
 	const int tries = te ? std::max(2, atoi(te)) : bytes < ((size_t)2 << 30) ? 64 : 16;
 	size_t fr = 0, tot = 0;
 	HIPCHK(hipMemGetInfo(&fr, &tot));
-	// the stash of the records and the reference buffer come out of the same half
-	const size_t room = fr / 2 > 2 * bytes ? fr / 2 - 2 * bytes : 0;
+	// the stash of the records and the reference buffer come out of the same half (a quarter with
+	// several ranks: rank processes rehearsed on one GPU tune at the same time)
+	const size_t half = c->nranks > 1 ? fr / 4 : fr / 2;
+	const size_t room = half > 2 * bytes ? half - 2 * bytes : 0;
 	const int extra = (int)std::min<size_t>((size_t)tries - 2, room / (bytes + 1));
 	if (extra < 1) return;
 	const uint64_t *lp = c->lcp + c->level_ptr[0];
