@@ -167,6 +167,8 @@ void lord_release(vbfm_ctx *c, bool keep_rows)
 	dfree(c->lpidx); dfree(c->lpx); dfree(c->post_tab); dfree(c->lpay); dfree(c->lpay2);
 	dfree(c->long_segs); dfree(c->seg_part);
 	c->seg_ptr.clear();
+	c->place_ms.clear();
+	c->place_pick[0] = c->place_pick[1] = -1;
 	c->long_min = 0;
 	c->lord = false;
 	c->estore = false;

@@ -1,7 +1,7 @@
 #!/bin/bash
 # One parameterised GPU-box runner (replaces the per-session scripts).
 # usage (from gpurun): bash tools/gpu.sh <outdir> <step> [<step> ...]
-#   tests[=<pytest -k expr>]   the -m gpu suite (or a subset), one process, per-test timeout
+#   tests[=<pytest -k expr>]   the -m gpu suite (or a subset; '+' separates words), one process, per-test timeout
 #   smoke                      __graft_entry__.smoke()
 #   bench[=<args>]             python bench.py <args> > bench.json (args: '+' separates words)
 #   prof[=<args>]              rocprofv3 --kernel-trace --stats of bench.py <args>
@@ -27,7 +27,7 @@ for step in "$@"; do
   case $name in
     tests)
       if [ -n "$arg" ]; then
-        timeout -k 10 1100 python -u -m pytest tests -x -v -m gpu -k "$arg" -p no:cacheprovider --timeout 400 \
+        timeout -k 10 1100 python -u -m pytest tests -x -v -m gpu -k "$args" -p no:cacheprovider --timeout 400 \
           --timeout-method thread > "$O/tests_$n.txt" 2>&1
       else
         timeout -k 10 1100 python -u -m pytest tests -x -v -m gpu -p no:cacheprovider --timeout 400 \
