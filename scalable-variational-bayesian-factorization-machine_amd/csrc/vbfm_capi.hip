@@ -337,7 +337,12 @@ static void tune_placement(vbfm_ctx *c)
 	const uint64_t *lp = c->lcp + c->level_ptr[0];
 	const uint32_t nfl = c->level_ptr[1] - c->level_ptr[0];
 	// the records wait in a stash while every candidate is overwritten
-	RowRec *keep = dalloc<RowRec>(n), *ref = dalloc<RowRec>(n);
+	RowRec *keep = nullptr, *ref = nullptr;
+	if (hipMalloc((void **)&keep, bytes) != hipSuccess || hipMalloc((void **)&ref, bytes) != hipSuccess) {
+		(void)hipGetLastError();
+		dfree(keep);
+		return;
+	}
 	HIPCHK(hipMemcpyAsync(keep, c->rows, bytes, hipMemcpyDeviceToDevice, c->s));
 	hipEvent_t e0, e1;
 	HIPCHK(hipEventCreate(&e0));
@@ -357,8 +362,16 @@ static void tune_placement(vbfm_ctx *c)
 	};
 	// candidates: plain allocations (physically contiguous ones, hipDeviceMallocContiguous, probed
 	// 14.1 ms against 11.5-11.8 ms for plain ones at C4 and no better at C3: not tried)
+	// (an allocation the driver refuses ends the list: the tuning never fails the store)
 	std::vector<RowRec *> cand = {c->rows, c->rows_alt};
-	for (int i = 0; i < extra; i++) cand.push_back(dalloc<RowRec>(n));
+	for (int i = 0; i < extra; i++) {
+		void *q = nullptr;
+		if (hipMalloc(&q, bytes) != hipSuccess) {
+			(void)hipGetLastError();
+			break;
+		}
+		cand.push_back((RowRec *)q);
+	}
 	std::vector<float> ms(cand.size());
 	for (size_t i = 0; i < cand.size(); i++) ms[i] = score(cand[i]);
 	std::vector<size_t> order(cand.size());
