@@ -350,6 +350,10 @@ def main():
                     help="one GPU through a real 1-rank RCCL communicator and the row-shard (split) kernels "
                          "(VBFM_FORCE_SPLIT / VBFM_FORCE_COMM): the per-rank path of an N-GPU run, minus the "
                          "other ranks -- for A/B of the per-level exchange on one GPU")
+    ap.add_argument("--host-upload", action="store_true",
+                    help="hand the train set over from host memory (vbfm_set_train: the copy to the device and "
+                         "the device's CSR build, the drop-in CLI's path) instead of generating it in HBM; the "
+                         "data is the same (generated on the device by a scratch context and copied back first)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-rows", type=int, default=20_000_000,
                     help="rows of the CPU baseline's sample (reported); a 2e6-row, 2-factor sample runs beside it")
@@ -411,6 +415,7 @@ def main():
     torch.cuda.set_device(device)
 
     t0 = time.time()
+    upload_s = None
     online = args.method == "vb_online"
     mc = args.method in ("mcmc", "als")
     if online:
@@ -447,6 +452,20 @@ def main():
     if multihot:
         fml.synth_multihot(0, N, NF, cfg["lo"], cfg["hi"], seed=1000, xmode=0, row_offset=row0)
         fml.synth_multihot(1, n_test, NF, cfg["lo"], cfg["hi"], seed=500000, xmode=0, row_offset=trow0)
+    elif args.host_upload:
+        # the same rows, copied to host memory by a scratch context, then handed over as a caller's
+        # host buffers (vbfm_set_train): at C4 nnz = 4e9 > 2^32 entries through the upload path
+        scratch = vbfm.FMLearnVB(1, 1, 1, D, min_target=1.0, max_target=5.0, device=device, place_candidates=1)
+        scratch.synth(0, N, F, S, seed=1000, xmode=0, row_offset=row0)
+        cp, ent, y = scratch.get_csc(0)
+        scratch.close()
+        host_train = vbfm.DataSubset(cp, ent, y, num_feature=NF)
+        del cp, ent, y
+        t_up = time.time()
+        fml.set_train(host_train)
+        upload_s = time.time() - t_up
+        del host_train
+        fml.synth(1, n_test, F, S, seed=500000, xmode=0, row_offset=trow0)
     else:
         fml.synth(0, N, F, S, seed=1000, xmode=0, row_offset=row0)
         fml.synth(1, n_test, F, S, seed=500000, xmode=0, row_offset=trow0)
@@ -464,8 +483,12 @@ def main():
         fml.set_profiling(True, launch_event_stride(fml.levels()[1], k))
     layout = fml.layout()
     nnz = fml.shape(0)[2]                # this rank's train entries
-    log("rank %d: setup %.1f s (N=%d F=%d S=%d features=%d nnz=%d k=%d, %s layout)" % (
-        rank, time.time() - t0, N, F, S, NF, nnz, k, layout))
+    setup_s = time.time() - t0
+    setup = fml.setup_info()             # the library's own split of it (vbfm_setup_info)
+    log("rank %d: setup %.1f s (N=%d F=%d S=%d features=%d nnz=%d k=%d, %s layout; train set %.2f s, "
+        "schedule %.2f s, store %.2f s incl. placement %.2f s over %d buffers)" % (
+            rank, setup_s, N, F, S, NF, nnz, k, layout, setup["s_set_train"], setup["s_schedule"],
+            setup["s_store"], setup["s_placement"], setup["place_candidates"]))
 
     cpu_leg = None
     run_leg, leg_reason = cpu_leg_plan(rank, world, args, mc, online, multihot)
@@ -626,6 +649,14 @@ def main():
         # the level store's record buffers: probe time of each candidate pair (level 0's pattern,
         # 4 passes), the first allocated first, and the pair kept (VBFM_PLACE)
         "placement": {"buffer_ms": [round(x, 4) for x in place_ms], "kept": place_kept} if place_ms else None,
+        # host seconds from the context's creation to the first iteration (device data generation,
+        # initial parameters, schedule, row store, placement search), and the library's split of it
+        "setup_s": setup_s,
+        "train_handover": ("host memory (vbfm_set_train: %.2f s for the copy and the device CSR build of %d entries)"
+                           % (upload_s, nnz)) if upload_s is not None else "generated in HBM (vbfm_synth_generate)",
+        "setup": {"train_set_s": setup["s_set_train"], "schedule_s": setup["s_schedule"],
+                  "store_s": setup["s_store"], "placement_s": setup["s_placement"],
+                  "placement_bytes": setup["place_bytes"], "placement_candidates": setup["place_candidates"]},
         "factor_sweep_ms_per_step": sweep_ms,
         "factor_sweep_nnz_k_per_s": nnz_total * k / (sweep_ms * 1e-3),
         "test_rmse": rmse_of(stats[-1]),

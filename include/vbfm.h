@@ -33,9 +33,11 @@ extern "C" {
 
 /* 2: vbfm_synth_generate's model_seed / row_offset, vbfm_synth_multihot, VBFM_LAYOUT_ENTRY,
  *    vbfm_iter_stats::ms_test_predict, checkpoints, vbfm_comm_info, vbfm_device_count and the
- *    per-level step entry points. A binding checks vbfm_abi_version() against the value it was
- *    built for and refuses a mismatch (struct sizes and argument lists differ). */
-#define VBFM_ABI_VERSION 2
+ *    per-level step entry points.
+ * 3: vbfm_config's placement budget (place_candidates, place_budget_bytes) and vbfm_setup_info.
+ * A binding checks vbfm_abi_version() against the value it was built for and refuses a mismatch
+ * (struct sizes and argument lists differ). */
+#define VBFM_ABI_VERSION 3
 
 typedef struct vbfm_ctx vbfm_ctx;
 
@@ -71,7 +73,24 @@ typedef struct {
 	float max_target;         /* train.max_target (libfm.cpp:332) */
 	int32_t device;           /* HIP device ordinal */
 	int32_t task;             /* 0 = regression (the only task the VB learner evaluates) */
+	/* Placement search of the level-ordered store's two record buffers (no reference counterpart;
+	 * DESIGN.md §5b): the scattered record writes of a level run up to ~20 % faster or slower
+	 * depending on where the driver placed the buffers, so at store build (>= 2e6 rows) the library
+	 * scores candidate buffers on level 0's pattern and keeps the two fastest. Results do not depend
+	 * on it (bit for bit). Zero-initialised fields take the defaults.
+	 *   place_candidates:   buffers scored, the store's own two included (0 = default: 64 for a
+	 *                       store under 2 GB of records, 16 above; 1 or 2 = no search);
+	 *   place_budget_bytes: device memory the search may hold at once on top of the store -- the
+	 *                       records' stash, a reference buffer and the fresh candidates (0 = default,
+	 *                       VBFM_PLACE_BUDGET_DEFAULT).
+	 * The search also never takes more than half of the device memory free when it starts (a quarter
+	 * with several ranks); when that leaves room for fewer candidates it scores fewer, or none: it
+	 * never fails the store. VBFM_PLACE=0 / VBFM_PLACE_TRIES=n / VBFM_PLACE_BUDGET_GB=x in the
+	 * environment override the two fields. vbfm_setup_info reports what the search held and took. */
+	int32_t place_candidates;
+	uint64_t place_budget_bytes;
 } vbfm_config;
+#define VBFM_PLACE_BUDGET_DEFAULT ((uint64_t)48 << 30)   /* 48 GiB: 8 candidates at C4 (6.4 GB buffers) */
 
 /* Variational and hyper parameters (fm_learn_vb.h:36-46). Arrays are caller-allocated. */
 typedef struct {
@@ -258,6 +277,22 @@ int vbfm_comm_info(vbfm_ctx *ctx, int32_t *nranks, int32_t *rank, int32_t *trans
  * first, and in kept[0], kept[1] the indices of the two buffers kept (records, alternate).
  * *count = 0 when no placement was tuned. ms holds up to *count on entry (in: capacity). */
 int vbfm_placement_info(vbfm_ctx *ctx, float *ms, int32_t *count, int32_t *kept);
+/* What setting up the train set cost (no reference counterpart; the reference's load and
+ * create_data_t are the host's, Data.h:106-283, 457-509): host wall seconds of the last
+ * vbfm_set_train (copy to the device + the device CSR build) and of the first sweep's set-up of that
+ * train set -- the dependency levels, the row store (level / entry store, long-column segments,
+ * split-form payloads) and, inside it, the placement search with the device memory it held at its
+ * peak and the candidates it scored (0: no search). Zero until the step has run. */
+typedef struct {
+	double s_set_train;       /* vbfm_set_train / vbfm_synth_generate of the train set */
+	double s_schedule;        /* dependency levels */
+	double s_store;           /* row store build, the placement search included */
+	double s_placement;       /* ... of which the placement search */
+	uint64_t place_bytes;     /* device memory the search held at its peak */
+	int32_t place_candidates; /* buffers scored (0: no search) */
+	int32_t place_kept[2];    /* the two kept, as vbfm_placement_info's kept */
+} vbfm_setup_stats;
+int vbfm_setup_info(vbfm_ctx *ctx, vbfm_setup_stats *out);
 
 /* Partition of the VB sweep over ranks (set before vbfm_set_train).
  *   VBFM_SHARD_ROWS (default): the exact row-sharded mode above.

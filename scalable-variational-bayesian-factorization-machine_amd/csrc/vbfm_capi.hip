@@ -305,6 +305,18 @@ bool build_estore(vbfm_ctx *c, const std::vector<uint64_t> &lcp, const std::vect
 	return true;
 }
 
+// Non-temporal record traffic of the deferred split kernels (LevelArgs::pending bits 2 = loads,
+// 4 = stores). VBFM_DEFER_NT=0..3 (bit 0 loads, bit 1 stores) overrides; default both: the moved
+// records then leave more of L2 to the posterior table the next level gathers from (one N = 8
+// rank's shape, 1.25e7 rows: 426-427 -> 415-417 us per split level, profiles/r05_split/; alone,
+// either half gained 0-1.5 %, profiles/probes/ab_defer_loads.txt, ab_defer_nt_store.txt)
+static int defer_nt(const vbfm_ctx *)
+{
+	const char *e = getenv("VBFM_DEFER_NT");
+	const int v = e ? atoi(e) : 3;
+	return ((v & 1) ? 2 : 0) | ((v & 2) ? 4 : 0);
+}
+
 // Placement of the store's two record buffers (VBFM_PLACE, default 1). The level kernel's
 // scattered whole-record writes run up to ~20 % faster or slower depending on where the driver
 // placed the two buffers, persistently per allocation, while streaming copies do not change
@@ -313,27 +325,38 @@ bool build_estore(vbfm_ctx *c, const std::vector<uint64_t> &lcp, const std::vect
 // so buffers are scored one at a time: the store's two buffers and up to VBFM_PLACE_TRIES - 2 fresh
 // allocations, each moved to and from one reference buffer on level 0's real pattern (k_place_move,
 // no arithmetic); the two best are kept (the records move with them), the rest freed. Only where a
-// launch is long enough to time (>= 2e6 rows) and the candidates fit in half of the free memory.
-// The results do not depend on the buffers (bit for bit).
+// launch is long enough to time (>= 2e6 rows), within the caller's budget (vbfm_config
+// place_candidates / place_budget_bytes) and half of the free memory. The results do not depend on
+// the buffers (bit for bit).
 static void tune_placement(vbfm_ctx *c)
 {
 	const uint32_t n = c->tr.n, L = nlevels(c);
+	c->t_place = 0;
+	c->place_bytes = 0;
+	if (n < 2000000u || L < 2 || !c->lnext) return;
 	const char *pe = getenv("VBFM_PLACE");
-	if ((pe && pe[0] == '0') || n < 2000000u || L < 2 || !c->lnext) return;
-	const char *te = getenv("VBFM_PLACE_TRIES");
+	if (pe && pe[0] == '0') return;
 	const size_t bytes = (size_t)n * sizeof(RowRec);
 	// stores under 2 GB (C3, one rank of N = 4 or 8) try 64 buffers, larger ones 16: the fast
 	// allocations come in clusters along the allocation sequence and a few tries miss them on some
 	// boxes (profiles/r04_short_columns/placement_tries/)
-	const int tries = te ? std::max(2, atoi(te)) : bytes < ((size_t)2 << 30) ? 64 : 16;
+	const char *te = getenv("VBFM_PLACE_TRIES");
+	int tries = bytes < ((size_t)2 << 30) ? 64 : 16;
+	if (c->place_cands_cfg > 0) tries = c->place_cands_cfg;
+	if (te) tries = atoi(te);
+	if (tries <= 2) return;
+	const char *be = getenv("VBFM_PLACE_BUDGET_GB");
+	uint64_t budget = c->place_budget_cfg ? c->place_budget_cfg : VBFM_PLACE_BUDGET_DEFAULT;
+	if (be) budget = (uint64_t)(atof(be) * (double)(1ull << 30));
 	size_t fr = 0, tot = 0;
 	HIPCHK(hipMemGetInfo(&fr, &tot));
-	// the stash of the records and the reference buffer come out of the same half (a quarter with
-	// several ranks: rank processes rehearsed on one GPU tune at the same time)
-	const size_t half = c->nranks > 1 ? fr / 4 : fr / 2;
-	const size_t room = half > 2 * bytes ? half - 2 * bytes : 0;
+	// no more than half of the free memory (a quarter with several ranks: rank processes rehearsed
+	// on one GPU tune at the same time); the records' stash and the reference buffer come out of it
+	const size_t cap = std::min<uint64_t>(budget, c->nranks > 1 ? fr / 4 : fr / 2);
+	const size_t room = cap > 2 * bytes ? cap - 2 * bytes : 0;
 	const int extra = (int)std::min<size_t>((size_t)tries - 2, room / (bytes + 1));
 	if (extra < 1) return;
+	const double t0 = wall_s();
 	const uint64_t *lp = c->lcp + c->level_ptr[0];
 	const uint32_t nfl = c->level_ptr[1] - c->level_ptr[0];
 	// the records wait in a stash while every candidate is overwritten
@@ -343,52 +366,81 @@ static void tune_placement(vbfm_ctx *c)
 		dfree(keep);
 		return;
 	}
-	HIPCHK(hipMemcpyAsync(keep, c->rows, bytes, hipMemcpyDeviceToDevice, c->s));
-	hipEvent_t e0, e1;
-	HIPCHK(hipEventCreate(&e0));
-	HIPCHK(hipEventCreate(&e1));
-	auto score = [&](RowRec *x) {
-		HIPCHK(vbk::place_move(ref, x, lp, c->lnext, nfl, c->s));   // warm-up
-		HIPCHK(hipEventRecord(e0, c->s));
-		for (int r = 0; r < 2; r++) {
-			HIPCHK(vbk::place_move(ref, x, lp, c->lnext, nfl, c->s));
-			HIPCHK(vbk::place_move(x, ref, lp, c->lnext, nfl, c->s));
-		}
-		HIPCHK(hipEventRecord(e1, c->s));
-		HIPCHK(hipEventSynchronize(e1));
-		float ms = 0.f;
-		HIPCHK(hipEventElapsedTime(&ms, e0, e1));
-		return ms;
-	};
-	// candidates: plain allocations (physically contiguous ones, hipDeviceMallocContiguous, probed
-	// 14.1 ms against 11.5-11.8 ms for plain ones at C4 and no better at C3: not tried)
-	// (an allocation the driver refuses ends the list: the tuning never fails the store)
+	hipEvent_t e0 = nullptr, e1 = nullptr;
+	// cand[0], cand[1]: the store's own pair; the rest fresh allocations this search owns until it
+	// commits. On any failure the records go back into c->rows from the stash, every fresh candidate,
+	// the stash and the reference buffer are freed, and the error propagates (build_schedule then
+	// leaves the schedule to be rebuilt by the next call)
 	std::vector<RowRec *> cand = {c->rows, c->rows_alt};
-	for (int i = 0; i < extra; i++) {
-		void *q = nullptr;
-		if (hipMalloc(&q, bytes) != hipSuccess) {
-			(void)hipGetLastError();
-			break;
+	bool stashed = false;
+	try {
+		HIPCHK(hipMemcpyAsync(keep, c->rows, bytes, hipMemcpyDeviceToDevice, c->s));
+		stashed = true;
+		HIPCHK(hipEventCreate(&e0));
+		HIPCHK(hipEventCreate(&e1));
+		auto score = [&](RowRec *x) {
+			HIPCHK(vbk::place_move(ref, x, lp, c->lnext, nfl, c->s));   // warm-up
+			HIPCHK(hipEventRecord(e0, c->s));
+			for (int r = 0; r < 2; r++) {
+				HIPCHK(vbk::place_move(ref, x, lp, c->lnext, nfl, c->s));
+				HIPCHK(vbk::place_move(x, ref, lp, c->lnext, nfl, c->s));
+			}
+			HIPCHK(hipEventRecord(e1, c->s));
+			HIPCHK(hipEventSynchronize(e1));
+			float ms = 0.f;
+			HIPCHK(hipEventElapsedTime(&ms, e0, e1));
+			return ms;
+		};
+		// candidates: plain allocations (physically contiguous ones, hipDeviceMallocContiguous, probed
+		// 14.1 ms against 11.5-11.8 ms for plain ones at C4 and no better at C3: not tried)
+		// (an allocation the driver refuses ends the list: the tuning never fails the store)
+		for (int i = 0; i < extra; i++) {
+			void *q = nullptr;
+			if (hipMalloc(&q, bytes) != hipSuccess) {
+				(void)hipGetLastError();
+				break;
+			}
+			cand.push_back((RowRec *)q);
 		}
-		cand.push_back((RowRec *)q);
+		c->place_bytes = (uint64_t)bytes * cand.size();   // the fresh candidates + the stash + the reference
+		std::vector<float> ms(cand.size());
+		for (size_t i = 0; i < cand.size(); i++) {
+			ms[i] = score(cand[i]);
+			if (i == 2 && fault_at("placement")) throw HipError{hipErrorOutOfMemory, "VBFM_FAULT=placement"};
+		}
+		std::vector<size_t> order(cand.size());
+		for (size_t i = 0; i < order.size(); i++) order[i] = i;
+		std::stable_sort(order.begin(), order.end(), [&](size_t x, size_t y) { return ms[x] < ms[y]; });
+		// commit (nothing below the frees can throw before c->rows names a live buffer again)
+		for (size_t j = 2; j < order.size(); j++) dfree(cand[order[j]]);
+		c->rows = cand[order[0]];
+		c->rows_alt = cand[order[1]];
+		cand.resize(2);   // every fresh buffer is now the store's or freed
+		HIPCHK(hipMemcpyAsync(c->rows, keep, bytes, hipMemcpyDeviceToDevice, c->s));
+		sync(c);
+		stashed = false;
+		c->place_ms.assign(ms.begin(), ms.end());
+		c->place_pick[0] = (int)order[0];
+		c->place_pick[1] = (int)order[1];
+	} catch (...) {
+		(void)hipStreamSynchronize(c->s);
+		if (stashed) (void)hipMemcpy(c->rows, keep, bytes, hipMemcpyDeviceToDevice);
+		for (size_t i = 2; i < cand.size(); i++) dfree(cand[i]);
+		dfree(keep);
+		dfree(ref);
+		if (e0) (void)hipEventDestroy(e0);
+		if (e1) (void)hipEventDestroy(e1);
+		c->place_ms.clear();
+		c->place_pick[0] = c->place_pick[1] = -1;
+		throw;
 	}
-	std::vector<float> ms(cand.size());
-	for (size_t i = 0; i < cand.size(); i++) ms[i] = score(cand[i]);
-	std::vector<size_t> order(cand.size());
-	for (size_t i = 0; i < order.size(); i++) order[i] = i;
-	std::stable_sort(order.begin(), order.end(), [&](size_t x, size_t y) { return ms[x] < ms[y]; });
-	for (size_t j = 2; j < order.size(); j++) dfree(cand[order[j]]);
-	c->rows = cand[order[0]];
-	c->rows_alt = cand[order[1]];
-	HIPCHK(hipMemcpyAsync(c->rows, keep, bytes, hipMemcpyDeviceToDevice, c->s));
-	sync(c);
 	dfree(keep);
 	dfree(ref);
 	(void)hipEventDestroy(e0);
 	(void)hipEventDestroy(e1);
-	c->place_ms.assign(ms.begin(), ms.end());
-	c->place_pick[0] = (int)order[0];
-	c->place_pick[1] = (int)order[1];
+	c->t_place = wall_s() - t0;
+	const auto &ms = c->place_ms;
+	const size_t order[2] = {(size_t)c->place_pick[0], (size_t)c->place_pick[1]};
 	const char *lg = getenv("VBFM_PLACE_LOG");
 	if (lg && lg[0] == '1') {
 		fprintf(stderr, "vbfm placement: %u rows, level-0 pattern to and from a reference buffer x2:", n);
@@ -684,6 +736,9 @@ static void kahn_levels(vbfm_ctx *c, uint32_t *level)
 // schedule: the one the un-sharded data set defines.
 void build_schedule(vbfm_ctx *c)
 {
+	const double t0 = wall_s();
+	c->t_schedule = c->t_store = c->t_place = 0;
+	c->place_bytes = 0;
 	DevData &d = c->tr;
 	const uint32_t nf = d.nf;
 	uint32_t *level = dalloc<uint32_t>(nf);
@@ -756,10 +811,20 @@ void build_schedule(vbfm_ctx *c)
 		c->stats_cap = maxlev;
 	}
 	c->sched_ready = true;
-	const char *chk = getenv("VBFM_CHECK");
-	if (chk && chk[0] == '1') check_schedule(c);
-	build_fshards(c);
-	build_lorder(c, cp, feats);
+	// a failure from here on (the store's allocations, the placement search) leaves the schedule to
+	// be rebuilt by the next call instead of running on a half-built store
+	try {
+		const char *chk = getenv("VBFM_CHECK");
+		if (chk && chk[0] == '1') check_schedule(c);
+		build_fshards(c);
+		const double t1 = wall_s();
+		c->t_schedule = t1 - t0;
+		build_lorder(c, cp, feats);
+		c->t_store = wall_s() - t1;
+	} catch (...) {
+		c->sched_ready = false;
+		throw;
+	}
 }
 
 // segments of the hyper / free-energy sums: (w or factor f) x group. The attributes are
@@ -965,7 +1030,7 @@ void sweep_level(vbfm_ctx *c, uint32_t l, bool is_w, int f)
 			const bool carried = (l == 0 || c->estore) && c->carry_in != 0;
 			a.pend_kind = carried ? c->carry_in : 0;
 			a.pending = (l > 0 || carried) ? 1 : 0;
-			if (c->tr.n > 50000000u) a.pending |= 2;     // non-temporal record loads (large shards)
+			a.pending |= defer_nt(c);   // non-temporal record loads (2) / stores (4)
 			a.first_prev = l == 1;
 			stats_exchange(c, a, [&](const LevelArgs &b) { HIPCHK(vbk::lord_defer_level(b, is_w, c->s)); });
 			HIPCHK(vbk::lord_defer_post(a, is_w, c->s));
@@ -1100,6 +1165,7 @@ void step_level(vbfm_ctx *c, bool is_w, int f, uint32_t l)
 	}
 	try {
 		sweep_level(c, l, is_w, f);
+		if (l == 1 && fault_at("level")) throw HipError{hipErrorLaunchFailure, "VBFM_FAULT=level"};
 	} catch (...) {
 		c->part_kind = -2;   // the records may be half moved: refuse everything until a restart
 		throw;
@@ -1274,6 +1340,7 @@ int vbfm_create(vbfm_ctx **out, const vbfm_config *cfg)
 	if (cfg->task != 0) return fail(nullptr, "task not supported by the VB learner (regression only)");
 	if (cfg->num_factor < 0) return fail(nullptr, "negative number of factors");
 	if (cfg->num_attr_groups == 0) return fail(nullptr, "num_attr_groups must be >= 1");
+	if (cfg->place_candidates < 0) return fail(nullptr, "place_candidates must be >= 0");
 	int ndev = 0;
 	if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return fail(nullptr, "no HIP device available");
 	if (cfg->device < 0 || cfg->device >= ndev) return fail(nullptr, "device ordinal out of range");
@@ -1282,6 +1349,8 @@ int vbfm_create(vbfm_ctx **out, const vbfm_config *cfg)
 	c->k0 = cfg->k0 != 0; c->k1 = cfg->k1 != 0; c->k = cfg->num_factor;
 	c->D = cfg->num_attribute; c->G = cfg->num_attr_groups;
 	c->min_target = cfg->min_target; c->max_target = cfg->max_target;
+	c->place_cands_cfg = cfg->place_candidates;
+	c->place_budget_cfg = cfg->place_budget_bytes;
 	{
 		const char *fs = getenv("VBFM_FORCE_SPLIT");
 		c->force_split = fs && fs[0] == '1';
@@ -1392,6 +1461,7 @@ int vbfm_set_train(vbfm_ctx *c, const vbfm_csc *in)
 {
 	if (!c) return fail(nullptr, "null context");
 	return guarded(c, [&] {
+		const double t0 = wall_s();
 		check_csc(in);
 		const uint32_t nf = global_nf(c, in->num_feature);
 		if (nf > c->D) throw std::string("train num_feature exceeds num_attribute");
@@ -1400,6 +1470,7 @@ int vbfm_set_train(vbfm_ctx *c, const vbfm_csc *in)
 		HIPCHK(vbk::mark_first(c->tr.row_ptr, c->tr.csr, c->tr.col_ptr, c->tr.csc, c->tr.n, c->s));
 		alloc_rows(c);
 		c->part_kind = -1;   // new records: no level-by-level sweep in progress
+		c->t_set_train = wall_s() - t0;
 	});
 }
 
@@ -1457,6 +1528,7 @@ int vbfm_synth_generate(vbfm_ctx *c, int32_t which, uint32_t n, uint32_t F, uint
 {
 	if (!c) return fail(nullptr, "null context");
 	return guarded(c, [&] {
+		const double t0 = wall_s();
 		if (which != 0 && which != 1) throw std::string("which must be 0 (train) or 1 (test)");
 		const uint64_t nf64 = (uint64_t)F * S;
 		if (nf64 >= 0xFFFFFFFFull || nf64 >= c->D || F == 0 || S == 0)
@@ -1500,6 +1572,7 @@ int vbfm_synth_generate(vbfm_ctx *c, int32_t which, uint32_t n, uint32_t F, uint
 		sync(c);
 		dfree(stmp); dfree(ki); dfree(ko); dfree(vi); dfree(vo);
 		synth_finish(c, which);
+		if (which == 0) c->t_set_train = wall_s() - t0;
 	});
 }
 
@@ -1508,6 +1581,7 @@ int vbfm_synth_multihot(vbfm_ctx *c, int32_t which, uint32_t n, uint32_t D, uint
 {
 	if (!c) return fail(nullptr, "null context");
 	return guarded(c, [&] {
+		const double t0 = wall_s();
 		if (which != 0 && which != 1) throw std::string("which must be 0 (train) or 1 (test)");
 		if (lo < 1 || hi < lo || hi > 64 || D < hi || D >= c->D)
 			throw std::string("multi-hot shape: need 1 <= lo <= hi <= 64, hi <= num_features < num_attribute");
@@ -1565,6 +1639,7 @@ int vbfm_synth_multihot(vbfm_ctx *c, int32_t which, uint32_t n, uint32_t D, uint
 		sync(c);
 		dfree(stmp); dfree(ki); dfree(ko); dfree(vi); dfree(vo); dfree(row_of); dfree(gains);
 		synth_finish(c, which);
+		if (which == 0) c->t_set_train = wall_s() - t0;
 	});
 }
 
@@ -1767,6 +1842,7 @@ int vbfm_get_rows(vbfm_ctx *c, double *e, double *t, double *q, double *tq, doub
 {
 	if (!c) return fail(nullptr, "null context");
 	return guarded(c, [&] {
+		if (c->part_kind == -2) no_partial(c);   // a failed level: the records may be half moved
 		std::vector<RowRec> h;
 		if (c->part_kind >= 0 && c->lord) {   // half a level-by-level sweep on a level-ordered store
 			sync(c);
@@ -1828,8 +1904,12 @@ struct StateHeader {
 	uint32_t level_order; // the records were in level-0 order (data-set sums add them in that order)
 	uint64_t layout;      // version 2: row layout (VBFM_LAYOUT_*) | shard mode << 8: both decide the
 	                      // order of the data-set sums, so a resume must use the same ones
-	uint64_t reserved[3];
+	uint64_t flags;       // STATE_FLAG_* (0 in files of libvbfm before round 5: was reserved)
+	uint64_t reserved[2];
 };
+// the layout word of an online checkpoint says whether its batches ran on the per-batch level store
+// (written since round 5; before, an online learner always wrote COLUMN, whichever it used)
+constexpr uint64_t STATE_FLAG_OV_LAYOUT = 1;
 static_assert(sizeof(StateHeader) == 104, "checkpoint header layout");
 constexpr char STATE_MAGIC[8] = {'V', 'B', 'F', 'M', 'S', 'T', '0', '1'};
 constexpr char MC_STATE_MAGIC[8] = {'V', 'B', 'F', 'M', 'M', 'C', '0', '1'};   // MCMC / ALS payload
@@ -1876,6 +1956,7 @@ StateHeader state_header(vbfm_ctx *c, uint32_t iter)
 	h.nranks = c->nranks; h.rank = c->rank;
 	h.iter = iter;
 	h.layout = state_layout(c);
+	h.flags = STATE_FLAG_OV_LAYOUT;
 	return h;
 }
 
@@ -1980,6 +2061,10 @@ int vbfm_load_state(vbfm_ctx *c, const char *path, uint32_t *iter)
 		if (h.n_train != c->tr.n || h.nf_train != c->tr.nf || h.nnz_train != c->tr.nnz ||
 		    h.data_fp != train_fingerprint(c))
 			throw std::string("checkpoint of another train data set");
+		if (kind == 2 && !(h.flags & STATE_FLAG_OV_LAYOUT))
+			throw std::string("an online VB checkpoint written by an older libvbfm, whose layout word does not record "
+			                  "whether the batches ran on the per-batch level store (the order of the batches' data-set "
+			                  "sums): resume it with the libvbfm that wrote it");
 		if (h.layout != state_layout(c))
 			throw std::string("checkpoint of another row layout or shard mode (the data-set sums would add the rows in "
 			                  "another order): resume with the same VBFM_LAYOUT / vbfm_set_layout and shard mode");
@@ -2214,6 +2299,22 @@ int vbfm_placement_info(vbfm_ctx *c, float *ms, int32_t *count, int32_t *kept)
 		kept[0] = c->place_pick[0];
 		kept[1] = c->place_pick[1];
 		for (int32_t i = 0; ms && i < std::min(cap, *count); i++) ms[i] = c->place_ms[(size_t)i];
+	});
+}
+
+int vbfm_setup_info(vbfm_ctx *c, vbfm_setup_stats *o)
+{
+	if (!c || !o) return fail(c, "null argument");
+	return guarded(c, [&] {
+		memset(o, 0, sizeof(*o));
+		o->s_set_train = c->t_set_train;
+		o->s_schedule = c->t_schedule;
+		o->s_store = c->t_store;
+		o->s_placement = c->t_place;
+		o->place_bytes = c->place_bytes;
+		o->place_candidates = (int32_t)c->place_ms.size();
+		o->place_kept[0] = c->place_pick[0];
+		o->place_kept[1] = c->place_pick[1];
 	});
 }
 

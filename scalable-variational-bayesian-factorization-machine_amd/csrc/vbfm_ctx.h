@@ -7,8 +7,10 @@
 
 #include <rccl/rccl.h>
 #include <rocprofiler-sdk-roctx/roctx.h>
+#include <chrono>
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
 
 #include <string>
 #include <vector>
@@ -65,6 +67,28 @@ template <class T> inline void dfree(T *&p)
 
 enum { EV_BEGIN, EV_W0, EV_W, EV_V, EV_HYPER, EV_TEST, EV_TP0, EV_TP1, EV_N };
 
+// host wall clock (s) of the set-up steps vbfm_setup_info reports
+inline double wall_s()
+{
+	return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+// the deferred MCMC / ALS split kernel's record stores non-temporal (VBFM_DEFER_NT bit 1, default
+// on; its loads always are), as the VB one's (vbfm_capi.hip defer_nt)
+inline bool defer_nt_stores()
+{
+	const char *e = getenv("VBFM_DEFER_NT");
+	return ((e ? atoi(e) : 3) & 2) != 0;
+}
+
+// test hook: VBFM_FAULT=<where> makes the named step throw as a failed HIP call would (the error
+// paths of the store build and the per-level steps, tests/test_placement_gpu.py)
+inline bool fault_at(const char *where)
+{
+	const char *e = getenv("VBFM_FAULT");
+	return e && !strcmp(e, where);
+}
+
 // roctx ranges around the phases of an iteration (VBFM_ROCTX=1; 2 adds one per level launch)
 // for rocprofv3 --marker-trace timelines
 inline int roctx_level()
@@ -117,6 +141,11 @@ struct vbfm_ctx {
 	int part_kind = -1, part_f = 0;
 	std::vector<float> place_ms;    // tune_placement: each candidate buffer's score (ms), [0], [1] = the first pair
 	int place_pick[2] = {-1, -1};   // ... and the two kept (records, alternate)
+	int place_cands_cfg = 0;        // vbfm_config::place_candidates / place_budget_bytes (0: defaults)
+	uint64_t place_budget_cfg = 0;
+	uint64_t place_bytes = 0;       // device memory the last search held at its peak
+	// host wall seconds of the set-up steps (vbfm_setup_info)
+	double t_set_train = 0, t_schedule = 0, t_store = 0, t_place = 0;
 	uint32_t part_next = 0;
 	uint32_t *level_feats = nullptr;
 	uint8_t *dup = nullptr;

@@ -26,15 +26,17 @@
 // The longest mean column of a level swept with the 64-thread x 2 workgroup shape (longer: 256 x
 // 1, 256 x 2, 512 x 2). Every level kernel -- fused, deferred split, column-gather, entry store,
 // MCMC -- takes its shape from the same thresholds: the same shape gives the same reduction tree,
-// so the layouts and the fused / split forms stay bit-identical to each other. 96: at 128 a level
-// of C4's per-rank shard on 8 GPUs (columns of ~100 entries) runs ~1 % faster in the deferred
-// split form but ~2 % slower fused (profiles/probes/ab_defer_small_shape.txt). VBFM_SMALL_MAX
-// overrides (A/B).
+// so the layouts and the fused / split forms stay bit-identical to each other. 128: a level of
+// C4's per-rank shard on 8 GPUs (columns of ~100 entries) runs 2-5 % faster in the deferred split
+// form with 64 x 2 than with 256 x 1 (one wave per column: more columns, and so more posterior
+// gathers, in flight per CU; profiles/r05_split/), ~1-2 % slower fused -- a shape that only a
+// row-sharded run meets among the BASELINE configurations (profiles/probes/ab_defer_small_shape.txt).
+// VBFM_SMALL_MAX overrides (A/B).
 inline uint32_t shape_small_max()
 {
 	static const uint32_t v = [] {
 		const char *e = getenv("VBFM_SMALL_MAX");
-		return e ? (uint32_t)atoi(e) : 96u;
+		return e ? (uint32_t)atoi(e) : 128u;
 	}();
 	return v;
 }
@@ -109,7 +111,7 @@ struct LevelArgs {
 	PostT *tab;                // posteriors of the previous level (read) / of this level (written)
 	const uint4 *lpay;         // {x bits, lnext, lpidx, lpx bits} per level-ordered entry (deferred split)
 	const uint2 *lpay2;        // ... {lnext, lpidx} instead when every x is 1 (lpay null)
-	int pending;               // bit 0: apply the previous level's correction first; bit 1: non-temporal record loads
+	int pending;               // bit 0: apply the previous level's correction first; bit 1: non-temporal record loads; bit 2: ... stores
 	int first_prev;            // the previous level is level 0 (q-cache restart of its entries)
 	int pend_kind;             // level 0 of a v sweep: the pending correction is the previous sweep's last
 	                           // level (1: v of the other q-cache slot, 2: w); 0: this sweep's own

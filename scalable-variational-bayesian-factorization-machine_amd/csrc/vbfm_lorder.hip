@@ -601,11 +601,15 @@ __global__ __launch_bounds__(LONG_BLOCK) void k_lord_long_move(LevelArgs a)
 	                                false, a.dst, a.first_level != 0, op);
 }
 
-// split form (row-sharded multi-GPU): statistics of the local rows -> all-reduce -> move
-template <int BLOCK, bool IS_W, int P>
+// split form (row-sharded multi-GPU): statistics of the local rows -> all-reduce -> move. The
+// launch shape is the fused kernel's (launch_lord): the same BLOCK gives the same reduction tree,
+// and a column's run takes no more LDS than it needs (with a fixed 256 x 2 shape the 100-entry
+// columns of one N = 8 rank held 33-35 KB per workgroup: 13-15 resident waves per CU, 336 + 472 us
+// per level against 341 us fused, profiles/r05_split/)
+template <int BLOCK, int R, bool IS_W, int P>
 __global__ __launch_bounds__(BLOCK) void k_level_lord_stats(LevelArgs a)
 {
-	constexpr uint32_t CAP = BLOCK * 2;
+	constexpr uint32_t CAP = BLOCK * R;
 	__shared__ double2 recs[CAP * 4];
 	__shared__ double lds[2 * (BLOCK / 64)];
 	const uint32_t j = level_feat(a, blockIdx.x);
@@ -620,10 +624,10 @@ __global__ __launch_bounds__(BLOCK) void k_level_lord_stats(LevelArgs a)
 	if (threadIdx.x == 0) a.stats[blockIdx.x] = make_double2(s1, s2);
 }
 
-template <int BLOCK, bool IS_W, int P, bool NEXT, bool ENT = false>
+template <int BLOCK, int R, bool IS_W, int P, bool NEXT, bool ENT = false>
 __global__ __launch_bounds__(BLOCK) void k_level_lord_move(LevelArgs a)
 {
-	constexpr uint32_t CAP = BLOCK * 2;
+	constexpr uint32_t CAP = BLOCK * R;
 	__shared__ double2 recs[CAP * 4];
 	__shared__ uint32_t dsts[CAP];
 	const uint32_t j = level_feat(a, blockIdx.x);
@@ -928,16 +932,34 @@ void launch_lord(const LevelArgs &a, hipStream_t s)
 	else k_level_lord<512, 2, IS_W, P, NEXT, false><<<a.nfeat, 512, 0, s>>>(a);
 }
 
+template <bool IS_W, int P, bool NEXT, bool ENT>
+void launch_lord_move_shape(const LevelArgs &a, hipStream_t s)
+{
+	if (a.avg_len <= shape_small_max()) k_level_lord_move<64, 2, IS_W, P, NEXT, ENT><<<a.nfeat, 64, 0, s>>>(a);
+	else if (a.avg_len <= 320) k_level_lord_move<256, 1, IS_W, P, NEXT, ENT><<<a.nfeat, 256, 0, s>>>(a);
+	else if (a.avg_len <= 640) k_level_lord_move<256, 2, IS_W, P, NEXT, ENT><<<a.nfeat, 256, 0, s>>>(a);
+	else k_level_lord_move<512, 2, IS_W, P, NEXT, ENT><<<a.nfeat, 512, 0, s>>>(a);
+}
+
 template <bool IS_W, int P>
 void launch_lord_move(const LevelArgs &a, hipStream_t s)
 {
 	if (a.ent) {
-		if (a.ms_next) k_level_lord_move<256, IS_W, P, true, true><<<a.nfeat, 256, 0, s>>>(a);
-		else k_level_lord_move<256, IS_W, P, false, true><<<a.nfeat, 256, 0, s>>>(a);
+		if (a.ms_next) launch_lord_move_shape<IS_W, P, true, true>(a, s);
+		else launch_lord_move_shape<IS_W, P, false, true>(a, s);
 		return;
 	}
-	if (a.ms_next) k_level_lord_move<256, IS_W, P, true><<<a.nfeat, 256, 0, s>>>(a);
-	else k_level_lord_move<256, IS_W, P, false><<<a.nfeat, 256, 0, s>>>(a);
+	if (a.ms_next) launch_lord_move_shape<IS_W, P, true, false>(a, s);
+	else launch_lord_move_shape<IS_W, P, false, false>(a, s);
+}
+
+template <bool IS_W, int P>
+void launch_lord_stats(const LevelArgs &a, hipStream_t s)
+{
+	if (a.avg_len <= shape_small_max()) k_level_lord_stats<64, 2, IS_W, P><<<a.nfeat, 64, 0, s>>>(a);
+	else if (a.avg_len <= 320) k_level_lord_stats<256, 1, IS_W, P><<<a.nfeat, 256, 0, s>>>(a);
+	else if (a.avg_len <= 640) k_level_lord_stats<256, 2, IS_W, P><<<a.nfeat, 256, 0, s>>>(a);
+	else k_level_lord_stats<512, 2, IS_W, P><<<a.nfeat, 512, 0, s>>>(a);
 }
 
 
@@ -1072,9 +1094,19 @@ __global__ __launch_bounds__(BLOCK) void k_lord_defer(LevelArgs a)
 			dsts[i] = ENT ? q[u].y & ~ENT_FIRST : q[u].y;
 		}
 		__syncthreads();
-		for (uint32_t t = threadIdx.x; t < m * 4; t += BLOCK) {
-			const uint32_t i = t >> 2, c = t & 3;
-			put_piece<ENT>(d, (size_t)dsts[i] * 4 + c, recs[lslot(i, c)]);
+		// non-temporal record stores (pending bit 2; always on the entry store): with non-temporal
+		// loads too the moved records no longer push the posterior table out of L2
+		// (tools/probe_defer8.hip: the gather's cost 43 -> 23 us per level at one N = 8 rank's shape)
+		if (ENT || (a.pending & 4)) {
+			for (uint32_t t = threadIdx.x; t < m * 4; t += BLOCK) {
+				const uint32_t i = t >> 2, c = t & 3;
+				put_piece<true>(d, (size_t)dsts[i] * 4 + c, recs[lslot(i, c)]);
+			}
+		} else {
+			for (uint32_t t = threadIdx.x; t < m * 4; t += BLOCK) {
+				const uint32_t i = t >> 2, c = t & 3;
+				put_piece<false>(d, (size_t)dsts[i] * 4 + c, recs[lslot(i, c)]);
+			}
 		}
 	}
 	block_sum2<BLOCK>(s1, s2, lds);
@@ -1383,9 +1415,16 @@ __global__ __launch_bounds__(BLOCK) void k_mc_lord_defer(McArgs a)
 			dsts[i] = q[u].y;
 		}
 		__syncthreads();
-		for (uint32_t tt = threadIdx.x; tt < m * 4; tt += BLOCK) {
-			const uint32_t i = tt >> 2, c = tt & 3;
-			d[(size_t)dsts[i] * 4 + c] = recs[lslot(i, c)];
+		if (a.pending & 4) {   // non-temporal record stores (as k_lord_defer)
+			for (uint32_t tt = threadIdx.x; tt < m * 4; tt += BLOCK) {
+				const uint32_t i = tt >> 2, c = tt & 3;
+				put_piece<true>(d, (size_t)dsts[i] * 4 + c, recs[lslot(i, c)]);
+			}
+		} else {
+			for (uint32_t tt = threadIdx.x; tt < m * 4; tt += BLOCK) {
+				const uint32_t i = tt >> 2, c = tt & 3;
+				d[(size_t)dsts[i] * 4 + c] = recs[lslot(i, c)];
+			}
 		}
 	}
 	block_sum2<BLOCK>(sm, ss, lds);
@@ -1558,9 +1597,9 @@ hipError_t lord_long(const LevelArgs &a, int is_w, hipStream_t s)
 hipError_t lord_level_stats(const LevelArgs &a, int is_w, hipStream_t s)
 {
 	if (a.nfeat == 0) return hipSuccess;
-	if (is_w) k_level_lord_stats<256, true, 0><<<a.nfeat, 256, 0, s>>>(a);
-	else if (a.slot == 0) k_level_lord_stats<256, false, 0><<<a.nfeat, 256, 0, s>>>(a);
-	else k_level_lord_stats<256, false, 1><<<a.nfeat, 256, 0, s>>>(a);
+	if (is_w) launch_lord_stats<true, 0>(a, s);
+	else if (a.slot == 0) launch_lord_stats<false, 0>(a, s);
+	else launch_lord_stats<false, 1>(a, s);
 	return hipGetLastError();
 }
 

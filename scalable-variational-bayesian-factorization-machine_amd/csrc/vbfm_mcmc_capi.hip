@@ -347,7 +347,7 @@ void mc_sweep(vbfm_ctx *c, bool is_w, int f)
 				a.lpay = c->lpay;
 				a.lpay2 = c->lpay2;
 				a.tab = c->post_tab;
-				a.pending = l > 0 ? 3 : 0;
+				a.pending = (l > 0 ? 3 : 0) | (defer_nt_stores() ? 4 : 0);
 				stats_exchange(c, a, [&](const McArgs &b) { HIPCHK(vbk::mc_lord_defer_level(b, is_w, c->s)); });
 				HIPCHK(vbk::mc_lord_defer_post(a, is_w, c->s));
 				if (l + 1 == nlevels(c)) {   // the sweep's last correction, on level-0-ordered records

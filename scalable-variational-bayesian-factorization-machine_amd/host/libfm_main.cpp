@@ -151,6 +151,7 @@ public:
 		line = std::string("\"method\": \"") + method + "\"";
 		num("iter", (double)it);
 	}
+	void str(const char *key, const char *v) { line += std::string(", \"") + key + "\": \"" + v + "\""; }
 	void num(const char *key, double v)
 	{
 		char b[48];
@@ -175,6 +176,39 @@ private:
 	FILE *f = nullptr;
 	std::string line;
 };
+
+// host wall seconds of the train and test loads (Data::load, libfm.cpp:149-171), for -parity_log
+static double g_load_s = 0;
+
+static double wall_now()
+{
+	struct timespec ts;
+	clock_gettime(CLOCK_MONOTONIC, &ts);
+	return (double)ts.tv_sec + ts.tv_nsec * 1e-9;
+}
+
+void check(int rc, vbfm_ctx *ctx);
+
+// -parity_log's first line: what setting the train set up cost (vbfm_setup_info): the load, the
+// hand-over to the device, the dependency levels, the row store and its placement search
+static void plog_setup(ParityLog &plog, vbfm_ctx *ctx, const char *method)
+{
+	if (!plog.on()) return;
+	vbfm_setup_stats su;
+	check(vbfm_setup_info(ctx, &su), ctx);
+	plog.begin("setup", 0);
+	plog.str("learner", method);
+	plog.num("load_s", g_load_s);
+	plog.num("set_train_s", su.s_set_train);
+	plog.num("schedule_s", su.s_schedule);
+	plog.num("store_s", su.s_store);
+	plog.num("placement_s", su.s_placement);
+	plog.num("placement_bytes", (double)su.place_bytes);
+	plog.num("placement_candidates", su.place_candidates);
+	plog.num("placement_kept_0", su.place_kept[0]);
+	plog.num("placement_kept_1", su.place_kept[1]);
+	plog.end();
+}
 
 double usertime()
 {
@@ -250,6 +284,10 @@ struct Rank {
 		Slice s;
 		uint32_t lo, hi;
 		range(h.num_rows, &lo, &hi);
+		if (lo == 0 && hi == h.num_rows) {   // every row: the loaded arrays themselves (no copy of nnz entries)
+			s.csc = vbfm_csc{h.num_rows, h.num_feature, h.nnz, h.col_ptr, h.col_ent, h.target};
+			return s;
+		}
 		s.cp.assign((size_t)h.num_feature + 1, 0);
 		auto run = [&](uint32_t j, const vbfm_entry **a, const vbfm_entry **z) {
 			const vbfm_entry *b = h.col_ent + h.col_ptr[j], *e = h.col_ent + h.col_ptr[j + 1];
@@ -418,6 +456,7 @@ static void run_mcmc(const McmcRun &r, Data &train, Data &test, const Rank &rk)
 		const std::string f_rmse = "test_rmse_" + tag.str() + "_mcmc";
 		if (rk.lead() && !resume) { std::ofstream a(f_rmse.c_str()); }   // truncate (:52-62); a resumed run appends
 		ParityLog plog(r.parity_file, rk.lead());
+		plog_setup(plog, ctx, r.sample ? "mcmc" : "als");
 		for (uint32_t it = it0; it < it0 + r.num_iter; it++) {
 			const double t_user = usertime();
 			const clock_t t_clock = clock();
@@ -734,6 +773,7 @@ static void run_vb(const VbRun &r, Data &train, Data &test, const Rank &rk)
 		const std::string f_rmse = "test_rmse_" + tag.str() + "_vb", f_fe = "free_energy_" + tag.str() + "_vb";
 		if (!resume && rk.lead()) { std::ofstream a(f_rmse.c_str()); std::ofstream b(f_fe.c_str()); }   // truncate (:58-73); a resumed run appends
 		ParityLog plog(r.parity_file, rk.lead());
+		plog_setup(plog, ctx, "vb");
 		for (uint32_t it = it0; it < it0 + r.num_iter; it++) {
 			time_t now = time(0);
 			std::cout << ctime(&now) << std::endl;
@@ -1027,8 +1067,10 @@ int main(int argc, char **argv)
 		}
 
 		Data train, test;
+		const double t_load = wall_now();
 		load(cmd.get(p_train), train, "train");
 		load(cmd.get(p_test), test, "test");
+		g_load_s = wall_now() - t_load;
 		if (cmd.geti(p_verb, 0) > 0) std::cout << "seed=" << seed << std::endl;
 		if (proto.row_shards() && train.h.num_rows < (uint32_t)proto.nranks)
 			throw std::string("-devices: fewer train rows than ranks");

@@ -30,7 +30,7 @@ P_u32, P_u64, P_f32, P_f64, P_u8 = (C.POINTER(C.c_uint32), C.POINTER(C.c_uint64)
                                     C.POINTER(C.c_double), C.POINTER(C.c_uint8))
 
 
-ABI_VERSION = 2        # VBFM_ABI_VERSION of include/vbfm.h this binding is written for
+ABI_VERSION = 3        # VBFM_ABI_VERSION of include/vbfm.h this binding is written for
 LAYOUTS = {"auto": 0, "column": 1, "level": 2, "entry": 3}   # VBFM_LAYOUT_* (include/vbfm.h)
 SYNTH_MODEL_SEED = 7   # tests/synth.py MODEL_SEED: the planted model shared by train, test and all shards
 
@@ -55,7 +55,18 @@ class Config(C.Structure):
     _fields_ = [("k0", C.c_int32), ("k1", C.c_int32), ("num_factor", C.c_int32),
                 ("num_attribute", C.c_uint32), ("num_attr_groups", C.c_uint32), ("attr_group", P_u32),
                 ("min_target", C.c_float), ("max_target", C.c_float), ("device", C.c_int32),
-                ("task", C.c_int32)]
+                ("task", C.c_int32), ("place_candidates", C.c_int32), ("place_budget_bytes", C.c_uint64)]
+
+
+class SetupStats(C.Structure):
+    _fields_ = [("s_set_train", C.c_double), ("s_schedule", C.c_double), ("s_store", C.c_double),
+                ("s_placement", C.c_double), ("place_bytes", C.c_uint64), ("place_candidates", C.c_int32),
+                ("place_kept", C.c_int32 * 2)]
+
+    def as_dict(self):
+        d = {k: getattr(self, k) for k, _ in self._fields_}
+        d["place_kept"] = list(self.place_kept)
+        return d
 
 
 class Params(C.Structure):
@@ -149,7 +160,7 @@ EXPORTS = ["vbfm_abi_version", "vbfm_last_error", "vbfm_create", "vbfm_destroy",
            "vbfm_step_v_level", "vbfm_step_hyper", "vbfm_device_count",
            "vbfm_free_energy", "vbfm_get_rows", "vbfm_get_test_e", "vbfm_factor_sweep", "vbfm_set_profiling",
            "vbfm_set_layout", "vbfm_get_layout", "vbfm_set_shard_mode",
-           "vbfm_comm_unique_id", "vbfm_comm_init", "vbfm_comm_init_host", "vbfm_comm_info", "vbfm_placement_info", "vbfm_load_data", "vbfm_free_host_data", "vbfm_save_data",
+           "vbfm_comm_unique_id", "vbfm_comm_init", "vbfm_comm_init_host", "vbfm_comm_info", "vbfm_placement_info", "vbfm_setup_info", "vbfm_load_data", "vbfm_free_host_data", "vbfm_save_data",
            "vbfm_init_params_host", "vbfm_mcmc_init", "vbfm_mcmc_set_params", "vbfm_mcmc_get_params",
            "vbfm_mcmc_init_caches", "vbfm_mcmc_iterate", "vbfm_mcmc_get_test_pred", "vbfm_mcmc_factor_sweep",
            "vbfm_online_init", "vbfm_online_epoch", "vbfm_online_get_state", "vbfm_save_state", "vbfm_load_state"]
@@ -214,6 +225,7 @@ def lib():
         L.vbfm_comm_init_host.argtypes = [V, C.c_int32, C.c_int32, EXCHANGE_FN, V]
         L.vbfm_comm_info.argtypes = [V, C.POINTER(C.c_int32), C.POINTER(C.c_int32), C.POINTER(C.c_int32)]
         L.vbfm_placement_info.argtypes = [V, C.POINTER(C.c_float), C.POINTER(C.c_int32), C.POINTER(C.c_int32)]
+        L.vbfm_setup_info.argtypes = [V, C.POINTER(SetupStats)]
         L.vbfm_load_data.argtypes = [C.c_char_p, C.POINTER(HostData)]
         L.vbfm_free_host_data.argtypes = [C.POINTER(HostData)]
         L.vbfm_save_data.argtypes = [C.c_char_p, C.POINTER(HostData)]
@@ -342,12 +354,15 @@ class FMLearnVB:
     """fm_learn_vb_simultaneous on one MI355X (src/libfm/src/fm_learn_vb_simultaneous.h)."""
 
     def __init__(self, k0=1, k1=1, num_factor=8, num_attribute=0, attr_group=None,
-                 min_target=1.0, max_target=5.0, device=0, layout="auto"):
+                 min_target=1.0, max_target=5.0, device=0, layout="auto", place_candidates=0,
+                 place_budget_bytes=0):
         self.k0, self.k1, self.k, self.D = int(bool(k0)), int(bool(k1)), int(num_factor), int(num_attribute)
         self.attr_group = None if attr_group is None else np.ascontiguousarray(attr_group, dtype=np.uint32)
         self.G = 1 if self.attr_group is None else int(self.attr_group.max()) + 1 if self.D else 1
+        # place_candidates / place_budget_bytes: the store's record-buffer placement search
+        # (include/vbfm.h vbfm_config; 0 = the library's defaults, place_candidates=1: no search)
         cfg = Config(self.k0, self.k1, self.k, self.D, self.G, _ptr(self.attr_group, P_u32),
-                     min_target, max_target, device, 0)
+                     min_target, max_target, device, 0, int(place_candidates), int(place_budget_bytes))
         self._ctx = C.c_void_p()
         _check(lib().vbfm_create(C.byref(self._ctx), C.byref(cfg)))
         _check(lib().vbfm_set_layout(self._ctx, LAYOUTS[layout]), self._ctx)
@@ -422,6 +437,12 @@ class FMLearnVB:
         return p
 
     # -- data ---------------------------------------------------------------------------
+    def set_train(self, train):
+        """vbfm_set_train alone: the train set from host memory (DataSubset)."""
+        self._train_csc = train._csc()
+        _check(lib().vbfm_set_train(self._ctx, C.byref(self._train_csc)), self._ctx)
+        self.n_train = train.num_cases
+
     def set_data(self, train, test):
         self._train_csc, self._test_csc = train._csc(), test._csc()
         _check(lib().vbfm_set_train(self._ctx, C.byref(self._train_csc)), self._ctx)
@@ -607,6 +628,14 @@ class FMLearnVB:
         n, k = C.c_int32(cap), (C.c_int32 * 2)()
         _check(lib().vbfm_placement_info(self._ctx, buf, C.byref(n), k), self._ctx)
         return [float(buf[i]) for i in range(min(n.value, cap))], [k[0], k[1]]
+
+    def setup_info(self):
+        """What setting up the train set cost (vbfm_setup_info): host seconds of the train set's
+        hand-over, of the dependency levels and of the row store (the placement search included),
+        and the search's peak device memory, candidates and kept pair."""
+        st = SetupStats()
+        _check(lib().vbfm_setup_info(self._ctx, C.byref(st)), self._ctx)
+        return st.as_dict()
 
     def close(self):
         if self._ctx:

@@ -56,6 +56,12 @@ int vbfm_create(vbfm_ctx **out, const vbfm_config *cfg)
 	return 0;
 }
 void vbfm_destroy(vbfm_ctx *c) { delete c; }
+int vbfm_setup_info(vbfm_ctx *, vbfm_setup_stats *o)
+{
+	memset(o, 0, sizeof(*o));
+	o->place_kept[0] = o->place_kept[1] = -1;
+	return 0;
+}
 int vbfm_set_shard_mode(vbfm_ctx *, int32_t, int32_t) { return 0; }
 int vbfm_comm_unique_id(uint8_t *) { return fail(nullptr, "no RCCL in the sanitizer build"); }
 int vbfm_comm_init(vbfm_ctx *c, int32_t, int32_t, const uint8_t *) { return fail(c, "no RCCL in the sanitizer build"); }

@@ -410,3 +410,26 @@ def test_online_checkpoint_refuses_other_store(tmp_path, monkeypatch):
             c.load_state(paths[other])
         assert c.load_state(paths[layout]) == 1
         c.close()
+
+
+def test_online_checkpoint_of_older_library_refused(tmp_path, monkeypatch):
+    """online checkpoints written before the layout word recorded the per-batch store
+    carry COLUMN whichever store ran; such a file (header flags word 0, as every older libvbfm
+    wrote it) is refused with a message naming its origin, not as "another row layout"."""
+    monkeypatch.delenv("VBFM_LAYOUT", raising=False)
+    tr, te, nf = _data(n=20000)
+    a = _ov_learner(tr, te, nf, 4)
+    a.epoch()
+    path = str(tmp_path / "ov.state")
+    a.save_state(path)
+    a.close()
+    raw = bytearray(open(path, "rb").read())
+    assert raw[80:88] == (1).to_bytes(8, "little")        # StateHeader::flags = STATE_FLAG_OV_LAYOUT
+    raw[80:88] = bytes(8)                                   # an older library's header
+    legacy = str(tmp_path / "ov_legacy.state")
+    open(legacy, "wb").write(bytes(raw))
+    c = _ov_learner(tr, te, nf, 4)
+    with pytest.raises(vbfm.VbfmError, match="older libvbfm"):
+        c.load_state(legacy)
+    assert c.load_state(path) == 1
+    c.close()

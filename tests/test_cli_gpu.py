@@ -192,6 +192,9 @@ def test_cli_parity_log_17_digits(case, tmp_path):
     run_cli(tmp_path, os.path.join(d, "train.libfm"), os.path.join(d, "test.libfm"), m["dim"], m["iter"], m["seed"],
             ["-init_stdev", str(m["init_stdev"]), "-parity_log", "parity.jsonl", "-vfile", "0"], method=method)
     lines = [json.loads(x) for x in open(tmp_path / "parity.jsonl")]
+    setup, lines = lines[0], lines[1:]            # the first line: what the set-up cost (vbfm_setup_info)
+    assert setup["method"] == "setup" and setup["learner"] == method and setup["schedule_s"] > 0
+    assert setup["placement_candidates"] == 0     # tiny data: no placement search
     assert len(lines) == m["iter"]
     for it, (got, ref) in enumerate(zip(lines, t["trace"])):
         assert got["iter"] == it and got["method"] == method
@@ -225,3 +228,63 @@ def test_cli_parity_log_online(tmp_path):
         for a, b in pairs:
             assert abs(a - b) <= 1e-9 * abs(b), (it, a, b)
         assert got["ms_v"] > 0 and got["sweep_nnz_k_per_s"] > 0
+
+
+def write_synth_binary(base, which_rows, F, S, seed, xmode, model_seed):
+    """One data set of the BASELINE configs' generator (tests/synth.py, generated on the device,
+    copied back) in the reference's binary format (<base>.x/.xt/.y, fmatrix.h:46-52), as the
+    reference's own Data::load reads it (Data.h:112-171)."""
+    import synth
+    import vbfm
+    g = vbfm.FMLearnVB(1, 1, 1, F * S + 1, min_target=1.0, max_target=5.0)
+    g.synth(0, which_rows, F, S, seed, xmode, model_seed)
+    cp, ent, y = g.get_csc(0)
+    g.close()
+    crow, cval = ent["id"], ent["value"]
+    del ent
+    rp, feat, val = synth.field_csr_from_csc(which_rows, F, S, cp, crow, cval)
+    synth.write_binary_csc(base, F * S, rp, feat, val, y, cp, crow, cval)
+
+
+def test_cli_c3_k50_binary_files_vs_reference(tmp_path):
+    """The drop-in CLI at a BASELINE configuration's own size: C3 -- 1e7 rows x
+    40 fields x 25,000 ids (nnz 4e8, real-valued x), k = 50 -- written in the reference's binary
+    format and run through bin/libFM -method vb -dim 1,1,50 -iter 2 -seed 3 exactly as the
+    reference's CLI would be (libfm.cpp:149-171 load, 215 num_all_attribute, 306-311 method; the
+    fixture tests/golden/c3_k50 is the reference's fm_learn_vb_simultaneous run on the same data and
+    seed). The -parity_log lines (17 digits) match the reference's trace within 1e-9 relative; the
+    reference-format files test_rmse_1150_vb / free_energy_1150_vb and the #Iter= lines match its
+    6-digit output; the setup line reports the load, hand-over, schedule and store times."""
+    import json
+    t, _ = load_case("c3_k50")
+    m = t["meta"]
+    n, F, S = m["n_rows"], m["n_fields"], m["ids_per_field"]
+    write_synth_binary(str(tmp_path / "c3_train"), n, F, S, m["seed"], m["xmode"], m["model_seed"])
+    write_synth_binary(str(tmp_path / "c3_test"), m["test_rows"], F, S, m["test_seed"], m["xmode"], m["model_seed"])
+    stdout = run_cli(tmp_path, str(tmp_path / "c3_train"), str(tmp_path / "c3_test"), m["dim"], m["iter"],
+                     m["ref_seed"], ["-init_stdev", str(m["init_stdev"]), "-parity_log", "parity.jsonl"])
+    assert "num_rows=%d\tnum_values=%d\tnum_features=%d" % (n, n * F, F * S) in stdout
+    lines = [json.loads(x) for x in open(tmp_path / "parity.jsonl")]
+    setup, its = lines[0], lines[1:]
+    assert setup["method"] == "setup" and setup["learner"] == "vb"
+    assert all(setup[kk] > 0 for kk in ("load_s", "set_train_s", "schedule_s", "store_s"))
+    print("C3 via bin/libFM: load %.2f s, hand-over %.2f s, schedule %.2f s, store %.2f s (placement %.2f s, %d "
+          "buffers); iterations %s ms" % (setup["load_s"], setup["set_train_s"], setup["schedule_s"],
+                                          setup["store_s"], setup["placement_s"], setup["placement_candidates"],
+                                          [round(x["ms_total"], 1) for x in its]))
+    assert len(its) == m["iter"]
+    for x, ref in zip(its, t["trace"]):
+        for got, key in (("train", "train"), ("test_rmse", "rmse"), ("test_mae", "mae"), ("alpha", "alpha"),
+                         ("sigma_0", "sigma_0"), ("mu_0_dash", "mu_0_dash"), ("sigma_0_dash", "sigma_0_dash"),
+                         ("free_energy", "free_energy")):
+            assert abs(x[got] - ref[key]) <= 1e-9 * abs(ref[key]), (x["iter"], got, x[got], ref[key])
+    rmse = open(tmp_path / "test_rmse_1150_vb").read().split()
+    fe = open(tmp_path / "free_energy_1150_vb").read().split()
+    iters = re.findall(r"#Iter=\s*(\d+)\tTrain=(\S+)\tTest=(\S+)", stdout)
+    assert len(rmse) == len(fe) == len(iters) == m["iter"]
+    for it, ref in enumerate(t["trace"]):
+        assert same6(rmse[it], g6(ref["rmse"])) and same6(fe[it], g6(-ref["free_energy"])), it
+        assert same6(iters[it][1], g6(ref["train"])) and same6(iters[it][2], g6(ref["rmse"])), it
+    vf = tmp_path / "v_file.txt"     # fm.v's k x D draws, as the reference always writes them
+    with open(vf) as fh:
+        assert len(fh.readline().split("\t")) == F * S + 1

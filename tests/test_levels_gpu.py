@@ -174,3 +174,20 @@ def test_per_level_steps_refuse_misuse(monkeypatch):
     with pytest.raises(vbfm.VbfmError, match="deferred"):
         d.step_v_level(0, 0)
     d.close()
+
+
+def test_failed_level_refuses_every_read_until_restart(monkeypatch):
+    """a level that fails mid-sweep may leave the records half moved; every entry point
+    that reads or sweeps them -- vbfm_get_rows included -- refuses until vbfm_set_train or
+    vbfm_load_state (VBFM_FAULT=level: the step of level 1 fails after its kernel ran)."""
+    g = _learner("tiny", "auto")
+    g.init_caches()
+    g.step_v_level(0, 0)
+    monkeypatch.setenv("VBFM_FAULT", "level")
+    with pytest.raises(vbfm.VbfmError, match="VBFM_FAULT=level"):
+        g.step_v_level(0, 1)
+    monkeypatch.delenv("VBFM_FAULT")
+    for call in (g.rows, g.iterate, g.step_w0, lambda: g.step_v_level(0, 0)):
+        with pytest.raises(vbfm.VbfmError, match="failed"):
+            call()
+    g.close()

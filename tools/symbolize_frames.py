@@ -9,7 +9,8 @@ just after call instructions of a candidate library is reported, with the functi
 falls in (objdump's symbol for the enclosing function).
 
 usage: tools/symbolize_frames.py <group: addr,addr,...> [<group> ...] -- <library> [<library> ...]
-A group prefixed with `pc:` is a faulting PC (an instruction boundary, not a return address).
+A group prefixed with `pc:` is a faulting PC (an instruction boundary, not a return address); inside a
+group of return addresses one address may carry `pc:` itself (the PC with the frames near it).
 """
 import bisect
 import re
@@ -57,17 +58,20 @@ def main():
         rset, iset = set(rets), set(insns)
         for grp in groups:
             is_pc = grp.startswith("pc:")
-            addrs = [int(x, 16) for x in grp[3 if is_pc else 0:].split(",")]
-            pool = insns if is_pc else rets
+            # a whole group prefixed pc: is faulting PCs; inside a group, one address prefixed pc:
+            # is the faulting PC among return addresses (mixed: the PC and the frames near it)
+            items = [x for x in grp[3 if is_pc else 0:].split(",")]
+            kinds = [is_pc or x.startswith("pc:") for x in items]
+            addrs = [int(x[3:] if x.startswith("pc:") else x, 16) for x in items]
             hits = []
-            a0 = addrs[0]
-            for r in pool:
+            a0, k0 = addrs[0], kinds[0]
+            for r in (insns if k0 else rets):
                 if (r & 0xFFF) != (a0 & 0xFFF):
                     continue
                 base = a0 - r
                 if base & 0xFFF:
                     continue
-                ok = all(((a - base) in (iset if is_pc else rset)) for a in addrs)
+                ok = all(((a - base) in (iset if k else rset)) for a, k in zip(addrs, kinds))
                 if ok:
                     hits.append(base)
             label = ("pc " if is_pc else "") + ",".join(hex(a) for a in addrs)
