@@ -915,10 +915,16 @@ void launch_wave(const LevelArgs &a, hipStream_t s)
 	else g4 ? launch_wave_g<4, 4, IS_W, P, NEXT>(a, s) : launch_wave_g<8, 4, IS_W, P, NEXT>(a, s);
 }
 
+// the wave kernels address a column's run through 32-bit buffer descriptors (num_records = run x
+// 64 B, soffset = chunk base x 64 B): a level whose longest column has 2^25 records or more (a
+// skewed shard) keeps the workgroup kernels
+constexpr uint32_t WAVE_MAX_RUN = (1u << 25) - 1;
+
 template <bool IS_W, int P, bool NEXT>
 void launch_lord(const LevelArgs &a, hipStream_t s)
 {
-	if (!a.ent && wave_mode() && a.avg_len > shape_small_max() && a.avg_len <= 640) return launch_wave<IS_W, P, NEXT>(a, s);
+	if (!a.ent && wave_mode() && a.avg_len > shape_small_max() && a.avg_len <= 640 && a.max_len <= WAVE_MAX_RUN)
+		return launch_wave<IS_W, P, NEXT>(a, s);
 	if (a.ent) {
 		if (a.avg_len <= shape_small_max()) k_level_lord<64, 2, IS_W, P, NEXT, true><<<a.nfeat, 64, 0, s>>>(a);
 		else if (a.avg_len <= 320) k_level_lord<256, 1, IS_W, P, NEXT, true><<<a.nfeat, 256, 0, s>>>(a);
@@ -1287,7 +1293,7 @@ template <bool IS_W, int P, bool NEXT, int PK, bool ENT>
 void launch_defer_shape(const LevelArgs &a, hipStream_t s)
 {
 	if constexpr (!ENT) {
-		if (wave_mode() && a.avg_len > shape_small_max() && a.avg_len <= 640) {   // k_defer_wave (256 shapes)
+		if (wave_mode() && a.avg_len > shape_small_max() && a.avg_len <= 640 && a.max_len <= WAVE_MAX_RUN) {   // k_defer_wave (256 shapes)
 			const unsigned wpb = wave_wpb(), gr = (a.nfeat + wpb - 1) / wpb;
 			if (a.lpay2) {
 				if (wpb == 1) k_defer_wave<256, 4, 1, IS_W, P, NEXT, PK, true><<<gr, 64, 0, s>>>(a);

@@ -4,10 +4,13 @@ kernel it replaces on 256-thread levels (k_level_lord<256, R>, VBFM_WAVE=0): bit
 The wave kernel keeps a column's run in registers and reproduces k_level_lord's reduction tree
 (virtual thread i mod 256, virtual waves added in order) on permuted lanes, so the column
 statistics, posteriors, corrections and moves must be identical, not merely close. Cases cover
-the register-resident path (G = 4 groups for ~100-entry columns, G = 8 for ~400), runs longer
-than the registers hold (~600 entries: statistics and move chunk by chunk), x stored or not
-(one-hot), both workgroup packings (VBFM_WAVE_WPB 1 / 4), the deferred split (which keeps the
-workgroup kernels: fused wave == split), and the oracle at 1e-9 (fm_learn_vb.h:577-644)."""
+the register-resident path (G = 4 groups for ~160-entry columns, G = 8 for ~400; columns of up to
+128 entries take the 64 x 2 workgroup shape, shape_small_max), runs longer than the registers hold
+(~600 entries: statistics and move chunk by chunk), x stored or not (one-hot), both workgroup
+packings (VBFM_WAVE_WPB 1 / 4), the deferred split (VBFM_FORCE_SPLIT with VBFM_WAVE=1 runs its
+wave form, k_defer_wave, against the fused workgroup kernel), the two-pass split (VBFM_DEFER=0:
+the workgroup statistics / move kernels against the fused wave kernel), and the oracle at 1e-9
+(fm_learn_vb.h:577-644)."""
 import numpy as np
 import pytest
 
@@ -19,7 +22,7 @@ pytestmark = pytest.mark.gpu
 
 
 def _run(n, F, S, k, xmode, seed, env, monkeypatch, iters=2):
-    for kk in ("VBFM_WAVE", "VBFM_WAVE_WPB", "VBFM_FORCE_SPLIT", "VBFM_LAYOUT"):
+    for kk in ("VBFM_WAVE", "VBFM_WAVE_WPB", "VBFM_FORCE_SPLIT", "VBFM_LAYOUT", "VBFM_DEFER"):
         monkeypatch.delenv(kk, raising=False)
     for kk, vv in env.items():
         monkeypatch.setenv(kk, vv)
@@ -46,17 +49,18 @@ def _same(a, b):
 
 
 # (rows, fields, ids per field): mean column length rows / ids
-SHAPES = [(40000, 4, 400), (80000, 4, 200), (120000, 3, 200)]
+SHAPES = [(64000, 4, 400), (80000, 4, 200), (120000, 3, 200)]
 
 
 @pytest.mark.parametrize("xmode", [0, 1])
-@pytest.mark.parametrize("shape", SHAPES, ids=["len100", "len400", "len600"])
+@pytest.mark.parametrize("shape", SHAPES, ids=["len160", "len400", "len600"])
 def test_wave_kernel_equals_workgroup_kernel(shape, xmode, monkeypatch):
     n, F, S = shape
     k = 3
     ref, _ = _run(n, F, S, k, xmode, 31, {"VBFM_WAVE": "0"}, monkeypatch)
     for env in ({"VBFM_WAVE": "1"}, {"VBFM_WAVE": "1", "VBFM_WAVE_WPB": "1"},
-                {"VBFM_WAVE": "1", "VBFM_FORCE_SPLIT": "1"}):
+                {"VBFM_WAVE": "1", "VBFM_FORCE_SPLIT": "1"},
+                {"VBFM_WAVE": "1", "VBFM_FORCE_SPLIT": "1", "VBFM_DEFER": "0"}):
         got, _ = _run(n, F, S, k, xmode, 31, env, monkeypatch)
         _same(got, ref)
 
