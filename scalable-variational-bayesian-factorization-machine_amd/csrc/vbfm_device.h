@@ -74,6 +74,9 @@ struct LongSeg {
 };
 
 struct LevelArgs {
+#ifdef VBFM_OV_STAMPS
+	unsigned long long *stamp;   // diagnostic build only (tools/ov_stamps.sh): per-workgroup phase stamps
+#endif
 	const uint64_t *col_ptr;
 	const uint2 *csc;
 	const uint32_t *feats;     // features of this level (ascending id)

@@ -490,6 +490,18 @@ __global__ void k_ov_pad_check(const uint64_t *gptr, const uint32_t *lptr, const
 // are read and written directly.
 constexpr uint32_t OV_CAP = 512;
 
+// Diagnostic build only (tools/ov_stamps.sh, -DVBFM_OV_STAMPS; never in lib/libvbfm.so): thread 0 of
+// every workgroup of one chosen level launch writes the 100-MHz real-time counter at five points
+// (entry, staged, posterior, corrected, stores issued) to a buffer of its own
+#ifdef VBFM_OV_STAMPS
+#define OV_STAMP(i)                                                                                    \
+	do {                                                                                               \
+		if (a.stamp && threadIdx.x == 0) a.stamp[(size_t)blockIdx.x * 5 + (i)] = __builtin_amdgcn_s_memrealtime(); \
+	} while (0)
+#else
+#define OV_STAMP(i) do {} while (0)
+#endif
+
 DEVI uint32_t ov_slot(uint32_t i, uint32_t c) { return i * 4 + (c ^ ((i >> 2) & 3)); }
 
 template <int G, bool IS_W, int P, bool NEXT, bool PAD>
@@ -498,6 +510,7 @@ __global__ __launch_bounds__(256) void k_ov_lord(LevelArgs a)
 	static_assert(G <= 64, "lane groups inside one wave");
 	__shared__ double2 stage[OV_CAP * 4];
 	__shared__ uint32_t dsts[OV_CAP];
+	OV_STAMP(0);
 	const uint32_t c0 = blockIdx.x * (256 / G);
 	const uint32_t c1 = min(c0 + 256 / G, a.nfeat);
 	const uint64_t wb = a.col_ptr[c0], we = a.col_ptr[c1];
@@ -589,6 +602,7 @@ __global__ __launch_bounds__(256) void k_ov_lord(LevelArgs a)
 #pragma unroll
 	for (int k = 0; k < KD; ++k) dsts[threadIdx.x + k * 256] = dv[k];
 	__syncthreads();
+	OV_STAMP(1);
 	auto get = [&](uint32_t i, Rec &r) {
 		const uint32_t o = o0 + i;
 		if (o < m) {
@@ -655,6 +669,7 @@ __global__ __launch_bounds__(256) void k_ov_lord(LevelArgs a)
 			}
 		}
 	}
+	OV_STAMP(2);
 	for (uint32_t i = lane, it = 0; i < n; i += G, ++it) {
 		Rec r;
 		get(i, r);
@@ -670,6 +685,7 @@ __global__ __launch_bounds__(256) void k_ov_lord(LevelArgs a)
 		}
 	}
 	__syncthreads();
+	OV_STAMP(3);
 	// non-temporal stores: v sweep 1129 -> 1086 ms per C3 epoch (profiles/probes/ab_online_nt_store.txt;
 	// write-through stores were 8 % slower, ab_write_through.txt)
 	typedef double ntv2 __attribute__((ext_vector_type(2)));
@@ -681,6 +697,7 @@ __global__ __launch_bounds__(256) void k_ov_lord(LevelArgs a)
 		w.y = v.y;
 		__builtin_nontemporal_store(w, d + (size_t)dsts[t >> 2] * 4 + (t & 3));
 	}
+	OV_STAMP(4);
 }
 
 inline unsigned grid_of(uint64_t n, unsigned block = 256) { return (unsigned)((n + block - 1) / block); }
@@ -904,7 +921,34 @@ void ov_launch_level(vbfm_ctx *c, LevelArgs &a, uint32_t l, bool is_w)
 		a.first_level = -1;
 		a.x_one = 0;
 	}
+#ifdef VBFM_OV_STAMPS
+	// VBFM_OV_STAMP=<n>: the n-th v-level launch of the process (and every 1000th after it) stamps
+	// its workgroups; the stamps go to stderr as one line per workgroup after the launch
+	static long launch_no = 0;
+	static const long want = [] { const char *e = getenv("VBFM_OV_STAMP"); return e ? atol(e) : -1L; }();
+	unsigned long long *st = nullptr;
+	const unsigned nwg = (a.nfeat + 31) / 32 + 4096;
+	if (!is_w && want >= 0 && launch_no >= want && (launch_no - want) % 1000 == 0) {
+		HIPCHK(hipMalloc(&st, (size_t)nwg * 5 * 8 * 8));
+		HIPCHK(hipMemsetAsync(st, 0, (size_t)nwg * 5 * 8 * 8, c->s));
+	}
+	a.stamp = st;
+	if (!is_w) launch_no++;
 	HIPCHK(vbk::ov_lord_level(a, is_w, c->s));
+	if (st) {
+		std::vector<unsigned long long> h((size_t)nwg * 5 * 8);
+		HIPCHK(hipMemcpyAsync(h.data(), st, h.size() * 8, hipMemcpyDeviceToHost, c->s));
+		sync(c);
+		(void)hipFree(st);
+		fprintf(stderr, "OVSTAMP launch %ld nfeat %u avg %u\n", launch_no - 1, a.nfeat, a.avg_len);
+		for (size_t w = 0; w * 5 < h.size() && h[w * 5] != 0; w++)
+			fprintf(stderr, "OVSTAMP %zu %llu %llu %llu %llu %llu\n", w, h[w * 5], h[w * 5 + 1], h[w * 5 + 2],
+			        h[w * 5 + 3], h[w * 5 + 4]);
+	}
+	a.stamp = nullptr;
+#else
+	HIPCHK(vbk::ov_lord_level(a, is_w, c->s));
+#endif
 	std::swap(c->rows, o.rows_other);
 }
 
