@@ -504,16 +504,22 @@ constexpr uint32_t OV_CAP = 512;
 
 DEVI uint32_t ov_slot(uint32_t i, uint32_t c) { return i * 4 + (c ^ ((i >> 2) & 3)); }
 
+// The pointers a workgroup's first loads need come as leading scalar arguments: with
+// -amdgpu-kernarg-preload-count (Makefile) the dispatcher preloads them into SGPRs, so the run's
+// record loads and the columns' parameter loads issue at wave start instead of after a scalar load
+// of the (freshly written, cold) kernarg segment; LevelArgs follows by value for the rest
 template <int G, bool IS_W, int P, bool NEXT, bool PAD>
-__global__ __launch_bounds__(256) void k_ov_lord(LevelArgs a)
+__global__ __launch_bounds__(256) void k_ov_lord(const uint64_t *__restrict__ col_ptr, const RowRec *src,
+                                                 const uint32_t *lnext, double2 *ms, double2 *nat, double *rho_p,
+                                                 const uint32_t *ccount, uint32_t nfeat, LevelArgs a)
 {
 	static_assert(G <= 64, "lane groups inside one wave");
 	__shared__ double2 stage[OV_CAP * 4];
 	__shared__ uint32_t dsts[OV_CAP];
 	OV_STAMP(0);
 	const uint32_t c0 = blockIdx.x * (256 / G);
-	const uint32_t c1 = min(c0 + 256 / G, a.nfeat);
-	const uint64_t wb = a.col_ptr[c0], we = a.col_ptr[c1];
+	const uint32_t c1 = min(c0 + 256 / G, nfeat);
+	const uint64_t wb = col_ptr[c0], we = col_ptr[c1];
 	const uint32_t m = (uint32_t)min<uint64_t>(we - wb, OV_CAP);
 	// the run's first record in the level's buffer: from the column bound, or (PAD) the slot
 	const uint32_t rb = PAD ? blockIdx.x * OV_CAP : (uint32_t)(wb - a.lbase);
@@ -521,10 +527,10 @@ __global__ __launch_bounds__(256) void k_ov_lord(LevelArgs a)
 	// for these only, not for the run's pieces issued in between
 	const uint32_t col_i = c0 + threadIdx.x / G;
 	const uint32_t lane = threadIdx.x % G;
-	const bool live = col_i < a.nfeat;
+	const bool live = col_i < nfeat;
 	const uint32_t j = live ? level_feat(a, col_i) : 0u;
-	const uint64_t cb = live ? a.col_ptr[col_i] : 0u;
-	const uint32_t n = live ? (uint32_t)(a.col_ptr[col_i + 1] - cb) : 0u;
+	const uint64_t cb = live ? col_ptr[col_i] : 0u;
+	const uint32_t n = live ? (uint32_t)(col_ptr[col_i + 1] - cb) : 0u;
 	// the run's pieces into registers first, only as many rounds as the run needs (uniform
 	// bound), the per-column loads below overlap them, the LDS writes come last (a load/write
 	// loop waits on every read before issuing the next)
@@ -533,8 +539,8 @@ __global__ __launch_bounds__(256) void k_ov_lord(LevelArgs a)
 	const uint32_t ks = (np + 255) / 256, kd = (m + 255) / 256;
 	double2 sv[KS];
 	uint32_t dv[KD];
-	const double2 *s2 = reinterpret_cast<const double2 *>(a.src + rb);
-	const uint32_t *nx2 = a.lnext + rb;
+	const double2 *s2 = reinterpret_cast<const double2 *>(src + rb);
+	const uint32_t *nx2 = lnext + rb;
 	if constexpr (PAD) {
 		// the slot's first KP rounds (320 records: the run is 256 +- 16 at C3's batch shape) and
 		// every next position are loaded at once; the rest only if the run is that long
@@ -584,10 +590,10 @@ __global__ __launch_bounds__(256) void k_ov_lord(LevelArgs a)
 	// (feat_contig), so these wait for nothing -- not for the column bounds (a column empty in
 	// this batch loads its parameters for nothing)
 	if (live) {
-		msj = a.ms[pi];
-		natj = a.nat[(size_t)j * a.nat_stride];
-		rho = a.rho[j];
-		cc = a.ccount[j];
+		msj = ms[pi];
+		natj = nat[(size_t)j * a.nat_stride];
+		rho = rho_p[j];
+		cc = ccount[j];
 		if (!a.hyp_uniform) hg = a.hyp[(size_t)a.attr_group[j] * a.hyp_stride];
 		if (a.tcount) tc = a.tcount[j];
 		if constexpr (NEXT) nx = a.ms_next[(size_t)j * a.ms_stride_next];
@@ -609,7 +615,7 @@ __global__ __launch_bounds__(256) void k_ov_lord(LevelArgs a)
 #pragma unroll
 			for (uint32_t c = 0; c < 4; ++c) r[c] = stage[ov_slot(o, c)];
 		} else {
-			load_rec(a.src, rb + o, r);
+			load_rec(src, rb + o, r);
 		}
 	};
 	const double mo = msj.x, so = msj.y;
@@ -658,12 +664,12 @@ __global__ __launch_bounds__(256) void k_ov_lord(LevelArgs a)
 			go = false;
 		}
 		if (leader) {
-			a.nat[(size_t)j * a.nat_stride] = make_double2(nmu, nsig);
-			a.ms[pi] = make_double2(mu, sig);
+			nat[(size_t)j * a.nat_stride] = make_double2(nmu, nsig);
+			ms[pi] = make_double2(mu, sig);
 			if constexpr (IS_W) {
 				const uint32_t t = tc + n;
 				a.tcount[j] = t;
-				a.rho[j] = pow((double)(T0 + t), -LAMDA);
+				rho_p[j] = pow((double)(T0 + t), -LAMDA);
 			} else {
 				if (a.tcount) a.tcount[j] = tc + n;
 			}
@@ -681,7 +687,7 @@ __global__ __launch_bounds__(256) void k_ov_lord(LevelArgs a)
 #pragma unroll
 			for (uint32_t c = 0; c < 4; ++c) stage[ov_slot(o, c)] = r[c];
 		} else {
-			store_rec(a.dst, a.lnext[rb + o], r);
+			store_rec(a.dst, lnext[rb + o], r);
 		}
 	}
 	__syncthreads();
@@ -729,16 +735,18 @@ void launch_ov_lord_pad(const LevelArgs &a, int is_w, hipStream_t s)
 {
 	const unsigned grid = (a.nfeat + 256 / G - 1) / (256 / G);
 	const bool nx = a.ms_next != nullptr;
+#define OV_LORD_ARGS a.col_ptr, a.src, a.lnext, a.ms, a.nat, a.rho, a.ccount, a.nfeat, a
 	if (is_w) {
-		if (nx) k_ov_lord<G, true, 0, true, PAD><<<grid, 256, 0, s>>>(a);
-		else k_ov_lord<G, true, 0, false, PAD><<<grid, 256, 0, s>>>(a);
+		if (nx) k_ov_lord<G, true, 0, true, PAD><<<grid, 256, 0, s>>>(OV_LORD_ARGS);
+		else k_ov_lord<G, true, 0, false, PAD><<<grid, 256, 0, s>>>(OV_LORD_ARGS);
 	} else if (a.slot == 0) {
-		if (nx) k_ov_lord<G, false, 0, true, PAD><<<grid, 256, 0, s>>>(a);
-		else k_ov_lord<G, false, 0, false, PAD><<<grid, 256, 0, s>>>(a);
+		if (nx) k_ov_lord<G, false, 0, true, PAD><<<grid, 256, 0, s>>>(OV_LORD_ARGS);
+		else k_ov_lord<G, false, 0, false, PAD><<<grid, 256, 0, s>>>(OV_LORD_ARGS);
 	} else {
-		if (nx) k_ov_lord<G, false, 1, true, PAD><<<grid, 256, 0, s>>>(a);
-		else k_ov_lord<G, false, 1, false, PAD><<<grid, 256, 0, s>>>(a);
+		if (nx) k_ov_lord<G, false, 1, true, PAD><<<grid, 256, 0, s>>>(OV_LORD_ARGS);
+		else k_ov_lord<G, false, 1, false, PAD><<<grid, 256, 0, s>>>(OV_LORD_ARGS);
 	}
+#undef OV_LORD_ARGS
 }
 
 template <int G>

@@ -1,13 +1,15 @@
 #!/bin/bash
-# Diagnostic build of libvbfm.so with per-workgroup phase stamps in the online level kernel
-# (k_ov_lord, -DVBFM_OV_STAMPS) into tools/ab_stamp/lib/libvbfm.so; never the product library.
-# Run: VBFM_LIB=tools/ab_stamp/lib/libvbfm.so VBFM_OV_STAMP=<launch> python bench.py --config c3 --method vb_online ...
+# Build libvbfm.so with extra / different compiler flags into <outdir>/lib for interleaved A/B
+# against the product library (VBFM_LIB=<outdir>/lib/libvbfm.so); never the product library.
+# usage: tools/build_variant.sh <outdir> [--no-preload] [extra hipcc flags...]
 set -e
 cd "$(dirname "$0")/.."
 P=scalable-variational-bayesian-factorization-machine_amd
-O=tools/ab_stamp
+O=$1; shift
+PRE="-mllvm -amdgpu-kernarg-preload-count=16"
+if [ "$1" = "--no-preload" ]; then PRE=""; shift; fi
 mkdir -p $O/build $O/lib
-F="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -Wall -Wno-unused-function -I/opt/rocm/include -mllvm -amdgpu-kernarg-preload-count=16 -DVBFM_OV_STAMPS"
+F="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -Wall -Wno-unused-function -I/opt/rocm/include $PRE $*"
 for s in vbfm_online vbfm_replay vbfm_lorder vbfm_kernels vbfm_mcmc vbfm_capi vbfm_mcmc_capi; do
   /opt/rocm/bin/hipcc $F -c $P/csrc/$s.hip -o $O/build/$s.o &
 done
