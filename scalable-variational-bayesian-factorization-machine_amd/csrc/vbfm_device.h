@@ -133,6 +133,7 @@ struct LevelArgs {
 	uint32_t pad_cap;          // online per-batch store, levels >= 1: workgroup w's run sits at record
 	                           // w * pad_cap of the level's buffer (no column-bound load before the
 	                           // run's loads); 0: runs packed (positions from the column bounds)
+	int ov_fast;               // ... and a v level may take k_ov_lord's tagged-argument form
 	int hyp_uniform;           // one attribute group: the prior is hyp0 (no per-column lookup)
 	double hyp0;
 	// long columns of the level-ordered store (fused single-rank VB sweep): columns longer than

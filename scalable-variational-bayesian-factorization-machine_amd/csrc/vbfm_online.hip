@@ -507,44 +507,52 @@ DEVI uint32_t ov_slot(uint32_t i, uint32_t c) { return i * 4 + (c ^ ((i >> 2) & 
 // The pointers a workgroup's first loads need come as leading scalar arguments: with
 // -amdgpu-kernarg-preload-count (Makefile) the dispatcher preloads them into SGPRs, so the run's
 // record loads and the columns' parameter loads issue at wave start instead of after a scalar load
-// of the (freshly written, cold) kernarg segment; LevelArgs follows by value for the rest
-template <int G, bool IS_W, int P, bool NEXT, bool PAD>
-__global__ __launch_bounds__(256) void k_ov_lord(const uint64_t *__restrict__ col_ptr, const RowRec *src,
-                                                 const uint32_t *lnext, double2 *ms, double2 *nat, double *rho_p,
-                                                 const uint32_t *ccount, uint32_t nfeat, LevelArgs a)
+// of the (freshly written, cold) kernarg segment; LevelArgs follows by value for the rest.
+//
+// FAST (v sweeps on the padded layout of field data, ov_lord_fast): only 14 argument dwords are
+// preloaded, so the two values those loads still need travel in the unused top 16 bits of the
+// 48-bit pointers -- the level's column count (col_ptr: low half, src: high half) and the stride
+// of ms (lnext) -- and ms / nat / rho / ccount arrive offset to the level's first feature. Every
+// load of the staging phase then issues at wave start: one memory round trip to the barrier
+// instead of three (kernarg -> column bounds -> records and parameters).
+constexpr uint64_t OV_PTR_MASK = (1ull << 48) - 1;
+// (through a global-address-space pointer: the loads stay global_load, not flat)
+template <class T> DEVI T *ov_untag(T *p)
+{
+	typedef __attribute__((address_space(1))) T gT;
+	return (T *)reinterpret_cast<gT *>(reinterpret_cast<uintptr_t>(p) & OV_PTR_MASK);
+}
+template <class T> DEVI uint32_t ov_tag(T *p) { return (uint32_t)(reinterpret_cast<uintptr_t>(p) >> 48); }
+
+template <int G, bool IS_W, int P, bool NEXT, bool PAD, bool FAST>
+__global__ __launch_bounds__(256) void k_ov_lord(const uint64_t *__restrict__ col_ptr_t, const RowRec *src_t,
+                                                 const uint32_t *lnext_t, double2 *ms, double2 *nat, double *rho_p,
+                                                 const uint32_t *ccount, uint32_t nfeat_arg, LevelArgs a)
 {
 	static_assert(G <= 64, "lane groups inside one wave");
+	static_assert(!FAST || (PAD && !IS_W), "the tagged arguments serve the v sweep's padded levels");
 	__shared__ double2 stage[OV_CAP * 4];
 	__shared__ uint32_t dsts[OV_CAP];
 	OV_STAMP(0);
-	const uint32_t c0 = blockIdx.x * (256 / G);
-	const uint32_t c1 = min(c0 + 256 / G, nfeat);
-	const uint64_t wb = col_ptr[c0], we = col_ptr[c1];
-	const uint32_t m = (uint32_t)min<uint64_t>(we - wb, OV_CAP);
-	// the run's first record in the level's buffer: from the column bound, or (PAD) the slot
-	const uint32_t rb = PAD ? blockIdx.x * OV_CAP : (uint32_t)(wb - a.lbase);
-	// the column's id and bounds first: the per-column loads that depend on them then wait
-	// for these only, not for the run's pieces issued in between
-	const uint32_t col_i = c0 + threadIdx.x / G;
-	const uint32_t lane = threadIdx.x % G;
-	const bool live = col_i < nfeat;
-	const uint32_t j = live ? level_feat(a, col_i) : 0u;
-	const uint64_t cb = live ? col_ptr[col_i] : 0u;
-	const uint32_t n = live ? (uint32_t)(col_ptr[col_i + 1] - cb) : 0u;
+	const uint64_t *col_ptr = FAST ? ov_untag(col_ptr_t) : col_ptr_t;
+	const RowRec *src = FAST ? ov_untag(src_t) : src_t;
+	const uint32_t *lnext = FAST ? ov_untag(lnext_t) : lnext_t;
+	const uint32_t nfeat = FAST ? ov_tag(col_ptr_t) | ov_tag(src_t) << 16 : nfeat_arg;
+	const uint32_t ms_stride = FAST ? ov_tag(lnext_t) : a.ms_stride;
+	const uint32_t nat_stride = FAST ? 1u : a.nat_stride;   // FAST: factor-major nat (ov_lord_fast checks)
 	// the run's pieces into registers first, only as many rounds as the run needs (uniform
 	// bound), the per-column loads below overlap them, the LDS writes come last (a load/write
 	// loop waits on every read before issuing the next)
 	constexpr int KS = OV_CAP * 4 / 256, KD = OV_CAP / 256;
-	const uint32_t np = m * 4;
-	const uint32_t ks = (np + 255) / 256, kd = (m + 255) / 256;
+	// the slot's first KP rounds (320 records: the run is 256 +- 16 at C3's batch shape) and every
+	// next position are loaded at once (PAD: before anything else); the rest only if the run is
+	// that long
+	constexpr int KP = 5;
 	double2 sv[KS];
 	uint32_t dv[KD];
-	const double2 *s2 = reinterpret_cast<const double2 *>(src + rb);
-	const uint32_t *nx2 = lnext + rb;
 	if constexpr (PAD) {
-		// the slot's first KP rounds (320 records: the run is 256 +- 16 at C3's batch shape) and
-		// every next position are loaded at once; the rest only if the run is that long
-		constexpr int KP = 5;
+		const double2 *s2 = reinterpret_cast<const double2 *>(src + blockIdx.x * OV_CAP);
+		const uint32_t *nx2 = lnext + blockIdx.x * OV_CAP;
 #pragma unroll
 		for (int k = 0; k < KS; ++k) {
 			sv[k] = make_double2(0.0, 0.0);
@@ -552,6 +560,49 @@ __global__ __launch_bounds__(256) void k_ov_lord(const uint64_t *__restrict__ co
 		}
 #pragma unroll
 		for (int k = 0; k < KD; ++k) dv[k] = nx2[threadIdx.x + k * 256];
+	}
+	const uint32_t c0 = blockIdx.x * (256 / G);
+	const uint32_t c1 = min(c0 + 256 / G, nfeat);
+	const uint64_t wb = col_ptr[c0], we = col_ptr[c1];
+	// the column's id and bounds (a dead lane of the level's last workgroup loads its first
+	// column's: no branch around the loads)
+	const uint32_t col_i = c0 + threadIdx.x / G;
+	const uint32_t lane = threadIdx.x % G;
+	const bool live = col_i < nfeat;
+	const uint32_t ci = live ? col_i : c0;
+	const uint32_t j = FAST ? a.feat_base + ci : level_feat(a, ci);   // the feature id
+	const uint32_t pj = FAST ? ci : j;                                   // its index into ms / nat / rho / ccount
+	const uint64_t cb = col_ptr[ci];
+	const uint64_t ce = col_ptr[ci + 1];
+	double2 msj, natj, nx = make_double2(0.0, 0.0);
+	double rho;
+	uint32_t cc;
+	const size_t pi = (size_t)pj * ms_stride;
+	// every per-column load issued at once: on field data the feature id is arithmetic
+	// (feat_contig), so these wait for nothing -- not for the column bounds (a column empty in
+	// this batch loads its parameters for nothing)
+	msj = ms[pi];
+	natj = nat[(size_t)pj * nat_stride];
+	rho = rho_p[pj];
+	cc = ccount[pj];
+	if constexpr (NEXT) nx = FAST ? ms[pi + 1] : a.ms_next[(size_t)j * a.ms_stride_next];
+	if constexpr (FAST) {
+		// the LevelArgs fields the rest of the workgroup reads, fetched here in one batch while the
+		// loads above are in flight (left to itself the compiler fetches them in two more batches,
+		// each a round trip after the previous wait); the empty asm only pins them to this point
+		asm volatile("; k_ov_lord: LevelArgs fields" ::"s"(a.x_one), "s"(a.first_level), "s"(a.first_mask), "s"(a.csc),
+		             "s"(a.hyp_uniform), "s"(a.hyp0), "s"(a.alpha), "s"(a.tcount), "s"(a.counters), "s"(a.dst),
+		             "s"(a.feat_base));
+	}
+	const uint32_t n = live ? (uint32_t)(ce - cb) : 0u;
+	const uint32_t m = (uint32_t)min<uint64_t>(we - wb, OV_CAP);
+	// the run's first record in the level's buffer: from the column bound, or (PAD) the slot
+	const uint32_t rb = PAD ? blockIdx.x * OV_CAP : (uint32_t)(wb - a.lbase);
+	const uint32_t np = m * 4;
+	const uint32_t ks = (np + 255) / 256, kd = (m + 255) / 256;
+	const double2 *s2 = reinterpret_cast<const double2 *>(src + rb);
+	const uint32_t *nx2 = lnext + rb;
+	if constexpr (PAD) {
 #pragma unroll
 		for (int k = KP; k < KS; ++k)
 			if (k < (int)ks) sv[k] = s2[threadIdx.x + k * 256];
@@ -582,22 +633,12 @@ __global__ __launch_bounds__(256) void k_ov_lord(const uint64_t *__restrict__ co
 		return it == 0 ? xr0 : it == 1 ? xr1 : ent_x(col[i]);
 	};
 	auto fof = [&](uint32_t i) -> bool { return fe_uniform ? fe : (col[i].x & a.first_mask) != 0; };
-	double2 msj = make_double2(0.0, 0.0), natj = make_double2(0.0, 0.0), nx = make_double2(0.0, 0.0);
-	double rho = 0.0, hg = a.hyp0;
-	uint32_t cc = 0, tc = 0;
-	const size_t pi = (size_t)j * a.ms_stride;
-	// every per-column load issued at once: on field data the feature id is arithmetic
-	// (feat_contig), so these wait for nothing -- not for the column bounds (a column empty in
-	// this batch loads its parameters for nothing)
-	if (live) {
-		msj = ms[pi];
-		natj = nat[(size_t)j * a.nat_stride];
-		rho = rho_p[j];
-		cc = ccount[j];
-		if (!a.hyp_uniform) hg = a.hyp[(size_t)a.attr_group[j] * a.hyp_stride];
-		if (a.tcount) tc = a.tcount[j];
-		if constexpr (NEXT) nx = a.ms_next[(size_t)j * a.ms_stride_next];
-	}
+	// these two follow a pointer from the kernarg segment (used after the statistics loop / only
+	// with several attribute groups)
+	double hg = a.hyp0;
+	uint32_t tc = 0;
+	if (!a.hyp_uniform) hg = a.hyp[(size_t)a.attr_group[j] * a.hyp_stride];
+	if (a.tcount) tc = a.tcount[j];
 	// unconditional: slots past the run are never read, and a guarded write lets the compiler
 	// merge it with its load and wait there
 #pragma unroll
@@ -664,12 +705,12 @@ __global__ __launch_bounds__(256) void k_ov_lord(const uint64_t *__restrict__ co
 			go = false;
 		}
 		if (leader) {
-			nat[(size_t)j * a.nat_stride] = make_double2(nmu, nsig);
+			nat[(size_t)pj * nat_stride] = make_double2(nmu, nsig);
 			ms[pi] = make_double2(mu, sig);
 			if constexpr (IS_W) {
 				const uint32_t t = tc + n;
 				a.tcount[j] = t;
-				rho_p[j] = pow((double)(T0 + t), -LAMDA);
+				rho_p[pj] = pow((double)(T0 + t), -LAMDA);
 			} else {
 				if (a.tcount) a.tcount[j] = tc + n;
 			}
@@ -737,23 +778,59 @@ void launch_ov_lord_pad(const LevelArgs &a, int is_w, hipStream_t s)
 	const bool nx = a.ms_next != nullptr;
 #define OV_LORD_ARGS a.col_ptr, a.src, a.lnext, a.ms, a.nat, a.rho, a.ccount, a.nfeat, a
 	if (is_w) {
-		if (nx) k_ov_lord<G, true, 0, true, PAD><<<grid, 256, 0, s>>>(OV_LORD_ARGS);
-		else k_ov_lord<G, true, 0, false, PAD><<<grid, 256, 0, s>>>(OV_LORD_ARGS);
+		if (nx) k_ov_lord<G, true, 0, true, PAD, false><<<grid, 256, 0, s>>>(OV_LORD_ARGS);
+		else k_ov_lord<G, true, 0, false, PAD, false><<<grid, 256, 0, s>>>(OV_LORD_ARGS);
 	} else if (a.slot == 0) {
-		if (nx) k_ov_lord<G, false, 0, true, PAD><<<grid, 256, 0, s>>>(OV_LORD_ARGS);
-		else k_ov_lord<G, false, 0, false, PAD><<<grid, 256, 0, s>>>(OV_LORD_ARGS);
+		if (nx) k_ov_lord<G, false, 0, true, PAD, false><<<grid, 256, 0, s>>>(OV_LORD_ARGS);
+		else k_ov_lord<G, false, 0, false, PAD, false><<<grid, 256, 0, s>>>(OV_LORD_ARGS);
 	} else {
-		if (nx) k_ov_lord<G, false, 1, true, PAD><<<grid, 256, 0, s>>>(OV_LORD_ARGS);
-		else k_ov_lord<G, false, 1, false, PAD><<<grid, 256, 0, s>>>(OV_LORD_ARGS);
+		if (nx) k_ov_lord<G, false, 1, true, PAD, false><<<grid, 256, 0, s>>>(OV_LORD_ARGS);
+		else k_ov_lord<G, false, 1, false, PAD, false><<<grid, 256, 0, s>>>(OV_LORD_ARGS);
 	}
 #undef OV_LORD_ARGS
+}
+
+// the tagged-argument form of a v sweep's padded level (k_ov_lord FAST): field data (the level's
+// features are consecutive ids), factor-major nat, the next factor's {mu, sigma} adjacent in ms (or
+// none), and pointers / values that fit the tags; false: the caller takes the plain form
+template <int G>
+bool launch_ov_lord_fast(const LevelArgs &a, int is_w, hipStream_t s)
+{
+	if (is_w || !a.pad_cap || !a.ov_fast || !a.feat_contig || a.nat_stride != 1) return false;
+	if (a.ms_next && a.ms_next != a.ms + 1) return false;
+	auto fits = [](const void *p) { return (reinterpret_cast<uintptr_t>(p) >> 48) == 0; };
+	if (!fits(a.col_ptr) || !fits(a.src) || !fits(a.lnext) || a.ms_stride > 0xffffu) return false;
+	auto tag = [](const void *p, uint64_t v) {
+		return reinterpret_cast<uintptr_t>(p) | (uintptr_t)(v << 48);
+	};
+	const uint64_t *cp = reinterpret_cast<const uint64_t *>(tag(a.col_ptr, a.nfeat & 0xffffu));
+	const RowRec *sr = reinterpret_cast<const RowRec *>(tag(a.src, a.nfeat >> 16));
+	const uint32_t *ln = reinterpret_cast<const uint32_t *>(tag(a.lnext, a.ms_stride));
+	double2 *ms = a.ms + (size_t)a.feat_base * a.ms_stride;
+	double2 *nat = a.nat + a.feat_base;
+	double *rho = a.rho + a.feat_base;
+	const uint32_t *cc = a.ccount + a.feat_base;
+	const unsigned grid = (a.nfeat + 256 / G - 1) / (256 / G);
+#define OV_FAST_ARGS cp, sr, ln, ms, nat, rho, cc, a.nfeat, a
+	if (a.slot == 0) {
+		if (a.ms_next) k_ov_lord<G, false, 0, true, true, true><<<grid, 256, 0, s>>>(OV_FAST_ARGS);
+		else k_ov_lord<G, false, 0, false, true, true><<<grid, 256, 0, s>>>(OV_FAST_ARGS);
+	} else {
+		if (a.ms_next) k_ov_lord<G, false, 1, true, true, true><<<grid, 256, 0, s>>>(OV_FAST_ARGS);
+		else k_ov_lord<G, false, 1, false, true, true><<<grid, 256, 0, s>>>(OV_FAST_ARGS);
+	}
+#undef OV_FAST_ARGS
+	return true;
 }
 
 template <int G>
 hipError_t launch_ov_lord(const LevelArgs &a, int is_w, hipStream_t s)
 {
-	if (a.pad_cap) launch_ov_lord_pad<G, true>(a, is_w, s);
-	else launch_ov_lord_pad<G, false>(a, is_w, s);
+	if (a.pad_cap) {
+		if (!launch_ov_lord_fast<G>(a, is_w, s)) launch_ov_lord_pad<G, true>(a, is_w, s);
+	} else {
+		launch_ov_lord_pad<G, false>(a, is_w, s);
+	}
 	return hipGetLastError();
 }
 
@@ -855,6 +932,7 @@ struct OvState {
 	std::vector<uint8_t> batch_pad;    // [num_batch]
 	uint64_t pad_rows = 0;             // records a padded level's buffer needs (max over levels)
 	bool pad_on = false;               // the batch being processed uses the padded layout
+	bool fast = true;                  // v levels on it take k_ov_lord's tagged arguments (VBFM_OV_FAST)
 	uint32_t cur_n = 0;                // its rows
 	uint64_t *lvl_d = nullptr;         // [num_batch * (L+1)] first entry of every level of every batch
 	std::vector<uint64_t> lvl_h;
@@ -919,6 +997,7 @@ void ov_launch_level(vbfm_ctx *c, LevelArgs &a, uint32_t l, bool is_w)
 	if (o.pad_on && l > 0) {   // the padded layout: slot w of the level's buffer, lnx likewise
 		a.pad_cap = vbk::ov_pad_cap();
 		a.lnext = o.lnx + o.cur_n + o.pad_prefix[l];
+		a.ov_fast = o.fast;
 	}
 	// every level of the store holds each batch row once and a row's features ascend with the
 	// levels: level 0 holds every row's first entry (the ROW_FIRST bit of its CSC entries)
@@ -1315,6 +1394,8 @@ int vbfm_online_init(vbfm_ctx *c, const vbfm_online_config *cfg)
 					// the padded layout (VBFM_OV_PAD=0: packed runs at every level); the lanes per
 					// column of a level's kernel follow its mean batch column (ov_level_args)
 					const char *pe = getenv("VBFM_OV_PAD");
+					const char *fe = getenv("VBFM_OV_FAST");   // A/B: 0 = the untagged arguments everywhere
+					o.fast = !(fe && fe[0] == '0');
 					if (!(pe && pe[0] == '0') && L > 1) {
 						const uint32_t cap = vbk::ov_pad_cap();
 						o.cpw_h.assign(L, 0);

@@ -166,3 +166,32 @@ def test_online_padded_store_bit_identical(xmode, monkeypatch):
     assert res["1"][0] == res["0"][0]
     for key in res["0"][1]:
         np.testing.assert_array_equal(res["1"][1][key], res["0"][1][key], err_msg=key)
+
+
+@pytest.mark.parametrize("xmode,S", [(0, 100), (1, 100), (0, 70000)])
+def test_online_tagged_arguments_bit_identical(xmode, S, monkeypatch):
+    """The v levels' tagged-argument form of k_ov_lord (the level's column count and the stride of
+    ms in the pointers' top bits, the parameter pointers offset to the level's first feature) runs
+    the same lanes as the plain form (VBFM_OV_FAST=0): epochs and parameters equal bit for bit.
+    S = 70000 puts more than 2^16 columns in a level (both halves of the count in use)."""
+    import synth
+    n, F, k, nb = (40000, 6, 3, 10) if S == 100 else (200000, 3, 2, 4)
+    rp, f, v, y = synth.generate(n, F, S, 61, xmode)
+    te = synth.generate(1000, F, S, 62, xmode)
+    res = {}
+    for fast in ("1", "0"):
+        monkeypatch.setenv("VBFM_OV_FAST", fast)
+        g = vbfm.FMLearnVBOnline(1, 1, k, F * S, min_target=float(y.min()), max_target=float(y.max()))
+        g.set_data(vbfm.DataSubset.from_csr(rp, f, v, y, F * S), vbfm.DataSubset.from_csr(*te, F * S))
+        g.init(5, 0.1, nb)
+        st = [g.epoch() for _ in range(2)]
+        assert st[-1].n_pad_batches == nb
+        p, s = g.get_params(), g.online_state()
+        res[fast] = ([(x.rmse, x.mae, x.free_energy_first, x.free_energy_last, x.alpha) for x in st],
+                     {key: np.asarray(p[key]) for key in ("mu_w", "sigma_w", "mu_v", "sigma_v")},
+                     {key: np.asarray(s[key]) for key in ("nat_mu_v", "nat_sigma_v", "new_vj")})
+        g.close()
+    assert res["1"][0] == res["0"][0]
+    for i in (1, 2):
+        for key in res["0"][i]:
+            np.testing.assert_array_equal(res["1"][i][key], res["0"][i][key], err_msg=key)
