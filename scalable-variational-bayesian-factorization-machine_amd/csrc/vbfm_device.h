@@ -22,9 +22,10 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdlib.h>
+#include <type_traits>
 
-// The longest mean column of a level swept with the 64-thread x 2 workgroup shape (longer: 256 x
-// 1, 256 x 2, 512 x 2). Every level kernel -- fused, deferred split, column-gather, entry store,
+// The longest mean column of a level swept with the 64-thread x 2 workgroup shape (longer: see
+// dispatch_shape). Every level kernel -- fused, deferred split, column-gather, entry store,
 // MCMC -- takes its shape from the same thresholds: the same shape gives the same reduction tree,
 // so the layouts and the fused / split forms stay bit-identical to each other. 128: a level of
 // C4's per-rank shard on 8 GPUs (columns of ~100 entries) runs 2-5 % faster in the deferred split
@@ -39,6 +40,43 @@ inline uint32_t shape_small_max()
 		return e ? (uint32_t)atoi(e) : 128u;
 	}();
 	return v;
+}
+
+// A level's workgroup shape: BLOCK threads per column, R records per thread staged in LDS
+// (CAP = BLOCK x R; a longer run is swept in chunks of CAP). f(BLOCK, R) is called with the shape
+// as std::integral_constant values, so every kernel family launches its own template from one
+// table. The reduction tree of a column depends on BLOCK only.
+//   mean column <= shape_small_max():  64 x 2  (CAP 128)
+//               <= 200:               256 x 1  (CAP 256)
+//               <= 384:               128 x 3  (CAP 384: ~3 standard deviations above the mean
+//                                     stay resident; 26 KB of LDS, 6 workgroups per CU, so a
+//                                     level of <= 1,536 columns runs in one round. Multi-hot
+//                                     bench +6 % against 256 x 2, field data of 250-entry columns
+//                                     +2 % against 256 x 1: profiles/r05_multihot/shape_ab/)
+//               <= 640:               256 x 2  (CAP 512)
+//               longer:               512 x 2  (CAP 1024)
+template <class F> inline void dispatch_shape(uint32_t avg, F &&f)
+{
+	typedef std::integral_constant<int, 64> B64;
+	typedef std::integral_constant<int, 128> B128;
+	typedef std::integral_constant<int, 256> B256;
+	typedef std::integral_constant<int, 512> B512;
+	typedef std::integral_constant<int, 1> R1;
+	typedef std::integral_constant<int, 2> R2;
+	typedef std::integral_constant<int, 3> R3;
+	if (avg <= shape_small_max()) f(B64(), R2());
+	else if (avg <= 200) f(B256(), R1());
+	else if (avg <= 384) f(B128(), R3());
+	else if (avg <= 640) f(B256(), R2());
+	else f(B512(), R2());
+}
+
+// the BLOCK of dispatch_shape (kernels that take no R)
+inline int shape_block(uint32_t avg)
+{
+	int b = 0;
+	dispatch_shape(avg, [&](auto B, auto) { b = B(); });
+	return b;
 }
 
 struct __attribute__((aligned(64))) RowRec {

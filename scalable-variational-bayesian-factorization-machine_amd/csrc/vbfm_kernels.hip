@@ -1359,24 +1359,18 @@ inline unsigned grid_for(uint64_t n, unsigned block = 256) { return (unsigned)((
 namespace vbk {
 
 // Column-length-adaptive launch shape: threads per column and entries held per thread
-// from the level's mean column length.
+// from the level's mean column length (dispatch_shape, vbfm_device.h).
 template <int P, bool NEXT>
 hipError_t launch_v_fused(const LevelArgs &a, hipStream_t s)
 {
-	if (a.avg_len <= shape_small_max()) k_v_level_fused<64, 2, P, NEXT><<<a.nfeat, 64, 0, s>>>(a);
-	else if (a.avg_len <= 320) k_v_level_fused<256, 1, P, NEXT><<<a.nfeat, 256, 0, s>>>(a);
-	else if (a.avg_len <= 640) k_v_level_fused<256, 2, P, NEXT><<<a.nfeat, 256, 0, s>>>(a);
-	else k_v_level_fused<512, 2, P, NEXT><<<a.nfeat, 512, 0, s>>>(a);
+	dispatch_shape(a.avg_len, [&](auto B, auto R) { k_v_level_fused<B(), R(), P, NEXT><<<a.nfeat, B(), 0, s>>>(a); });
 	return hipGetLastError();
 }
 
 template <bool NEXT>
 hipError_t launch_w_fused(const LevelArgs &a, hipStream_t s)
 {
-	if (a.avg_len <= shape_small_max()) k_w_level_fused<64, 2, NEXT><<<a.nfeat, 64, 0, s>>>(a);
-	else if (a.avg_len <= 320) k_w_level_fused<256, 1, NEXT><<<a.nfeat, 256, 0, s>>>(a);
-	else if (a.avg_len <= 640) k_w_level_fused<256, 2, NEXT><<<a.nfeat, 256, 0, s>>>(a);
-	else k_w_level_fused<512, 2, NEXT><<<a.nfeat, 512, 0, s>>>(a);
+	dispatch_shape(a.avg_len, [&](auto B, auto R) { k_w_level_fused<B(), R(), NEXT><<<a.nfeat, B(), 0, s>>>(a); });
 	return hipGetLastError();
 }
 
@@ -1414,8 +1408,11 @@ hipError_t col_long(const LevelArgs &a, int is_w, hipStream_t s)
 hipError_t v_level_stats(const LevelArgs &a, hipStream_t s)
 {
 	if (a.nfeat == 0) return hipSuccess;
-	if (a.slot == 0) k_v_level_stats<256, 0><<<a.nfeat, 256, 0, s>>>(a);
-	else k_v_level_stats<256, 1><<<a.nfeat, 256, 0, s>>>(a);
+	// the fused kernel's BLOCK: the same reduction tree, so the split form equals the fused one
+	dispatch_shape(a.avg_len, [&](auto B, auto) {
+		if (a.slot == 0) k_v_level_stats<B(), 0><<<a.nfeat, B(), 0, s>>>(a);
+		else k_v_level_stats<B(), 1><<<a.nfeat, B(), 0, s>>>(a);
+	});
 	return hipGetLastError();
 }
 hipError_t v_level_correct(const LevelArgs &a, hipStream_t s)
@@ -1434,7 +1431,7 @@ hipError_t v_level_correct(const LevelArgs &a, hipStream_t s)
 hipError_t w_level_stats(const LevelArgs &a, hipStream_t s)
 {
 	if (a.nfeat == 0) return hipSuccess;
-	k_w_level_stats<256><<<a.nfeat, 256, 0, s>>>(a);
+	dispatch_shape(a.avg_len, [&](auto B, auto) { k_w_level_stats<B()><<<a.nfeat, B(), 0, s>>>(a); });
 	return hipGetLastError();
 }
 hipError_t w_level_correct(const LevelArgs &a, hipStream_t s)

@@ -899,20 +899,21 @@ static int wave_wpb()
 	return e && atoi(e) == 1 ? 1 : 4;
 }
 
-template <int G, int WPB, bool IS_W, int P, bool NEXT>
+template <int VB, int G, int WPB, bool IS_W, int P, bool NEXT>
 void launch_wave_g(const LevelArgs &a, hipStream_t s)
 {
-	k_level_wave<256, G, WPB, IS_W, P, NEXT><<<(a.nfeat + WPB - 1) / WPB, 64 * WPB, 0, s>>>(a);
+	k_level_wave<VB, G, WPB, IS_W, P, NEXT><<<(a.nfeat + WPB - 1) / WPB, 64 * WPB, 0, s>>>(a);
 }
 
 // registers for G*64 records: the level's mean column plus ~3 standard deviations of the
-// binomial spread fits (runs that do not are swept in chunks, the same results)
-template <bool IS_W, int P, bool NEXT>
+// binomial spread fits (runs that do not are swept in chunks, the same results); VB: the
+// workgroup kernel's BLOCK for the level (128 or 256), whose reduction tree the wave reproduces
+template <int VB, bool IS_W, int P, bool NEXT>
 void launch_wave(const LevelArgs &a, hipStream_t s)
 {
 	const bool g4 = a.avg_len <= 200;
-	if (wave_wpb() == 1) g4 ? launch_wave_g<4, 1, IS_W, P, NEXT>(a, s) : launch_wave_g<8, 1, IS_W, P, NEXT>(a, s);
-	else g4 ? launch_wave_g<4, 4, IS_W, P, NEXT>(a, s) : launch_wave_g<8, 4, IS_W, P, NEXT>(a, s);
+	if (wave_wpb() == 1) g4 ? launch_wave_g<VB, 4, 1, IS_W, P, NEXT>(a, s) : launch_wave_g<VB, 8, 1, IS_W, P, NEXT>(a, s);
+	else g4 ? launch_wave_g<VB, 4, 4, IS_W, P, NEXT>(a, s) : launch_wave_g<VB, 8, 4, IS_W, P, NEXT>(a, s);
 }
 
 // the wave kernels address a column's run through 32-bit buffer descriptors (num_records = run x
@@ -923,28 +924,21 @@ constexpr uint32_t WAVE_MAX_RUN = (1u << 25) - 1;
 template <bool IS_W, int P, bool NEXT>
 void launch_lord(const LevelArgs &a, hipStream_t s)
 {
-	if (!a.ent && wave_mode() && a.avg_len > shape_small_max() && a.avg_len <= 640 && a.max_len <= WAVE_MAX_RUN)
-		return launch_wave<IS_W, P, NEXT>(a, s);
-	if (a.ent) {
-		if (a.avg_len <= shape_small_max()) k_level_lord<64, 2, IS_W, P, NEXT, true><<<a.nfeat, 64, 0, s>>>(a);
-		else if (a.avg_len <= 320) k_level_lord<256, 1, IS_W, P, NEXT, true><<<a.nfeat, 256, 0, s>>>(a);
-		else if (a.avg_len <= 640) k_level_lord<256, 2, IS_W, P, NEXT, true><<<a.nfeat, 256, 0, s>>>(a);
-		else k_level_lord<512, 2, IS_W, P, NEXT, true><<<a.nfeat, 512, 0, s>>>(a);
+	if (!a.ent && wave_mode() && a.avg_len > shape_small_max() && a.avg_len <= 640 && a.max_len <= WAVE_MAX_RUN) {
+		if (shape_block(a.avg_len) == 128) launch_wave<128, IS_W, P, NEXT>(a, s);
+		else launch_wave<256, IS_W, P, NEXT>(a, s);
 		return;
 	}
-	if (a.avg_len <= shape_small_max()) k_level_lord<64, 2, IS_W, P, NEXT, false><<<a.nfeat, 64, 0, s>>>(a);
-	else if (a.avg_len <= 320) k_level_lord<256, 1, IS_W, P, NEXT, false><<<a.nfeat, 256, 0, s>>>(a);
-	else if (a.avg_len <= 640) k_level_lord<256, 2, IS_W, P, NEXT, false><<<a.nfeat, 256, 0, s>>>(a);
-	else k_level_lord<512, 2, IS_W, P, NEXT, false><<<a.nfeat, 512, 0, s>>>(a);
+	dispatch_shape(a.avg_len, [&](auto B, auto R) {
+		if (a.ent) k_level_lord<B(), R(), IS_W, P, NEXT, true><<<a.nfeat, B(), 0, s>>>(a);
+		else k_level_lord<B(), R(), IS_W, P, NEXT, false><<<a.nfeat, B(), 0, s>>>(a);
+	});
 }
 
 template <bool IS_W, int P, bool NEXT, bool ENT>
 void launch_lord_move_shape(const LevelArgs &a, hipStream_t s)
 {
-	if (a.avg_len <= shape_small_max()) k_level_lord_move<64, 2, IS_W, P, NEXT, ENT><<<a.nfeat, 64, 0, s>>>(a);
-	else if (a.avg_len <= 320) k_level_lord_move<256, 1, IS_W, P, NEXT, ENT><<<a.nfeat, 256, 0, s>>>(a);
-	else if (a.avg_len <= 640) k_level_lord_move<256, 2, IS_W, P, NEXT, ENT><<<a.nfeat, 256, 0, s>>>(a);
-	else k_level_lord_move<512, 2, IS_W, P, NEXT, ENT><<<a.nfeat, 512, 0, s>>>(a);
+	dispatch_shape(a.avg_len, [&](auto B, auto R) { k_level_lord_move<B(), R(), IS_W, P, NEXT, ENT><<<a.nfeat, B(), 0, s>>>(a); });
 }
 
 template <bool IS_W, int P>
@@ -962,10 +956,7 @@ void launch_lord_move(const LevelArgs &a, hipStream_t s)
 template <bool IS_W, int P>
 void launch_lord_stats(const LevelArgs &a, hipStream_t s)
 {
-	if (a.avg_len <= shape_small_max()) k_level_lord_stats<64, 2, IS_W, P><<<a.nfeat, 64, 0, s>>>(a);
-	else if (a.avg_len <= 320) k_level_lord_stats<256, 1, IS_W, P><<<a.nfeat, 256, 0, s>>>(a);
-	else if (a.avg_len <= 640) k_level_lord_stats<256, 2, IS_W, P><<<a.nfeat, 256, 0, s>>>(a);
-	else k_level_lord_stats<512, 2, IS_W, P><<<a.nfeat, 512, 0, s>>>(a);
+	dispatch_shape(a.avg_len, [&](auto B, auto R) { k_level_lord_stats<B(), R(), IS_W, P><<<a.nfeat, B(), 0, s>>>(a); });
 }
 
 
@@ -1293,29 +1284,32 @@ template <bool IS_W, int P, bool NEXT, int PK, bool ENT>
 void launch_defer_shape(const LevelArgs &a, hipStream_t s)
 {
 	if constexpr (!ENT) {
-		if (wave_mode() && a.avg_len > shape_small_max() && a.avg_len <= 640 && a.max_len <= WAVE_MAX_RUN) {   // k_defer_wave (256 shapes)
+		if (wave_mode() && a.avg_len > shape_small_max() && a.avg_len <= 640 && a.max_len <= WAVE_MAX_RUN) {
+			// k_defer_wave with the workgroup kernel's BLOCK as its virtual block (128 or 256)
 			const unsigned wpb = wave_wpb(), gr = (a.nfeat + wpb - 1) / wpb;
-			if (a.lpay2) {
-				if (wpb == 1) k_defer_wave<256, 4, 1, IS_W, P, NEXT, PK, true><<<gr, 64, 0, s>>>(a);
-				else k_defer_wave<256, 4, 4, IS_W, P, NEXT, PK, true><<<gr, 256, 0, s>>>(a);
-			} else {
-				if (wpb == 1) k_defer_wave<256, 4, 1, IS_W, P, NEXT, PK, false><<<gr, 64, 0, s>>>(a);
-				else k_defer_wave<256, 4, 4, IS_W, P, NEXT, PK, false><<<gr, 256, 0, s>>>(a);
-			}
+			auto go = [&](auto VB) {
+				if (a.lpay2) {
+					if (wpb == 1) k_defer_wave<VB(), 4, 1, IS_W, P, NEXT, PK, true><<<gr, 64, 0, s>>>(a);
+					else k_defer_wave<VB(), 4, 4, IS_W, P, NEXT, PK, true><<<gr, 256, 0, s>>>(a);
+				} else {
+					if (wpb == 1) k_defer_wave<VB(), 4, 1, IS_W, P, NEXT, PK, false><<<gr, 64, 0, s>>>(a);
+					else k_defer_wave<VB(), 4, 4, IS_W, P, NEXT, PK, false><<<gr, 256, 0, s>>>(a);
+				}
+			};
+			if (shape_block(a.avg_len) == 128) go(std::integral_constant<int, 128>());
+			else go(std::integral_constant<int, 256>());
 			return;
 		}
 	}
 	if (a.lpay2) {   // every x 1: 8-B payloads
-		if (a.avg_len <= shape_small_max()) k_lord_defer<64, 2, IS_W, P, NEXT, PK, true, ENT><<<a.nfeat, 64, 0, s>>>(a);
-		else if (a.avg_len <= 320) k_lord_defer<256, 1, IS_W, P, NEXT, PK, true, ENT><<<a.nfeat, 256, 0, s>>>(a);
-		else if (a.avg_len <= 640) k_lord_defer<256, 2, IS_W, P, NEXT, PK, true, ENT><<<a.nfeat, 256, 0, s>>>(a);
-		else k_lord_defer<512, 2, IS_W, P, NEXT, PK, true, ENT><<<a.nfeat, 512, 0, s>>>(a);
+		dispatch_shape(a.avg_len, [&](auto B, auto R) {
+			k_lord_defer<B(), R(), IS_W, P, NEXT, PK, true, ENT><<<a.nfeat, B(), 0, s>>>(a);
+		});
 		return;
 	}
-	if (a.avg_len <= shape_small_max()) k_lord_defer<64, 2, IS_W, P, NEXT, PK, false, ENT><<<a.nfeat, 64, 0, s>>>(a);
-	else if (a.avg_len <= 320) k_lord_defer<256, 1, IS_W, P, NEXT, PK, false, ENT><<<a.nfeat, 256, 0, s>>>(a);
-	else if (a.avg_len <= 640) k_lord_defer<256, 2, IS_W, P, NEXT, PK, false, ENT><<<a.nfeat, 256, 0, s>>>(a);
-	else k_lord_defer<512, 2, IS_W, P, NEXT, PK, false, ENT><<<a.nfeat, 512, 0, s>>>(a);
+	dispatch_shape(a.avg_len, [&](auto B, auto R) {
+		k_lord_defer<B(), R(), IS_W, P, NEXT, PK, false, ENT><<<a.nfeat, B(), 0, s>>>(a);
+	});
 }
 
 template <bool IS_W, int P, bool NEXT, int PK>
@@ -1480,16 +1474,14 @@ template <bool IS_W, int P, bool NEXT>
 void launch_mc_defer(const McArgs &a, hipStream_t s)
 {
 	if (a.lpay2) {   // every x 1: 8-B payloads
-		if (a.avg_len <= shape_small_max()) k_mc_lord_defer<64, 2, IS_W, P, NEXT, true><<<a.nfeat, 64, 0, s>>>(a);
-		else if (a.avg_len <= 320) k_mc_lord_defer<256, 1, IS_W, P, NEXT, true><<<a.nfeat, 256, 0, s>>>(a);
-		else if (a.avg_len <= 640) k_mc_lord_defer<256, 2, IS_W, P, NEXT, true><<<a.nfeat, 256, 0, s>>>(a);
-		else k_mc_lord_defer<512, 2, IS_W, P, NEXT, true><<<a.nfeat, 512, 0, s>>>(a);
+		dispatch_shape(a.avg_len, [&](auto B, auto R) {
+			k_mc_lord_defer<B(), R(), IS_W, P, NEXT, true><<<a.nfeat, B(), 0, s>>>(a);
+		});
 		return;
 	}
-	if (a.avg_len <= shape_small_max()) k_mc_lord_defer<64, 2, IS_W, P, NEXT, false><<<a.nfeat, 64, 0, s>>>(a);
-	else if (a.avg_len <= 320) k_mc_lord_defer<256, 1, IS_W, P, NEXT, false><<<a.nfeat, 256, 0, s>>>(a);
-	else if (a.avg_len <= 640) k_mc_lord_defer<256, 2, IS_W, P, NEXT, false><<<a.nfeat, 256, 0, s>>>(a);
-	else k_mc_lord_defer<512, 2, IS_W, P, NEXT, false><<<a.nfeat, 512, 0, s>>>(a);
+	dispatch_shape(a.avg_len, [&](auto B, auto R) {
+		k_mc_lord_defer<B(), R(), IS_W, P, NEXT, false><<<a.nfeat, B(), 0, s>>>(a);
+	});
 }
 
 template <int BLOCK, int R, int MODE, bool ENT>
@@ -1522,10 +1514,7 @@ void launch_mc_lord_shape(const McArgs &a, int is_w, hipStream_t s)
 {
 	// the column-gather MCMC kernel's BLOCK (vbfm_mcmc.hip launch_level), records per thread
 	// as the VB level kernel
-	if (a.avg_len <= shape_small_max()) launch_mc_lord<64, 2, MODE>(a, is_w, s);
-	else if (a.avg_len <= 320) launch_mc_lord<256, 1, MODE>(a, is_w, s);
-	else if (a.avg_len <= 640) launch_mc_lord<256, 2, MODE>(a, is_w, s);
-	else launch_mc_lord<512, 2, MODE>(a, is_w, s);
+	dispatch_shape(a.avg_len, [&](auto B, auto R) { launch_mc_lord<B(), R(), MODE>(a, is_w, s); });
 }
 
 }  // namespace

@@ -392,9 +392,10 @@ static void launch_w(const McArgs &a, hipStream_t s)
 template <int MODE>
 static void launch_level(const McArgs &a, bool is_w, hipStream_t s)
 {
-	if (a.avg_len <= shape_small_max()) { if (is_w) launch_w<64, MODE>(a, s); else launch_v<64, MODE>(a, s); }
-	else if (a.avg_len <= 640) { if (is_w) launch_w<256, MODE>(a, s); else launch_v<256, MODE>(a, s); }
-	else { if (is_w) launch_w<512, MODE>(a, s); else launch_v<512, MODE>(a, s); }
+	dispatch_shape(a.avg_len, [&](auto B, auto) {
+		if (is_w) launch_w<B(), MODE>(a, s);
+		else launch_v<B(), MODE>(a, s);
+	});
 }
 
 static hipError_t mc_level(const McArgs &a, int mode, bool is_w, hipStream_t s)
