@@ -328,19 +328,34 @@ DEVI void res_move(double2 *recs, uint32_t *dsts, uint32_t n, const float (&xr)[
 // correct and move every record. Runs longer than CAP = BLOCK*R records are streamed twice
 // (contiguous, L2-warm).
 template <int BLOCK, int R, bool IS_W, int P, bool NEXT, bool ENT>
-__global__ __launch_bounds__(BLOCK) void k_level_lord(LevelArgs a)
+__global__ __launch_bounds__(BLOCK) void k_level_lord(const uint64_t *lcp, const uint32_t *feats, const RowRec *src_l,
+                                                      const uint32_t *lnext_l, const float *lx_l, double2 *ms,
+                                                      uint32_t ms_stride, LevelArgs a)
 {
 	constexpr uint32_t CAP = BLOCK * R;
 	__shared__ double2 recs[CAP * 4];
 	__shared__ uint32_t dsts[CAP];
 	__shared__ double lds[2 * (BLOCK / 64)];
-	const uint32_t j = level_feat(a, blockIdx.x);
-	const uint64_t sb = a.lcp[blockIdx.x];
-	const uint32_t n = (uint32_t)(a.lcp[blockIdx.x + 1] - sb);
+	// the column's run bounds and its parameters first, from preloaded arguments only (LordLead):
+	// the feature's index into ms (relative to the level's first feature on field data) ...
+	// (no branch around a load: a branch puts a wait behind it; the feature-list load reads lcp's
+	// word instead when there is no list)
+	const uint64_t sb = lcp[blockIdx.x];
+	const uint64_t se = lcp[blockIdx.x + 1];
+	const uint32_t fj = *(feats ? feats + blockIdx.x : reinterpret_cast<const uint32_t *>(lcp + blockIdx.x));
+	const uint32_t jr = feats ? fj : blockIdx.x;
+	const uint32_t n = (uint32_t)(se - sb);
+	const double2 msj = ms[(size_t)jr * ms_stride];
+	// ... and every LevelArgs field the workgroup reads, fetched in one batch with them (left to
+	// itself the compiler fetches them in several batches, each after a wait); the empty asm only
+	// pins them to this point
+	asm volatile("; k_level_lord: LevelArgs fields" ::"s"(a.long_min), "s"(a.lbase), "s"(a.hyp_uniform), "s"(a.hyp0),
+	             "s"(a.alpha), "s"(a.counters), "s"(a.dst), "s"(a.first_level), "s"(a.feat_base),
+	             "s"(a.ms_next), "s"(a.ms_stride_next));
+	const uint32_t j = feats ? jr : a.feat_base + jr;   // the feature id
 	if (a.long_min && n > a.long_min) return;      // a long column: the segment kernels' (lord_long)
-	const RowRec *src = a.src + (sb - a.lbase);
-	const float *lx = a.lx ? a.lx + sb : nullptr;   // null: every x is 1 (lx not stored)
-	const double2 msj = a.ms[(size_t)j * a.ms_stride];
+	const RowRec *src = src_l + (sb - a.lbase);
+	const float *lx = lx_l ? lx_l + sb : nullptr;   // null: every x is 1 (lx not stored)
 	VbOp<IS_W, P, NEXT> op;
 	op.mo = msj.x; op.so = msj.y;
 	op.nx = NEXT ? a.ms_next[(size_t)j * a.ms_stride_next] : make_double2(0.0, 0.0);
@@ -351,21 +366,21 @@ __global__ __launch_bounds__(BLOCK) void k_level_lord(LevelArgs a)
 	if (n <= CAP) {   // the run stays in LDS from the statistics to the move
 		float xr[R];
 		uint32_t nr[R];
-		res_prefetch<BLOCK, R>(lx, a.lnext + sb, n, xr, nr);
+		res_prefetch<BLOCK, R>(lx, lnext_l + sb, n, xr, nr);
 		stage_in<BLOCK, R>(recs, reinterpret_cast<const double2 *>(src), n);
 		__syncthreads();
 		res_stats<BLOCK, R>(recs, n, xr, op, s1, s2);
 		block_sum2<BLOCK>(s1, s2, lds);
 		op.go = vb_post<IS_W>(s1, s2, hyp, a.alpha, op.mo, op.so, op.mu, op.sig, a.counters, threadIdx.x == 0);
-		if (threadIdx.x == 0) a.ms[(size_t)j * a.ms_stride] = make_double2(op.mu, op.sig);
+		if (threadIdx.x == 0) ms[(size_t)jr * ms_stride] = make_double2(op.mu, op.sig);
 		res_move<BLOCK, R, VbOp<IS_W, P, NEXT>, ENT>(recs, dsts, n, xr, nr, a.dst, a.first_level != 0, op);
 		return;
 	}
 	lord_stats<BLOCK, CAP>(recs, src, lx, n, op, s1, s2);
 	block_sum2<BLOCK>(s1, s2, lds);
 	op.go = vb_post<IS_W>(s1, s2, hyp, a.alpha, op.mo, op.so, op.mu, op.sig, a.counters, threadIdx.x == 0);
-	if (threadIdx.x == 0) a.ms[(size_t)j * a.ms_stride] = make_double2(op.mu, op.sig);
-	lord_move<BLOCK, CAP, VbOp<IS_W, P, NEXT>, ENT>(recs, dsts, src, lx, a.lnext + sb, n, false, a.dst,
+	if (threadIdx.x == 0) ms[(size_t)jr * ms_stride] = make_double2(op.mu, op.sig);
+	lord_move<BLOCK, CAP, VbOp<IS_W, P, NEXT>, ENT>(recs, dsts, src, lx, lnext_l + sb, n, false, a.dst,
 	                                                a.first_level != 0, op);
 }
 
@@ -921,6 +936,33 @@ void launch_wave(const LevelArgs &a, hipStream_t s)
 // skewed shard) keeps the workgroup kernels
 constexpr uint32_t WAVE_MAX_RUN = (1u << 25) - 1;
 
+// The leading (preloaded, -amdgpu-kernarg-preload-count) arguments of k_level_lord: everything the
+// loads of a column's bounds and parameters need, so they issue at wave start. On field data ms
+// arrives offset to the level's first feature (feats null: the column's index is blockIdx.x)
+struct LordLead {
+	const uint64_t *lcp;
+	const uint32_t *feats;
+	const RowRec *src;
+	const uint32_t *lnext;
+	const float *lx;
+	double2 *ms;
+	uint32_t ms_stride;
+};
+#define LORD_LEAD_ARGS(L) L.lcp, L.feats, L.src, L.lnext, L.lx, L.ms, L.ms_stride
+
+inline LordLead lord_lead(const LevelArgs &a)
+{
+	LordLead L;
+	L.lcp = a.lcp;
+	L.feats = a.feat_contig ? nullptr : a.feats;
+	L.src = a.src;
+	L.lnext = a.lnext;
+	L.lx = a.lx;
+	L.ms = a.feat_contig ? a.ms + (size_t)a.feat_base * a.ms_stride : a.ms;
+	L.ms_stride = a.ms_stride;
+	return L;
+}
+
 template <bool IS_W, int P, bool NEXT>
 void launch_lord(const LevelArgs &a, hipStream_t s)
 {
@@ -929,9 +971,10 @@ void launch_lord(const LevelArgs &a, hipStream_t s)
 		else launch_wave<256, IS_W, P, NEXT>(a, s);
 		return;
 	}
+	const LordLead L = lord_lead(a);
 	dispatch_shape(a.avg_len, [&](auto B, auto R) {
-		if (a.ent) k_level_lord<B(), R(), IS_W, P, NEXT, true><<<a.nfeat, B(), 0, s>>>(a);
-		else k_level_lord<B(), R(), IS_W, P, NEXT, false><<<a.nfeat, B(), 0, s>>>(a);
+		if (a.ent) k_level_lord<B(), R(), IS_W, P, NEXT, true><<<a.nfeat, B(), 0, s>>>(LORD_LEAD_ARGS(L), a);
+		else k_level_lord<B(), R(), IS_W, P, NEXT, false><<<a.nfeat, B(), 0, s>>>(LORD_LEAD_ARGS(L), a);
 	});
 }
 
