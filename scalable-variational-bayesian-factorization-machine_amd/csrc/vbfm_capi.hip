@@ -914,6 +914,13 @@ void require_train(vbfm_ctx *c)
 	if (!c->sched_ready) build_schedule(c);
 }
 
+// VBFM_PREFETCH=0 (A/B): the level kernels do not touch the next level's column bounds
+static bool pf_enabled()
+{
+	const char *e = getenv("VBFM_PREFETCH");
+	return !(e && e[0] == '0');
+}
+
 LevelArgs level_args(vbfm_ctx *c, uint32_t l, bool is_w, int f)
 {
 	LevelArgs a = {};
@@ -994,6 +1001,13 @@ void sweep_level(vbfm_ctx *c, uint32_t l, bool is_w, int f)
 	if (c->lord) {
 		// level-ordered store: stream this level's records, move them to the next level's order
 		a.lcp = c->lcp + c->level_ptr[l];
+		{   // the level after this one in launch order: l + 1, or level 0 of the next sweep
+			const uint32_t ln = l + 1 < nlevels(c) ? l + 1 : 0;
+			a.pf_lcp = pf_enabled() ? c->lcp + c->level_ptr[ln] : nullptr;
+			const bool contig = ln < c->level_base.size() && c->level_base[ln] != ~0u;
+			a.pf_feats = contig ? nullptr : c->level_feats + c->level_ptr[ln];
+			a.pf_n = a.pf_lcp ? c->level_ptr[ln + 1] - c->level_ptr[ln] : 0u;
+		}
 		a.lx = c->lx;
 		a.lnext = c->lnext;
 		a.lbase = (uint64_t)l * c->tr.n;

@@ -172,6 +172,11 @@ struct LevelArgs {
 	                           // w * pad_cap of the level's buffer (no column-bound load before the
 	                           // run's loads); 0: runs packed (positions from the column bounds)
 	int ov_fast;               // ... and a v level may take k_ov_lord's tagged-argument form
+	// level-ordered store: the next level's column bounds (and feature list, or null), whose lines
+	// each workgroup of this level touches once so that the next launch finds them in its L2
+	const uint64_t *pf_lcp;
+	const uint32_t *pf_feats;
+	uint32_t pf_n;
 	int hyp_uniform;           // one attribute group: the prior is hyp0 (no per-column lookup)
 	double hyp0;
 	// long columns of the level-ordered store (fused single-rank VB sweep): columns longer than

@@ -351,7 +351,7 @@ __global__ __launch_bounds__(BLOCK) void k_level_lord(const uint64_t *lcp, const
 	// pins them to this point
 	asm volatile("; k_level_lord: LevelArgs fields" ::"s"(a.long_min), "s"(a.lbase), "s"(a.hyp_uniform), "s"(a.hyp0),
 	             "s"(a.alpha), "s"(a.counters), "s"(a.dst), "s"(a.first_level), "s"(a.feat_base),
-	             "s"(a.ms_next), "s"(a.ms_stride_next));
+	             "s"(a.ms_next), "s"(a.ms_stride_next), "s"(a.pf_lcp), "s"(a.pf_feats), "s"(a.pf_n));
 	const uint32_t j = feats ? jr : a.feat_base + jr;   // the feature id
 	if (a.long_min && n > a.long_min) return;      // a long column: the segment kernels' (lord_long)
 	const RowRec *src = src_l + (sb - a.lbase);
@@ -369,11 +369,22 @@ __global__ __launch_bounds__(BLOCK) void k_level_lord(const uint64_t *lcp, const
 		res_prefetch<BLOCK, R>(lx, lnext_l + sb, n, xr, nr);
 		stage_in<BLOCK, R>(recs, reinterpret_cast<const double2 *>(src), n);
 		__syncthreads();
+		// the next level's column bounds (and feature id) of this workgroup index into this XCD's
+		// L2 (the next launch puts workgroup blockIdx.x on the same XCD): its first load then hits
+		// L2 instead of HBM. Issued after the run is staged, so the run's stream does not evict
+		// it (the moves below are non-temporal on the entry store); the value is kept by a test
+		// that never holds, at the end
+		uint64_t pf = 0;
+		if (threadIdx.x == 0 && blockIdx.x < a.pf_n) {
+			pf = a.pf_lcp[blockIdx.x];
+			if (a.pf_feats) pf += a.pf_feats[blockIdx.x];
+		}
 		res_stats<BLOCK, R>(recs, n, xr, op, s1, s2);
 		block_sum2<BLOCK>(s1, s2, lds);
 		op.go = vb_post<IS_W>(s1, s2, hyp, a.alpha, op.mo, op.so, op.mu, op.sig, a.counters, threadIdx.x == 0);
 		if (threadIdx.x == 0) ms[(size_t)jr * ms_stride] = make_double2(op.mu, op.sig);
 		res_move<BLOCK, R, VbOp<IS_W, P, NEXT>, ENT>(recs, dsts, n, xr, nr, a.dst, a.first_level != 0, op);
+		if (pf == ~0ull) a.counters[CNT_N - 1] = 0u;   // never: positions and ids are < 2^63
 		return;
 	}
 	lord_stats<BLOCK, CAP>(recs, src, lx, n, op, s1, s2);
