@@ -797,17 +797,11 @@ void build_schedule(vbfm_ctx *c)
 		const uint32_t lo = c->level_ptr[l], hi = c->level_ptr[l + 1];   // ascending, distinct ids
 		if (hi > lo && feats[hi - 1] - feats[lo] == hi - lo - 1) c->level_base[l] = feats[lo];
 	}
-	c->level_max.assign(L, 0);
 	for (uint32_t l = 0; l < L; l++) {
-		uint64_t z = 0, mx = 0;
-		for (uint32_t i = c->level_ptr[l]; i < c->level_ptr[l + 1]; i++) {
-			const uint64_t len = cp[feats[i] + 1] - cp[feats[i]];
-			z += len;
-			mx = std::max(mx, len);
-		}
+		uint64_t z = 0;
+		for (uint32_t i = c->level_ptr[l]; i < c->level_ptr[l + 1]; i++) z += cp[feats[i] + 1] - cp[feats[i]];
 		const uint32_t nfl = c->level_ptr[l + 1] - c->level_ptr[l];
 		c->level_avg[l] = nfl ? (uint32_t)std::min<uint64_t>(z / nfl, 0xFFFFFFFFu) : 0;
-		c->level_max[l] = (uint32_t)std::min<uint64_t>(mx, 0xFFFFFFFFu);
 	}
 	uint32_t maxlev = 0;
 	for (uint32_t l = 0; l < L; l++) maxlev = std::max(maxlev, c->level_ptr[l + 1] - c->level_ptr[l]);
@@ -946,7 +940,6 @@ LevelArgs level_args(vbfm_ctx *c, uint32_t l, bool is_w, int f)
 	a.counters = c->counters;
 	a.stats = c->stats;
 	a.avg_len = c->level_avg[l];
-	a.max_len = c->level_max[l];
 	a.first_mask = ROW_FIRST;
 	if (is_w) {
 		a.slot = 0;                                          // fused q-cache of factor 0

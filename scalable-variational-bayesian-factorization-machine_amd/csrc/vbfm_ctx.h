@@ -131,7 +131,7 @@ struct vbfm_ctx {
 	std::vector<double> hyp_w, hyp_v;
 	double alpha = 1.0, sigma_0 = 1.0, mu0 = 0.0, s0d = 0.02;
 	// schedule
-	std::vector<uint32_t> level_ptr, level_h, level_avg, level_max;
+	std::vector<uint32_t> level_ptr, level_h, level_avg;
 	std::vector<uint32_t> level_base;   // first id of a level of consecutive feature ids, else ~0u
 	int q_ready[2] = {-1, -1};     // factor whose q-cache each slot holds (-1: none)
 	int qslot = 0;                 // slot reported by vbfm_get_rows

@@ -135,7 +135,6 @@ struct LevelArgs {
 	uint32_t ms_stride_next;
 	int slot;                  // q-cache slot of the factor being swept (v) / of factor 0 (w)
 	uint32_t avg_len;          // mean column length of the level (launch shape)
-	uint32_t max_len;          // longest column of the level (the wave kernels' 32-bit buffer offsets)
 	uint32_t first_mask;       // ROW_FIRST: the fused q-cache restarts at a row's first entry;
 	                           // 0 (feature shards): partial sums from a zeroed slot
 	// level-ordered row store (vbfm_lorder.hip); unused by the column-gather kernels

@@ -201,6 +201,9 @@ __global__ __launch_bounds__(BLOCK) void k_v_level_correct(LevelArgs a)
 	double mu, sig;
 	const double sv_g = (a.hyp_uniform ? a.hyp0 : a.hyp[(size_t)a.attr_group[j] * a.hyp_stride]);
 	const bool go = v_post(st.x, st.y, sv_g, a.alpha, msj.x, msj.y, mu, sig, a.counters, threadIdx.x == 0);
+	// every wave has used the old value (v_post above) before it is overwritten: without the
+	// barrier a wave of this workgroup could still read the new one as its "old"
+	__syncthreads();
 	if (threadIdx.x == 0) a.ms[(size_t)j * a.ms_stride] = make_double2(mu, sig);
 	if (!go && !NEXT) return;
 	if (a.dup[j]) {
@@ -326,6 +329,9 @@ __global__ __launch_bounds__(BLOCK) void k_w_level_correct(LevelArgs a)
 	double mu, sig;
 	const double sw_g = (a.hyp_uniform ? a.hyp0 : a.hyp[(size_t)a.attr_group[j] * a.hyp_stride]);
 	const bool go = w_post(st.x, st.y, sw_g, a.alpha, msj.x, msj.y, mu, sig, a.counters, threadIdx.x == 0);
+	// every wave has used the old value (v_post above) before it is overwritten: without the
+	// barrier a wave of this workgroup could still read the new one as its "old"
+	__syncthreads();
 	if (threadIdx.x == 0) a.ms[(size_t)j * a.ms_stride] = make_double2(mu, sig);
 	if (!go && !NEXT) return;
 	if (a.dup[j]) {

@@ -395,183 +395,6 @@ __global__ __launch_bounds__(BLOCK) void k_level_lord(const uint64_t *lcp, const
 	                                                a.first_level != 0, op);
 }
 
-// ---- one wave per column, records in registers ----------------------------------------------
-// k_level_lord gives every column a workgroup of VB threads, stages the run in LDS and pays
-// three block barriers and a serial posterior per column; on short columns (C3: ~400 rows, one
-// rank of C4 on 8 GPUs: ~100) those fixed costs and the few columns a CU holds at once (LDS:
-// 4 x 34 KB) leave HBM idle between a column's load and its scatter. Here one wave owns a
-// column and keeps the run in VGPRs:
-//   * load: wave instruction (g, u) reads 1 KB of the run, lane 4m+c piece c of record
-//     64g+16u+m (whole records per quad, as the LDS staging);
-//   * a quad transpose (two DPP exchange stages) leaves lane 4m+c with all four pieces of record
-//     64g+16c+m, so statistics and correction run on whole records in every lane;
-//   * the reduction reproduces k_level_lord's tree for the same VB bit for bit: record i belongs
-//     to virtual thread t = i mod VB (entries t, t+VB, ... added in order), virtual wave
-//     w = t / 64 = g mod (VB/64), lane l = i mod 64 = 16c + m; each virtual wave's xor butterfly
-//     over l runs on the physical lanes with l's bits mapped to L's (l^32 = L^2, l^16 = L^1,
-//     l^8 = L^32, l^4 = L^16, l^2 = L^8, l^1 = L^4), then the virtual waves add in order;
-//   * the posterior is wave-uniform (no barrier), the transpose is undone and every quad writes
-//     its record whole to the next level's order (the destination broadcast in the quad).
-// A run longer than G*64 records is swept twice per chunk of G*64 (statistics, then reload and
-// move), in the same order. Bit-identical to k_level_lord<VB, *> (only VB decides the tree).
-template <int CTRL> DEVI double dpp_d(double v)
-{
-	const int lo = __builtin_amdgcn_mov_dpp(__double2loint(v), CTRL, 0xF, 0xF, false);
-	const int hi = __builtin_amdgcn_mov_dpp(__double2hiint(v), CTRL, 0xF, 0xF, false);
-	return __hiloint2double(hi, lo);
-}
-
-template <int CTRL> DEVI double2 dpp_d2(double2 v) { return make_double2(dpp_d<CTRL>(v.x), dpp_d<CTRL>(v.y)); }
-
-DEVI double2 sel2(bool s, double2 a, double2 b) { return s ? a : b; }
-
-// the value of quad lane U in every lane of the quad
-template <int U> DEVI uint32_t quad_bcast(uint32_t v)
-{
-	return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, U * 0x55, 0xF, 0xF, false);
-}
-
-// quad transpose of four 16-B registers: lane c of a quad, register u <-> lane u, register c
-// (stage 1 swaps across lane bit 0 / register bit 0, stage 2 across bit 1; its own inverse)
-DEVI void quad_transpose(double2 (&v)[4], uint32_t c)
-{
-	constexpr int X1 = 0xB1, X2 = 0x4E;   // quad_perm [1,0,3,2], [2,3,0,1]
-	const bool b0 = c & 1, b1 = (c >> 1) & 1;
-	{
-		const double2 ra = dpp_d2<X1>(sel2(b0, v[0], v[1]));
-		const double2 rb = dpp_d2<X1>(sel2(b0, v[2], v[3]));
-		if (b0) { v[0] = ra; v[2] = rb; } else { v[1] = ra; v[3] = rb; }
-	}
-	{
-		const double2 ra = dpp_d2<X2>(sel2(b1, v[0], v[2]));
-		const double2 rb = dpp_d2<X2>(sel2(b1, v[1], v[3]));
-		if (b1) { v[0] = ra; v[1] = rb; } else { v[2] = ra; v[3] = rb; }
-	}
-}
-
-// xor butterfly over the virtual lane l = 16 (L & 3) + (L >> 2), in wave_sum's order of l offsets
-DEVI double wave_sum_perm(double v)
-{
-	v += __shfl_xor(v, 2, 64);    // l ^ 32
-	v += __shfl_xor(v, 1, 64);    // l ^ 16
-	v += __shfl_xor(v, 32, 64);   // l ^ 8
-	v += __shfl_xor(v, 16, 64);   // l ^ 4
-	v += __shfl_xor(v, 8, 64);    // l ^ 2
-	v += __shfl_xor(v, 4, 64);    // l ^ 1
-	return v;
-}
-
-// buffer descriptors of one column's run (wave-uniform inputs: no waterfall loops); loads past
-// the run return zeros, so no index is clamped and every load takes an immediate offset
-DEVI __amdgpu_buffer_rsrc_t wave_rsrc(const void *p, uint32_t bytes)
-{
-	return __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(p), (short)0, (int)bytes, 0x00020000);
-}
-
-// G groups of 64 records from record `base` on: group g, instruction u = lane 4m+c reads piece
-// c of record 64g+16u+m (1 KB per wave instruction)
-template <int G>
-DEVI void wave_load(double2 (&r)[G][4], __amdgpu_buffer_rsrc_t rs, uint32_t base, uint32_t ng, uint32_t lane)
-{
-#pragma unroll
-	for (int g = 0; g < G; ++g) {
-		if ((uint32_t)g < ng) {
-#pragma unroll
-			for (int u = 0; u < 4; ++u)
-				r[g][u] = __builtin_bit_cast(double2, __builtin_amdgcn_raw_buffer_load_b128(
-				                                          rs, lane * 16, base * 64 + 1024 * (4 * g + u), 0));
-		}
-	}
-}
-
-template <int VB, int G, int WPB, bool IS_W, int P, bool NEXT>
-__global__ __launch_bounds__(64 * WPB) void k_level_wave(LevelArgs a)
-{
-	constexpr int NW = VB / 64;      // virtual waves of k_level_lord<VB>
-	constexpr uint32_t CAPW = 64u * G;
-	static_assert(G % NW == 0, "a chunk of G groups must hold whole rounds of the virtual waves");
-	const uint32_t col = blockIdx.x * WPB + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-	if (col >= a.nfeat) return;
-	const uint32_t lane = threadIdx.x & 63, c = lane & 3, m = lane >> 2;
-	const uint32_t j = level_feat(a, col);
-	const uint64_t sb = a.lcp[col];
-	const uint32_t n = (uint32_t)(a.lcp[col + 1] - sb);
-	if (a.long_min && n > a.long_min) return;      // a long column: the segment kernels'
-	const __amdgpu_buffer_rsrc_t rs = wave_rsrc(a.src + (sb - a.lbase), n * 64);
-	const __amdgpu_buffer_rsrc_t rn = wave_rsrc(a.lnext + sb, n * 4);
-	const __amdgpu_buffer_rsrc_t rx = wave_rsrc(a.lx ? (const void *)(a.lx + sb) : (const void *)(a.lnext + sb), n * 4);
-	const bool has_x = a.lx != nullptr;            // null: every x is 1 (lx not stored)
-	const double2 msj = a.ms[(size_t)j * a.ms_stride];
-	VbOp<IS_W, P, NEXT> op;
-	op.mo = msj.x; op.so = msj.y;
-	op.nx = NEXT ? a.ms_next[(size_t)j * a.ms_stride_next] : make_double2(0.0, 0.0);
-	const double hyp = a.hyp_uniform ? a.hyp0 : a.hyp[(size_t)a.attr_group[j] * a.hyp_stride];
-	const bool first = a.first_level != 0;
-	const uint32_t lrec = 16 * c + m;              // this lane's record within a group of 64
-
-	double s1[NW], s2[NW];
-#pragma unroll
-	for (int w = 0; w < NW; ++w) { s1[w] = 0.0; s2[w] = 0.0; }
-	double2 r[G][4];
-	float xr[G];
-	uint32_t nr[G];
-	const bool resident = n <= CAPW;
-	auto load_payload = [&](uint32_t base, bool want_next) {
-#pragma unroll
-		for (int g = 0; g < G; ++g) {
-			const uint32_t off = (64u * g + lrec) * 4;
-			nr[g] = want_next ? __builtin_amdgcn_raw_buffer_load_b32(rn, off, base * 4, 0) : 0u;
-			xr[g] = has_x ? __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rx, off, base * 4, 0)) : 1.0f;
-		}
-	};
-	// pass 1: statistics (a resident run stays in registers for the move)
-	for (uint32_t base = 0; base < n; base += CAPW) {
-		const uint32_t mm = min(CAPW, n - base), ng = (mm + 63) / 64;
-		load_payload(base, resident);
-		wave_load<G>(r, rs, base, ng, lane);
-#pragma unroll
-		for (int g = 0; g < G; ++g) {
-			if ((uint32_t)g < ng) {
-				quad_transpose(r[g], c);
-				// global group base/64 + g: virtual wave (base/64 + g) mod NW = g mod NW (base is a
-				// multiple of 64G and G of NW)
-				if (64u * g + lrec < mm) op.stat(r[g], xr[g], s1[g % NW], s2[g % NW]);
-			}
-		}
-	}
-	double t1 = wave_sum_perm(s1[0]), t2 = wave_sum_perm(s2[0]);
-#pragma unroll
-	for (int w = 1; w < NW; ++w) {
-		t1 += wave_sum_perm(s1[w]);
-		t2 += wave_sum_perm(s2[w]);
-	}
-	op.go = vb_post<IS_W>(t1, t2, hyp, a.alpha, op.mo, op.so, op.mu, op.sig, a.counters, lane == 0);
-	if (lane == 0) a.ms[(size_t)j * a.ms_stride] = make_double2(op.mu, op.sig);
-	// pass 2: correction and move (a non-resident run is reloaded chunk by chunk)
-	double2 *d = reinterpret_cast<double2 *>(a.dst);
-	for (uint32_t base = 0; base < n; base += CAPW) {
-		const uint32_t mm = min(CAPW, n - base), ng = (mm + 63) / 64;
-		if (!resident) {
-			load_payload(base, true);
-			wave_load<G>(r, rs, base, ng, lane);
-		}
-#pragma unroll
-		for (int g = 0; g < G; ++g) {
-			if ((uint32_t)g < ng) {
-				if (!resident) quad_transpose(r[g], c);
-				if (64u * g + lrec < mm) op.apply(r[g], xr[g], first);
-				quad_transpose(r[g], c);
-				// record 64g + 16u + m: its destination sits in quad lane u (full-record layout)
-				const uint32_t dn[4] = {quad_bcast<0>(nr[g]), quad_bcast<1>(nr[g]), quad_bcast<2>(nr[g]),
-				                        quad_bcast<3>(nr[g])};
-#pragma unroll
-				for (int u = 0; u < 4; ++u)
-					if (64u * g + 16u * u + m < mm) d[(size_t)dn[u] * 4 + c] = r[g][u];
-			}
-		}
-	}
-}
-
 // Long columns (skewed data: a popular item): one workgroup would stream the whole run while
 // the rest of the level is long done. Their runs are cut into segments, one workgroup each:
 // k_lord_long_stats writes each segment's statistics (and the column's parameters before the
@@ -666,6 +489,9 @@ __global__ __launch_bounds__(BLOCK) void k_level_lord_move(LevelArgs a)
 	op.nx = NEXT ? a.ms_next[(size_t)j * a.ms_stride_next] : make_double2(0.0, 0.0);
 	const double hyp = (a.hyp_uniform ? a.hyp0 : a.hyp[(size_t)a.attr_group[j] * a.hyp_stride]);
 	op.go = vb_post<IS_W>(st.x, st.y, hyp, a.alpha, op.mo, op.so, op.mu, op.sig, a.counters, threadIdx.x == 0);
+	// every wave has used the old value (v_post above) before it is overwritten: without the
+	// barrier a wave of this workgroup could still read the new one as its "old"
+	__syncthreads();
 	if (threadIdx.x == 0) a.ms[(size_t)j * a.ms_stride] = make_double2(op.mu, op.sig);
 	lord_move<BLOCK, CAP, VbOp<IS_W, P, NEXT>, ENT>(recs, dsts, a.src + (sb - a.lbase), a.lx ? a.lx + sb : nullptr,
 	                                                a.lnext + sb, n, false, a.dst, a.first_level != 0, op);
@@ -726,6 +552,9 @@ __global__ __launch_bounds__(BLOCK) void k_mc_level_lord(McArgs a)
 		const uint32_t g = mc_group(a, j);
 		op.go = mc_draw(sm, ss, op.vo, mc_lambda(a, g), mc_mu(a, g), a.alpha,
 		                mc_z(a, j), a.z != nullptr, a.sample, !IS_W, op.v, a.counters, threadIdx.x == 0);
+		// MODE 2: every wave has used the old value (the draw) before it is overwritten (no
+		// barrier since the kernel began; without one a wave could read the new value as "old")
+		if constexpr (MODE == 2) __syncthreads();
 		if (threadIdx.x == 0) a.par[(size_t)j * a.stride].x = op.v;
 		lord_move<BLOCK, CAP, McOp<IS_W, P, NEXT>, ENT>(recs, dsts, src, lx, a.lnext + sb, n, false, a.dst,
 		                                                a.first_level != 0, op);
@@ -910,43 +739,6 @@ __global__ __launch_bounds__(256) void k_estore_build(const uint64_t *row_ptr, c
 	lfirst[r] = s0;
 }
 
-// one wave per column (k_level_wave / k_defer_wave) for the 256-thread shapes' levels with
-// VBFM_WAVE=1 (default 0: k_level_lord / k_lord_defer, measured faster or equal), VBFM_WAVE_WPB sets the columns (waves) per workgroup (1 or 4). Read at every
-// launch (a getenv per level launch is far below a launch's cost) so that tests can switch.
-static int wave_mode()
-{
-	const char *e = getenv("VBFM_WAVE");
-	return e ? atoi(e) : 0;
-}
-
-static int wave_wpb()
-{
-	const char *e = getenv("VBFM_WAVE_WPB");
-	return e && atoi(e) == 1 ? 1 : 4;
-}
-
-template <int VB, int G, int WPB, bool IS_W, int P, bool NEXT>
-void launch_wave_g(const LevelArgs &a, hipStream_t s)
-{
-	k_level_wave<VB, G, WPB, IS_W, P, NEXT><<<(a.nfeat + WPB - 1) / WPB, 64 * WPB, 0, s>>>(a);
-}
-
-// registers for G*64 records: the level's mean column plus ~3 standard deviations of the
-// binomial spread fits (runs that do not are swept in chunks, the same results); VB: the
-// workgroup kernel's BLOCK for the level (128 or 256), whose reduction tree the wave reproduces
-template <int VB, bool IS_W, int P, bool NEXT>
-void launch_wave(const LevelArgs &a, hipStream_t s)
-{
-	const bool g4 = a.avg_len <= 200;
-	if (wave_wpb() == 1) g4 ? launch_wave_g<VB, 4, 1, IS_W, P, NEXT>(a, s) : launch_wave_g<VB, 8, 1, IS_W, P, NEXT>(a, s);
-	else g4 ? launch_wave_g<VB, 4, 4, IS_W, P, NEXT>(a, s) : launch_wave_g<VB, 8, 4, IS_W, P, NEXT>(a, s);
-}
-
-// the wave kernels address a column's run through 32-bit buffer descriptors (num_records = run x
-// 64 B, soffset = chunk base x 64 B): a level whose longest column has 2^25 records or more (a
-// skewed shard) keeps the workgroup kernels
-constexpr uint32_t WAVE_MAX_RUN = (1u << 25) - 1;
-
 // The leading (preloaded, -amdgpu-kernarg-preload-count) arguments of k_level_lord: everything the
 // loads of a column's bounds and parameters need, so they issue at wave start. On field data ms
 // arrives offset to the level's first feature (feats null: the column's index is blockIdx.x)
@@ -977,11 +769,6 @@ inline LordLead lord_lead(const LevelArgs &a)
 template <bool IS_W, int P, bool NEXT>
 void launch_lord(const LevelArgs &a, hipStream_t s)
 {
-	if (!a.ent && wave_mode() && a.avg_len > shape_small_max() && a.avg_len <= 640 && a.max_len <= WAVE_MAX_RUN) {
-		if (shape_block(a.avg_len) == 128) launch_wave<128, IS_W, P, NEXT>(a, s);
-		else launch_wave<256, IS_W, P, NEXT>(a, s);
-		return;
-	}
 	const LordLead L = lord_lead(a);
 	dispatch_shape(a.avg_len, [&](auto B, auto R) {
 		if (a.ent) k_level_lord<B(), R(), IS_W, P, NEXT, true><<<a.nfeat, B(), 0, s>>>(LORD_LEAD_ARGS(L), a);
@@ -1164,88 +951,6 @@ __global__ __launch_bounds__(BLOCK) void k_lord_defer(LevelArgs a)
 	if (threadIdx.x == 0) a.stats[blockIdx.x] = make_double2(s1, s2);
 }
 
-// k_lord_defer as one wave per column (the layout and reduction tree of k_level_wave): the
-// record's pending correction, this level's q-cache term, this level's statistics and the move
-// need nothing from this level's posterior, so a run is swept in one pass, chunk by chunk (G*64
-// records: the payloads, the records and the posteriors their payloads name in flight together),
-// and only the statistics leave the wave (lane 0). Field store only (not ENT). Bit-identical to
-// k_lord_defer<VB, *> and, through the deferred split's arithmetic, to the fused kernels.
-template <int VB, int G, int WPB, bool IS_W, int P, bool NEXT, int PK, bool PAY8>
-__global__ __launch_bounds__(64 * WPB) void k_defer_wave(LevelArgs a)
-{
-	constexpr int NW = VB / 64;
-	constexpr uint32_t CAPW = 64u * G, PB = PAY8 ? 8 : 16;   // payload bytes per entry
-	static_assert(G % NW == 0, "a chunk of G groups must hold whole rounds of the virtual waves");
-	const uint32_t col = blockIdx.x * WPB + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-	if (col >= a.nfeat) return;
-	const uint32_t lane = threadIdx.x & 63, c = lane & 3, m = lane >> 2;
-	const uint32_t j = level_feat(a, col);
-	const uint64_t sb = a.lcp[col];
-	const uint32_t n = (uint32_t)(a.lcp[col + 1] - sb);
-	const __amdgpu_buffer_rsrc_t rs = wave_rsrc(a.src + (sb - a.lbase), n * 64);
-	const __amdgpu_buffer_rsrc_t rp = wave_rsrc(PAY8 ? (const void *)(a.lpay2 + sb) : (const void *)(a.lpay + sb), n * PB);
-	const double2 msj = a.ms[(size_t)j * a.ms_stride];
-	VbOp<IS_W, P, NEXT> op;
-	op.mo = msj.x; op.so = msj.y;
-	const double2 nx = NEXT ? a.ms_next[(size_t)j * a.ms_stride_next] : make_double2(0.0, 0.0);
-	const bool first = a.first_level != 0;
-	const bool pending = (a.pending & 1) != 0;
-	const uint32_t lrec = 16 * c + m;
-	double2 *d = reinterpret_cast<double2 *>(a.dst);
-	double s1[NW], s2[NW];
-#pragma unroll
-	for (int w = 0; w < NW; ++w) { s1[w] = 0.0; s2[w] = 0.0; }
-	for (uint32_t base = 0; base < n; base += CAPW) {
-		const uint32_t mm = min(CAPW, n - base), ng = (mm + 63) / 64;
-		uint4 q[G];
-#pragma unroll
-		for (int g = 0; g < G; ++g) {
-			const uint32_t off = (64u * g + lrec) * PB;
-			if constexpr (PAY8) {
-				const uint2 w = __builtin_bit_cast(uint2, __builtin_amdgcn_raw_buffer_load_b64(rp, off, base * PB, 0));
-				q[g] = make_uint4(0x3f800000u, w.x, w.y, 0x3f800000u);
-			} else {
-				q[g] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rp, off, base * PB, 0));
-			}
-		}
-		double2 r[G][4];
-		wave_load<G>(r, rs, base, ng, lane);
-		// past the run the payloads read as zeros: tab[0] (a.tab always holds a level's width)
-		PostT t[G];
-#pragma unroll
-		for (int g = 0; g < G; ++g) t[g] = a.tab[q[g].z];
-#pragma unroll
-		for (int g = 0; g < G; ++g) {
-			if ((uint32_t)g < ng) {
-				quad_transpose(r[g], c);
-				if (64u * g + lrec < mm) {
-					const float x = __uint_as_float(q[g].x), px = __uint_as_float(q[g].w);
-					if (pending) {
-						if constexpr (PK == 0) apply_pending<IS_W, P>(r[g], t[g], px);
-						else if constexpr (PK == 1) apply_pending<false, 1 - P>(r[g], t[g], px);
-						else apply_pending<true, 0>(r[g], t[g], px);
-					}
-					if constexpr (NEXT) add_next_q<IS_W, P>(r[g], x, first, nx);
-					op.stat(r[g], x, s1[g % NW], s2[g % NW]);
-				}
-				quad_transpose(r[g], c);
-				const uint32_t dn[4] = {quad_bcast<0>(q[g].y), quad_bcast<1>(q[g].y), quad_bcast<2>(q[g].y),
-				                        quad_bcast<3>(q[g].y)};
-#pragma unroll
-				for (int u = 0; u < 4; ++u)
-					if (64u * g + 16u * u + m < mm) d[(size_t)dn[u] * 4 + c] = r[g][u];
-			}
-		}
-	}
-	double t1 = wave_sum_perm(s1[0]), t2 = wave_sum_perm(s2[0]);
-#pragma unroll
-	for (int w = 1; w < NW; ++w) {
-		t1 += wave_sum_perm(s1[w]);
-		t2 += wave_sum_perm(s2[w]);
-	}
-	if (lane == 0) a.stats[col] = make_double2(t1, t2);
-}
-
 // posteriors of the level's features from the all-reduced statistics (update_v :597-619 /
 // update_w :540-565): parameters, and the table the next level's kernel reads
 template <bool IS_W, bool NEXT>
@@ -1337,24 +1042,6 @@ __global__ __launch_bounds__(256) void k_lord_prev_fill(const uint32_t *feats, c
 template <bool IS_W, int P, bool NEXT, int PK, bool ENT>
 void launch_defer_shape(const LevelArgs &a, hipStream_t s)
 {
-	if constexpr (!ENT) {
-		if (wave_mode() && a.avg_len > shape_small_max() && a.avg_len <= 640 && a.max_len <= WAVE_MAX_RUN) {
-			// k_defer_wave with the workgroup kernel's BLOCK as its virtual block (128 or 256)
-			const unsigned wpb = wave_wpb(), gr = (a.nfeat + wpb - 1) / wpb;
-			auto go = [&](auto VB) {
-				if (a.lpay2) {
-					if (wpb == 1) k_defer_wave<VB(), 4, 1, IS_W, P, NEXT, PK, true><<<gr, 64, 0, s>>>(a);
-					else k_defer_wave<VB(), 4, 4, IS_W, P, NEXT, PK, true><<<gr, 256, 0, s>>>(a);
-				} else {
-					if (wpb == 1) k_defer_wave<VB(), 4, 1, IS_W, P, NEXT, PK, false><<<gr, 64, 0, s>>>(a);
-					else k_defer_wave<VB(), 4, 4, IS_W, P, NEXT, PK, false><<<gr, 256, 0, s>>>(a);
-				}
-			};
-			if (shape_block(a.avg_len) == 128) go(std::integral_constant<int, 128>());
-			else go(std::integral_constant<int, 256>());
-			return;
-		}
-	}
 	if (a.lpay2) {   // every x 1: 8-B payloads
 		dispatch_shape(a.avg_len, [&](auto B, auto R) {
 			k_lord_defer<B(), R(), IS_W, P, NEXT, PK, true, ENT><<<a.nfeat, B(), 0, s>>>(a);

@@ -103,6 +103,8 @@ __global__ __launch_bounds__(BLOCK) void k_mc_v_level(McArgs a)
 	double v;
 	const bool go = mc_draw(sm, ss, vo, mc_lambda(a, g), mc_mu(a, g), a.alpha,
 	                        mc_z(a, j), a.z != nullptr, a.sample, true, v, a.counters, threadIdx.x == 0);
+	// MODE 2: every wave has used the old value (the draw) before it is overwritten
+	if constexpr (MODE == 2) __syncthreads();
 	if (threadIdx.x == 0) a.par[(size_t)j * a.stride].x = v;
 	if (!go && !NEXT && !a.pk) return;
 	auto entry = [&](uint2 ent) {
@@ -159,6 +161,8 @@ __global__ __launch_bounds__(BLOCK) void k_mc_w_level(McArgs a)
 	double w;
 	const bool go = mc_draw(sm, ss, wo, mc_lambda(a, g), mc_mu(a, g), a.alpha,
 	                        mc_z(a, j), a.z != nullptr, a.sample, false, w, a.counters, threadIdx.x == 0);
+	// MODE 2: every wave has used the old value (the draw) before it is overwritten
+	if constexpr (MODE == 2) __syncthreads();
 	if (threadIdx.x == 0) a.par[(size_t)j * a.stride].x = w;
 	if (!go && !NEXT) return;
 	if (a.dup[j]) {

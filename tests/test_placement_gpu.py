@@ -26,7 +26,7 @@ def _data(n=N_ROWS, F=3, S=2100, seed=41):
 
 
 def _run(env, monkeypatch, k=2, cfg=None, data=None, fail_first=None):
-    for kk in ("VBFM_PLACE", "VBFM_PLACE_TRIES", "VBFM_PLACE_BUDGET_GB", "VBFM_LAYOUT", "VBFM_WAVE", "VBFM_FAULT"):
+    for kk in ("VBFM_PLACE", "VBFM_PLACE_TRIES", "VBFM_PLACE_BUDGET_GB", "VBFM_LAYOUT", "VBFM_FAULT"):
         monkeypatch.delenv(kk, raising=False)
     for kk, vv in env.items():
         monkeypatch.setenv(kk, vv)
@@ -123,7 +123,7 @@ def test_placement_failure_frees_candidates_and_rebuilds(monkeypatch):
     import torch
     data = _data()
     ref, _, _ = _run({"VBFM_PLACE": "0"}, monkeypatch, data=data)
-    for kk in ("VBFM_PLACE", "VBFM_LAYOUT", "VBFM_WAVE"):
+    for kk in ("VBFM_PLACE", "VBFM_LAYOUT"):
         monkeypatch.delenv(kk, raising=False)
     monkeypatch.setenv("VBFM_PLACE_TRIES", "24")
     train, test, D, lo, hi = data

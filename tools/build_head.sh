@@ -1,13 +1,13 @@
 #!/bin/bash
 # Build libvbfm.so of a committed tree (default HEAD) into tools/ab_head/lib for interleaved A/B
 # against the working tree's product library (VBFM_LIB=tools/ab_head/lib/libvbfm.so).
-# usage: tools/build_head.sh [<commit>]
+# usage: tools/build_head.sh [<commit> [<outdir>]]
 set -e
 cd "$(dirname "$0")/.."
 C=${1:-HEAD}
 T=$(mktemp -d)
 git archive "$C" scalable-variational-bayesian-factorization-machine_amd/csrc include | tar -x -C "$T"
-O=tools/ab_head
+O=${2:-tools/ab_head}
 rm -rf $O && mkdir -p $O/build $O/lib
 P=$T/scalable-variational-bayesian-factorization-machine_amd
 F="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -Wall -Wno-unused-function -I/opt/rocm/include -mllvm -amdgpu-kernarg-preload-count=16"
