@@ -271,12 +271,13 @@ def shard_plan(rows, world, rank, mode):
     return {"rows": hi - lo, "row_offset": lo, "rows_total": rows}
 
 
-def launch_event_stride(levels, k, limit=8000):
-    """Time every stride-th level launch: 1 up to `limit` launches per iteration, else the
-    smallest stride >= 16 coprime with the level count (every level sampled alike)."""
-    if levels * k <= limit:
-        return 1
-    stride = 16
+def launch_event_stride(levels, k, samples=500):
+    """Time every stride-th level launch, about `samples` launches per iteration: the smallest
+    stride >= launches / samples that is coprime with the level count (every level sampled
+    alike). An event pair opens a gap of ~5 us of device time between two launches (kernel
+    trace of the multi-hot bench, profiles/r05_multihot/events/): timing every 16th of its 39,250
+    launches per iteration cost 59 ms of a 644-ms iteration, every 79th costs ~0.1 %."""
+    stride = max(1, -(-levels * k // samples))
     while math.gcd(stride, levels) != 1:
         stride += 1
     return stride
@@ -477,9 +478,9 @@ def main():
         fml.init_caches()
     launch_events = not online and not args.no_launch_events
     if launch_events:   # per-launch event pairs: the online epoch has num_batch * k * levels launches
-        # short level launches (many levels): an event pair costs up to ~4.5 us of device time
-        # on some boxes, so time a sample -- every stride-th launch, stride coprime with the
-        # level count so that every level is sampled alike
+        # an event pair costs ~5 us of device time, so time a sample of ~500 launches per
+        # iteration -- every stride-th launch, stride coprime with the level count so that every
+        # level is sampled alike
         fml.set_profiling(True, launch_event_stride(fml.levels()[1], k))
     layout = fml.layout()
     nnz = fml.shape(0)[2]                # this rank's train entries
