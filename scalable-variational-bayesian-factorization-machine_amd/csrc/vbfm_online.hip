@@ -490,16 +490,23 @@ __global__ void k_ov_pad_check(const uint64_t *gptr, const uint32_t *lptr, const
 // are read and written directly.
 constexpr uint32_t OV_CAP = 512;
 
-// Diagnostic build only (tools/ov_stamps.sh, -DVBFM_OV_STAMPS; never in lib/libvbfm.so): thread 0 of
-// every workgroup of one chosen level launch writes the 100-MHz real-time counter at five points
-// (entry, staged, posterior, corrected, stores issued) to a buffer of its own
+// Diagnostic build only (tools/ov_stamps.sh, -DVBFM_OV_STAMPS; never in lib/libvbfm.so): every wave
+// reads the 100-MHz real-time counter at five points (entry, staged, posterior, corrected, stores
+// issued) into registers; at the end thread 0 of every workgroup of one chosen level launch writes
+// them to a buffer of its own (only then is the buffer's address needed, so the stamps do not hold
+// the entry up on a kernarg load)
 #ifdef VBFM_OV_STAMPS
-#define OV_STAMP(i)                                                                                    \
+#define OV_STAMP_DECL unsigned long long ov_st_[5] = {0, 0, 0, 0, 0}
+#define OV_STAMP(i) (ov_st_[i] = __builtin_amdgcn_s_memrealtime())
+#define OV_STAMP_FLUSH                                                                                 \
 	do {                                                                                               \
-		if (a.stamp && threadIdx.x == 0) a.stamp[(size_t)blockIdx.x * 5 + (i)] = __builtin_amdgcn_s_memrealtime(); \
+		if (a.stamp && threadIdx.x == 0)                                                               \
+			for (int i_ = 0; i_ < 5; ++i_) a.stamp[(size_t)blockIdx.x * 5 + i_] = ov_st_[i_];           \
 	} while (0)
 #else
+#define OV_STAMP_DECL do {} while (0)
 #define OV_STAMP(i) do {} while (0)
+#define OV_STAMP_FLUSH do {} while (0)
 #endif
 
 DEVI uint32_t ov_slot(uint32_t i, uint32_t c) { return i * 4 + (c ^ ((i >> 2) & 3)); }
@@ -533,6 +540,7 @@ __global__ __launch_bounds__(256) void k_ov_lord(const uint64_t *__restrict__ co
 	static_assert(!FAST || (PAD && !IS_W), "the tagged arguments serve the v sweep's padded levels");
 	__shared__ double2 stage[OV_CAP * 4];
 	__shared__ uint32_t dsts[OV_CAP];
+	OV_STAMP_DECL;
 	OV_STAMP(0);
 	const uint64_t *col_ptr = FAST ? ov_untag(col_ptr_t) : col_ptr_t;
 	const RowRec *src = FAST ? ov_untag(src_t) : src_t;
@@ -745,6 +753,7 @@ __global__ __launch_bounds__(256) void k_ov_lord(const uint64_t *__restrict__ co
 		__builtin_nontemporal_store(w, d + (size_t)dsts[t >> 2] * 4 + (t & 3));
 	}
 	OV_STAMP(4);
+	OV_STAMP_FLUSH;
 }
 
 inline unsigned grid_of(uint64_t n, unsigned block = 256) { return (unsigned)((n + block - 1) / block); }
