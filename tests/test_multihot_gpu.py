@@ -62,13 +62,19 @@ def test_multihot_two_iterations_vs_oracle(k, layout):
     assert rel_err(g.get_params()["mu_v"], o.params()["mu_v"]) <= REL
 
 
+# rows of the small multi-hot sets: 20,000 give ~143-entry columns (the 256 x 1 workgroup shape),
+# 45,000 ~320-entry columns (128 x 3, dispatch_shape in csrc/vbfm_device.h)
+SHAPE_ROWS = [20_000, 45_000]
+
+
+@pytest.mark.parametrize("n", SHAPE_ROWS)
 @pytest.mark.parametrize("xmode", [0, 1])
-def test_entry_store_equals_column_layout(xmode):
+def test_entry_store_equals_column_layout(xmode, n):
     """The entry store sweeps every column's entries in the column layout's order with the same
     per-thread assignment and reduction tree, and the data-set sums (w0, alpha, free energy,
     train quirk) add the rows in row order on both: the two layouts agree bit for bit over three
-    iterations (x = 1 without a stored x array, and x ~ U(0.5, 1.5))."""
-    n, D, lo, hi, k = 20_000, 3000, 3, 40, 4
+    iterations (x = 1 without a stored x array, and x ~ U(0.5, 1.5)), at two workgroup shapes."""
+    D, lo, hi, k = 3000, 3, 40, 4
     res = {}
     for layout in ("entry", "column"):
         g = vbfm.FMLearnVB(1, 1, k, D + 1, min_target=1.0, max_target=5.0, layout=layout)
@@ -115,17 +121,19 @@ def test_entry_store_refused_where_it_cannot_apply(monkeypatch):
     assert g.layout() == "column"
 
 
+@pytest.mark.parametrize("n", SHAPE_ROWS)
 @pytest.mark.parametrize("xmode", [0, 1])
 @pytest.mark.parametrize("form", ["deferred", "two_pass", "rccl_chunks"])
-def test_entry_store_split_forms_equal_fused(form, xmode, monkeypatch):
+def test_entry_store_split_forms_equal_fused(form, xmode, n, monkeypatch):
     """The entry store under row shards (VBFM_FORCE_SPLIT=1 on one rank): deferred -- level l's
     kernel applies each record's pending correction (its row's previous entry, from any earlier
     level, through a posterior table over all level features; a row's first entry the previous
     sweep's carried one), reduces, moves; two_pass -- statistics, all-reduce, correction + move
     (VBFM_DEFER=0); rccl_chunks -- the deferred form through a 1-rank RCCL communicator with
     each level's exchange in 3 chunks. Every form equals the fused single-rank entry store bit
-    for bit over three iterations (the same per-column order of every sum)."""
-    n, D, lo, hi, k = 20_000, 3000, 3, 40, 4
+    for bit over three iterations (the same per-column order of every sum), at two workgroup
+    shapes."""
+    D, lo, hi, k = 3000, 3, 40, 4
 
     def run(split):
         monkeypatch.setenv("VBFM_FORCE_SPLIT", split)
@@ -175,3 +183,33 @@ def test_entry_store_split_mcmc_equals_fused(method, monkeypatch):
     fused, split = run("0"), run("1")
     assert split[0] == fused[0]
     np.testing.assert_array_equal(split[1], fused[1])
+
+
+def test_next_level_prefetch_changes_nothing(monkeypatch):
+    """The level kernel's touch of the next level's column bounds (VBFM_PREFETCH, default on) is a
+    load whose value is never used: the entry store and the field store run bit for bit as
+    without it."""
+    res = {}
+    for pf in ("1", "0"):
+        monkeypatch.setenv("VBFM_PREFETCH", pf)
+        g = vbfm.FMLearnVB(1, 1, 3, 3001, min_target=1.0, max_target=5.0, layout="entry")
+        g.init(7, 0.1)
+        g.synth_multihot(0, 45_000, 3000, 3, 40, 1000, 0)
+        g.synth_multihot(1, 2000, 3000, 3, 40, 500000, 0)
+        g.init_caches()
+        st = [g.iterate() for _ in range(2)]
+        res["entry", pf] = ([(s.rmse, s.free_energy) for s in st], g.get_params()["mu_v"])
+        g.close()
+        rp, f, v, y = synth.generate(30_000, 6, 100, 3, 0)
+        te = synth.generate(1000, 6, 100, 4, 0)
+        g = vbfm.FMLearnVB(1, 1, 3, 601, min_target=float(y.min()), max_target=float(y.max()), layout="level")
+        g.init(7, 0.1)
+        g.set_data(vbfm.DataSubset.from_csr(rp, f, v, y, 600), vbfm.DataSubset.from_csr(*te, 600))
+        g.init_caches()
+        assert g.layout() == "level"
+        st = [g.iterate() for _ in range(2)]
+        res["level", pf] = ([(s.rmse, s.free_energy) for s in st], g.get_params()["mu_v"])
+        g.close()
+    for lay in ("entry", "level"):
+        assert res[lay, "1"][0] == res[lay, "0"][0]
+        np.testing.assert_array_equal(res[lay, "1"][1], res[lay, "0"][1])
