@@ -755,3 +755,37 @@ def test_chunked_exchange_is_bit_identical(method, layout, monkeypatch):
     chunked = run("1", 4)
     assert chunked[0] == fused[0]
     np.testing.assert_array_equal(chunked[1], fused[1])
+
+
+def test_shape_128x3_forms_agree(monkeypatch):
+    """Field data of ~300-entry columns takes the 128 x 3 workgroup shape (dispatch_shape,
+    csrc/vbfm_device.h) in every kernel family. On the level store the fused kernel, the deferred
+    split and the two-pass split agree bit for bit; on the column layout the split's statistics
+    kernel takes the fused kernel's BLOCK, so split == fused bit for bit there too; the two
+    layouts agree within the data-set sums' row order (1e-12)."""
+    n, F, S, k = 30000, 6, 100, 4
+    rp, f, v, y = synth.generate(n, F, S, 23, 1)
+    rpt, ft, vt, yt = synth.generate(1000, F, S, 24, 1)
+    D = F * S + 1
+    res = {}
+    for layout, split, defer in (("level", "0", "1"), ("level", "1", "1"), ("level", "1", "0"),
+                                 ("column", "0", "1"), ("column", "1", "1")):
+        monkeypatch.setenv("VBFM_FORCE_SPLIT", split)
+        monkeypatch.setenv("VBFM_DEFER", defer)
+        g = vbfm.FMLearnVB(1, 1, k, D, min_target=float(y.min()), max_target=float(y.max()), layout=layout)
+        g.init(5, 0.1)
+        g.set_data(vbfm.DataSubset.from_csr(rp, f, v, y, F * S), vbfm.DataSubset.from_csr(rpt, ft, vt, yt, F * S))
+        g.init_caches()
+        assert g.layout() == layout
+        st = [g.iterate() for _ in range(3)]
+        res[layout, split, defer] = ([(s.rmse, s.free_energy) for s in st], np.asarray(g.get_params()["mu_v"]))
+        g.close()
+    base = res["level", "0", "1"]
+    for key in (("level", "1", "1"), ("level", "1", "0")):
+        assert res[key][0] == base[0], key
+        np.testing.assert_array_equal(res[key][1], base[1], err_msg=str(key))
+    col = res["column", "0", "1"]
+    assert res["column", "1", "1"][0] == col[0]
+    np.testing.assert_array_equal(res["column", "1", "1"][1], col[1])
+    close([x for t in col[0] for x in t], [x for t in base[0] for x in t], 1e-12)
+    close(col[1], base[1], 1e-12)

@@ -161,11 +161,13 @@ def test_entry_store_split_forms_equal_fused(form, xmode, n, monkeypatch):
     np.testing.assert_array_equal(split[2], fused[2])
 
 
+@pytest.mark.parametrize("n", [15_000, 45_000])
 @pytest.mark.parametrize("method", ["als", "mcmc"])
-def test_entry_store_split_mcmc_equals_fused(method, monkeypatch):
+def test_entry_store_split_mcmc_equals_fused(method, n, monkeypatch):
     """MCMC / ALS on the entry store under row shards (the two-pass split: statistics, all-reduce,
-    draw + move) with the device RNG streams: the fused single-rank chain bit for bit."""
-    n, D, lo, hi, k = 15_000, 2500, 3, 30, 3
+    draw + move) with the device RNG streams: the fused single-rank chain bit for bit, at two
+    workgroup shapes (~100- and ~300-entry columns: 64 x 2 and 128 x 3)."""
+    D, lo, hi, k = 2500, 3, 30, 3
 
     def run(split):
         monkeypatch.setenv("VBFM_FORCE_SPLIT", split)
