@@ -411,6 +411,37 @@ static void tune_placement(vbfm_ctx *c)
 		std::vector<size_t> order(cand.size());
 		for (size_t i = 0; i < order.size(); i++) order[i] = i;
 		std::stable_sort(order.begin(), order.end(), [&](size_t x, size_t y) { return ms[x] < ms[y]; });
+		// the store ping-pongs between its two buffers, so the best few are also scored as pairs:
+		// each level streams one and scatters into the other (VBFM_PLACE_PAIRS=<K>: the best K;
+		// 0: keep the best two singles)
+		const char *pp = getenv("VBFM_PLACE_PAIRS");
+		const size_t K = std::min<size_t>(pp ? (size_t)atoi(pp) : 6, order.size());
+		if (K > 2) {
+			auto score_pair = [&](RowRec *x, RowRec *y) {
+				HIPCHK(vbk::place_move(x, y, lp, c->lnext, nfl, c->s));   // warm-up
+				HIPCHK(hipEventRecord(e0, c->s));
+				for (int r = 0; r < 2; r++) {
+					HIPCHK(vbk::place_move(x, y, lp, c->lnext, nfl, c->s));
+					HIPCHK(vbk::place_move(y, x, lp, c->lnext, nfl, c->s));
+				}
+				HIPCHK(hipEventRecord(e1, c->s));
+				HIPCHK(hipEventSynchronize(e1));
+				float t = 0.f;
+				HIPCHK(hipEventElapsedTime(&t, e0, e1));
+				return t;
+			};
+			float best = 0.f;
+			size_t ba = 0, bb = 1;
+			c->place_pair_ms.clear();
+			for (size_t a = 0; a < K; a++)
+				for (size_t b = a + 1; b < K; b++) {
+					const float t = score_pair(cand[order[a]], cand[order[b]]);
+					c->place_pair_ms.push_back(t);
+					if ((a == 0 && b == 1) || t < best) { best = t; ba = a; bb = b; }
+				}
+			std::swap(order[0], order[ba]);
+			std::swap(order[1], order[bb]);   // bb > ba >= 0: untouched by the first swap
+		}
 		// commit (nothing below the frees can throw before c->rows names a live buffer again)
 		for (size_t j = 2; j < order.size(); j++) dfree(cand[order[j]]);
 		c->rows = cand[order[0]];
@@ -446,6 +477,11 @@ static void tune_placement(vbfm_ctx *c)
 		fprintf(stderr, "vbfm placement: %u rows, level-0 pattern to and from a reference buffer x2:", n);
 		for (size_t i = 0; i < ms.size(); i++)
 			fprintf(stderr, " %.3f%s", ms[i], (i == order[0] || i == order[1]) ? "*" : "");
+		fprintf(stderr, " ms");
+		if (!c->place_pair_ms.empty()) {
+			fprintf(stderr, "; the best as pairs, both directions x2:");
+			for (float t : c->place_pair_ms) fprintf(stderr, " %.3f", t);
+		}
 		fprintf(stderr, " ms\n");
 	}
 }

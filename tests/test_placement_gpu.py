@@ -1,7 +1,9 @@
 """Record-buffer placement tuning of the level store (tune_placement, csrc/vbfm_capi.hip; DESIGN
 §5b): which physical buffers hold the records changes the level kernel's speed only, so a learner
 that tuned its placement must match one that did not, bit for bit, and the report
-(vbfm_placement_info) must name the two best-scored candidates. The search stays inside the
+(vbfm_placement_info) must name the kept pair: the best pair among the best-scored candidates
+(the store ping-pongs between two buffers, so the best few singles are scored again as pairs),
+or the best two singles with VBFM_PLACE_PAIRS=0. The search stays inside the
 caller's budget (vbfm_config place_candidates / place_budget_bytes) and half of the free device
 memory, degrades to fewer candidates (or none) when memory is short, and a failure inside it
 leaves no candidate allocated and the next call rebuilding the store (VBFM_FAULT=placement)."""
@@ -26,7 +28,8 @@ def _data(n=N_ROWS, F=3, S=2100, seed=41):
 
 
 def _run(env, monkeypatch, k=2, cfg=None, data=None, fail_first=None):
-    for kk in ("VBFM_PLACE", "VBFM_PLACE_TRIES", "VBFM_PLACE_BUDGET_GB", "VBFM_LAYOUT", "VBFM_FAULT"):
+    for kk in ("VBFM_PLACE", "VBFM_PLACE_TRIES", "VBFM_PLACE_BUDGET_GB", "VBFM_PLACE_PAIRS", "VBFM_LAYOUT",
+               "VBFM_FAULT"):
         monkeypatch.delenv(kk, raising=False)
     for kk, vv in env.items():
         monkeypatch.setenv(kk, vv)
@@ -62,7 +65,7 @@ def test_placement_is_bit_identical_and_reported(monkeypatch):
     assert p0 == ([], [-1, -1])
     assert s0["place_candidates"] == 0 and s0["place_bytes"] == 0 and s0["s_placement"] == 0
     assert s0["s_schedule"] > 0 and s0["s_store"] > 0 and s0["s_set_train"] > 0
-    got, (ms, kept), su = _run({"VBFM_PLACE_TRIES": "6"}, monkeypatch)
+    got, (ms, kept), su = _run({"VBFM_PLACE_TRIES": "6", "VBFM_PLACE_PAIRS": "3"}, monkeypatch)
     _same(got, ref)
     assert su["place_candidates"] == 6 and su["place_kept"] == kept
     assert su["place_bytes"] == 6 * REC_BYTES            # 4 fresh candidates + the stash + the reference
@@ -70,7 +73,11 @@ def test_placement_is_bit_identical_and_reported(monkeypatch):
     assert len(ms) == 6 and all(m > 0 for m in ms)
     assert kept[0] != kept[1] and all(0 <= i < 6 for i in kept)
     order = sorted(range(6), key=lambda i: ms[i])
-    assert ms[kept[0]] == ms[order[0]] and ms[kept[1]] == ms[order[1]]
+    assert set(kept) <= set(order[:3])                   # a pair among the best three singles
+    got2, (ms2, kept2), _ = _run({"VBFM_PLACE_TRIES": "6", "VBFM_PLACE_PAIRS": "0"}, monkeypatch)
+    _same(got2, ref)
+    order2 = sorted(range(6), key=lambda i: ms2[i])
+    assert ms2[kept2[0]] == ms2[order2[0]] and ms2[kept2[1]] == ms2[order2[1]]   # the best two singles
 
 
 def test_placement_budget_from_config(monkeypatch):
