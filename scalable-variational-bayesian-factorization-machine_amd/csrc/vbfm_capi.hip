@@ -944,11 +944,15 @@ void require_train(vbfm_ctx *c)
 	if (!c->sched_ready) build_schedule(c);
 }
 
-// VBFM_PREFETCH=0 (A/B): the level kernels do not touch the next level's column bounds
-static bool pf_enabled()
+// VBFM_PREFETCH=0 (A/B): the level kernels do not touch the next level's column bounds (read once
+// per context)
+static bool pf_enabled(vbfm_ctx *c)
 {
-	const char *e = getenv("VBFM_PREFETCH");
-	return !(e && e[0] == '0');
+	if (c->prefetch < 0) {
+		const char *e = getenv("VBFM_PREFETCH");
+		c->prefetch = (e && e[0] == '0') ? 0 : 1;
+	}
+	return c->prefetch != 0;
 }
 
 LevelArgs level_args(vbfm_ctx *c, uint32_t l, bool is_w, int f)
@@ -1032,7 +1036,7 @@ void sweep_level(vbfm_ctx *c, uint32_t l, bool is_w, int f)
 		a.lcp = c->lcp + c->level_ptr[l];
 		{   // the level after this one in launch order: l + 1, or level 0 of the next sweep
 			const uint32_t ln = l + 1 < nlevels(c) ? l + 1 : 0;
-			a.pf_lcp = pf_enabled() ? c->lcp + c->level_ptr[ln] : nullptr;
+			a.pf_lcp = pf_enabled(c) ? c->lcp + c->level_ptr[ln] : nullptr;
 			const bool contig = ln < c->level_base.size() && c->level_base[ln] != ~0u;
 			a.pf_feats = contig ? nullptr : c->level_feats + c->level_ptr[ln];
 			a.pf_n = a.pf_lcp ? c->level_ptr[ln + 1] - c->level_ptr[ln] : 0u;

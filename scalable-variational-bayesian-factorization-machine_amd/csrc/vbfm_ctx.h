@@ -142,6 +142,7 @@ struct vbfm_ctx {
 	std::vector<float> place_ms;    // tune_placement: each candidate buffer's score (ms), [0], [1] = the first pair
 	int place_pick[2] = {-1, -1};   // ... and the two kept (records, alternate)
 	std::vector<float> place_pair_ms;   // ... the best few scored as pairs (a < b in score order)
+	int prefetch = -1;              // the level kernels touch the next level's column bounds (VBFM_PREFETCH; -1: not read yet)
 	int place_cands_cfg = 0;        // vbfm_config::place_candidates / place_budget_bytes (0: defaults)
 	uint64_t place_budget_cfg = 0;
 	uint64_t place_bytes = 0;       // device memory the last search held at its peak

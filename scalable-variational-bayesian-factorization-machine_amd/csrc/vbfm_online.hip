@@ -942,6 +942,7 @@ struct OvState {
 	uint64_t pad_rows = 0;             // records a padded level's buffer needs (max over levels)
 	bool pad_on = false;               // the batch being processed uses the padded layout
 	bool fast = true;                  // v levels on it take k_ov_lord's tagged arguments (VBFM_OV_FAST)
+	bool legacy = false;               // A/B: the round-3 kernel's per-entry x and flag (VBFM_OV_LEGACY)
 	uint32_t cur_n = 0;                // its rows
 	uint64_t *lvl_d = nullptr;         // [num_batch * (L+1)] first entry of every level of every batch
 	std::vector<uint64_t> lvl_h;
@@ -1012,8 +1013,7 @@ void ov_launch_level(vbfm_ctx *c, LevelArgs &a, uint32_t l, bool is_w)
 	// levels: level 0 holds every row's first entry (the ROW_FIRST bit of its CSC entries)
 	a.first_level = l == 0 && a.first_mask != 0;
 	a.x_one = o.x_one;
-	const char *lg = getenv("VBFM_OV_LEGACY");   // A/B: x and the first-entry bit from the CSC per entry
-	if (lg && lg[0] == '1') {
+	if (o.legacy) {   // A/B (VBFM_OV_LEGACY=1): x and the first-entry bit from the CSC per entry
 		a.first_level = -1;
 		a.x_one = 0;
 	}
@@ -1405,6 +1405,8 @@ int vbfm_online_init(vbfm_ctx *c, const vbfm_online_config *cfg)
 					const char *pe = getenv("VBFM_OV_PAD");
 					const char *fe = getenv("VBFM_OV_FAST");   // A/B: 0 = the untagged arguments everywhere
 					o.fast = !(fe && fe[0] == '0');
+					const char *lg = getenv("VBFM_OV_LEGACY");
+					o.legacy = lg && lg[0] == '1';
 					if (!(pe && pe[0] == '0') && L > 1) {
 						const uint32_t cap = vbk::ov_pad_cap();
 						o.cpw_h.assign(L, 0);
