@@ -552,10 +552,13 @@ __global__ __launch_bounds__(256) void k_ov_lord(const uint64_t *__restrict__ co
 	// bound), the per-column loads below overlap them, the LDS writes come last (a load/write
 	// loop waits on every read before issuing the next)
 	constexpr int KS = OV_CAP * 4 / 256, KD = OV_CAP / 256;
-	// the slot's first KP rounds (320 records: the run is 256 +- 16 at C3's batch shape) and every
+	// the slot's first KP rounds (256 records: the run is 256 +- 16 at C3's batch shape) and every
 	// next position are loaded at once (PAD: before anything else); the rest only if the run is
-	// that long
-	constexpr int KP = 5;
+	// that long, once the column bounds are in -- inside the staging's bandwidth-bound wait, so
+	// the half of the workgroups that need a 5th round lose nothing by it, and every workgroup
+	// reads 64 fewer records (C3 epoch -0.7 % against KP = 5; 3: no gain; 4 plus half a round at
+	// once for 128 lanes: +1.7 %, profiles/r05_online/kp_ab/)
+	constexpr int KP = 4;
 	double2 sv[KS];
 	uint32_t dv[KD];
 	if constexpr (PAD) {
