@@ -558,7 +558,7 @@ __global__ __launch_bounds__(256) void k_ov_lord(const uint64_t *__restrict__ co
 	// the half of the workgroups that need a 5th round lose nothing by it, and every workgroup
 	// reads 64 fewer records (C3 epoch -0.7 % against KP = 5; 3: no gain; 4 plus half a round at
 	// once for 128 lanes: +1.7 %, profiles/r05_online/kp_ab/)
-	constexpr int KP = 4;
+	constexpr int KP = 4, KDP = 1;
 	double2 sv[KS];
 	uint32_t dv[KD];
 	if constexpr (PAD) {
@@ -570,7 +570,12 @@ __global__ __launch_bounds__(256) void k_ov_lord(const uint64_t *__restrict__ co
 			if (k < KP) sv[k] = s2[threadIdx.x + k * 256];
 		}
 #pragma unroll
-		for (int k = 0; k < KD; ++k) dv[k] = nx2[threadIdx.x + k * 256];
+		// the first 256 next positions at once, the rest with the records' later rounds (C3 epoch
+		// -0.7 % against both at once, profiles/r05_online/kp_ab/)
+		for (int k = 0; k < KD; ++k) {
+			dv[k] = 0;
+			if (k < KDP) dv[k] = nx2[threadIdx.x + k * 256];
+		}
 	}
 	const uint32_t c0 = blockIdx.x * (256 / G);
 	const uint32_t c1 = min(c0 + 256 / G, nfeat);
@@ -617,6 +622,9 @@ __global__ __launch_bounds__(256) void k_ov_lord(const uint64_t *__restrict__ co
 #pragma unroll
 		for (int k = KP; k < KS; ++k)
 			if (k < (int)ks) sv[k] = s2[threadIdx.x + k * 256];
+#pragma unroll
+		for (int k = KDP; k < KD; ++k)
+			if (k < (int)kd) dv[k] = nx2[threadIdx.x + k * 256];
 	} else {
 #pragma unroll
 		for (int k = 0; k < KS; ++k) {
