@@ -375,7 +375,7 @@ __global__ __launch_bounds__(BLOCK) void k_level_lord(const uint64_t *lcp, const
 		// it (the moves below are non-temporal on the entry store); the value is kept by a test
 		// that never holds, at the end
 		uint64_t pf = 0;
-		if (threadIdx.x == 0 && blockIdx.x < a.pf_n) {
+		if (blockIdx.x < a.pf_n) {   // uniform: scalar loads, whose counter the stores do not share
 			pf = a.pf_lcp[blockIdx.x];
 			if (a.pf_feats) pf += a.pf_feats[blockIdx.x];
 		}
