@@ -283,9 +283,13 @@ def launch_event_stride(levels, k, samples=500):
     return stride
 
 
-def spawn_ranks(n):
-    """Start n rank processes of this script (one per GPU) and wait for them. This process
-    never touches a GPU; each child gets the torchrun environment."""
+def spawn_ranks(n, grace_s=10.0):
+    """Start n rank processes of this script (one per GPU) and watch them. This process never
+    touches a GPU; each child gets the torchrun environment and a process group of its own. The
+    first rank that exits non-zero stops the run: the others -- which would otherwise wait in a
+    collective for it until the deadline -- get SIGTERM (their whole group: the CPU leg's
+    reference process with them), SIGKILL after grace_s, and that rank's status is returned."""
+    import signal
     import socket
     with socket.socket() as so:
         so.bind(("127.0.0.1", 0))
@@ -295,12 +299,48 @@ def spawn_ranks(n):
         env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
                    MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
         env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
-        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
-    codes = [p.wait() for p in procs]
-    bad = [c for c in codes if c != 0]
-    if bad:
-        log("bench.py: rank exit codes %s" % codes)
-    return bad[0] if bad else 0
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env,
+                                      start_new_session=True))
+    failed = None
+    while failed is None:
+        codes = [p.poll() for p in procs]
+        failed = next(((r, c) for r, c in enumerate(codes) if c not in (None, 0)), None)
+        if failed is None and all(c == 0 for c in codes):
+            return 0
+        if failed is None:
+            time.sleep(0.1)
+    rank, code = failed
+    log("bench.py: rank %d of %d exited with status %d; stopping the other ranks" % (rank, n, code))
+
+    def signal_all(sig):
+        for p in procs:
+            if p.poll() is None:
+                try:
+                    os.killpg(p.pid, sig)
+                except OSError:
+                    pass
+
+    signal_all(signal.SIGTERM)
+    end = time.time() + grace_s
+    while time.time() < end and any(p.poll() is None for p in procs):
+        time.sleep(0.1)
+    signal_all(signal.SIGKILL)
+    for p in procs:
+        p.wait()
+    log("bench.py: rank exit codes %s" % [p.returncode for p in procs])
+    return code if code > 0 else 128 - code     # a signal -s as the shell reports it (128 + s)
+
+
+def bench_fault_hook(rank):
+    """Test hook (tests/test_bench_cpu.py): VBFM_BENCH_FAULT=exit:R makes rank R exit with status
+    3 at start while every other rank hangs (sleeps) as it would in a collective waiting for R."""
+    spec = os.environ.get("VBFM_BENCH_FAULT", "")
+    if not spec.startswith("exit:"):
+        return
+    if rank == int(spec.split(":", 1)[1]):
+        log("rank %d: VBFM_BENCH_FAULT: exiting with status 3" % rank)
+        sys.exit(3)
+    time.sleep(600)
 
 
 def loaded_libs(name):
@@ -375,6 +415,7 @@ def main():
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         raise SystemExit("bench.py: --gpus %d but WORLD_SIZE=%d" % (args.gpus, world))
+    bench_fault_hook(rank)
     if args.one_rank_comm:   # read by vbfm_create / vbfm_comm_init
         if world != 1:
             raise SystemExit("--one-rank-comm is a one-rank mode")
@@ -409,8 +450,13 @@ def main():
     import torch.distributed as dist
     import vbfm
 
+    # the library's deadline for a collective (VBFM_COMM_TIMEOUT_S, include/vbfm.h) bounds the
+    # bench's own gloo barriers too
+    comm_timeout_s = float(os.environ.get("VBFM_COMM_TIMEOUT_S", "300"))
     if world > 1:
-        dist.init_process_group("gloo", rank=rank, world_size=world)
+        import datetime
+        dist.init_process_group("gloo", rank=rank, world_size=world,
+                                timeout=datetime.timedelta(seconds=max(comm_timeout_s, 30.0)))
     ndev = torch.cuda.device_count()
     device = local_rank % max(1, ndev)      # one rank per GPU; a rehearsal with more ranks than GPUs shares them
     torch.cuda.set_device(device)
@@ -512,6 +558,9 @@ def main():
         return st.rmse_all if mc else st.rmse
 
     n_ranks_seen, _, transport = fml.comm_info()
+    if n_ranks_seen != args.gpus:   # every rank must have joined the one communicator
+        raise SystemExit("bench.py: rank %d sees %d rank(s) in its communicator (%s), --gpus %d" % (
+            rank, n_ranks_seen, transport, args.gpus))
     place_ms, place_kept = fml.placement()
     rccl_libs = loaded_libs("librccl")
     if len(rccl_libs) > 1:
@@ -530,8 +579,10 @@ def main():
     barrier()
     t_start = time.perf_counter()
     stats = []
+    xstats = []
     for i in range(args.steps):
         stats.append(fml.iterate())
+        xstats.append(fml.exchange_info())
         st = stats[-1]
         rmse_trace.append(rmse_of(st))
         log("step %d: %.1f ms (v sweep %.1f, w %.1f, hyper %.1f, %s %.1f) rmse %.6f" % (
@@ -663,6 +714,15 @@ def main():
         "test_rmse": rmse_of(stats[-1]),
         "test_rmse_trace": [round(x, 9) for x in rmse_trace],
         "n_ranks_seen": n_ranks_seen, "transport": transport, "rccl_libs": rccl_libs,
+        # this rank's all-reduces per step (vbfm_exchange_info): calls, payload bytes, and their
+        # time -- RCCL: event pairs around the sampled ones (launch-event stride), scaled to all
+        # calls, the wait for the slowest rank included; host exchange: every call's wall time
+        "ms_exchange": sum(x["ms_estimated"] for x in xstats) / len(xstats),
+        "exchange_bytes": sum(x["bytes"] for x in xstats) // len(xstats),
+        "exchange": {"calls_per_step": sum(x["n_calls"] for x in xstats) / len(xstats),
+                     "timed": sum(x["n_timed"] for x in xstats),
+                     "ms_timed": sum(x["ms_timed"] for x in xstats),
+                     "timeout_s": xstats[-1]["timeout_s"]} if xstats else None,
         "free_energy": None if mc else stats[-1].free_energy_last if online else stats[-1].free_energy,
         "phase_ms": {kk: getattr(stats[-1], kk) for kk in (
             ("ms_hyper", "ms_w", "ms_v", "ms_predict", "ms_total") if mc else

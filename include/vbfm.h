@@ -35,9 +35,10 @@ extern "C" {
  *    vbfm_iter_stats::ms_test_predict, checkpoints, vbfm_comm_info, vbfm_device_count and the
  *    per-level step entry points.
  * 3: vbfm_config's placement budget (place_candidates, place_budget_bytes) and vbfm_setup_info.
+ * 4: vbfm_exchange_info; RCCL communicators are non-blocking with a deadline (VBFM_COMM_TIMEOUT_S).
  * A binding checks vbfm_abi_version() against the value it was built for and refuses a mismatch
  * (struct sizes and argument lists differ). */
-#define VBFM_ABI_VERSION 3
+#define VBFM_ABI_VERSION 4
 
 typedef struct vbfm_ctx vbfm_ctx;
 
@@ -272,6 +273,32 @@ int vbfm_comm_init_host(vbfm_ctx *ctx, int32_t nranks, int32_t rank, vbfm_exchan
 /* The communicator as RCCL reports it (ncclCommCount / ncclCommUserRank): transport 0 = none
  * (one rank), 1 = RCCL, 2 = host exchange (nranks / rank as given to vbfm_comm_init_host). */
 int vbfm_comm_info(vbfm_ctx *ctx, int32_t *nranks, int32_t *rank, int32_t *transport);
+/* Failure handling of the exchange (no reference counterpart: the reference is one process).
+ * vbfm_comm_init creates a non-blocking RCCL communicator (ncclCommInitRankConfig, blocking = 0).
+ * Wherever the library waits for work that holds a collective -- the communicator's set-up, an
+ * RCCL call that returns ncclInProgress, a stream synchronisation after an all-reduce -- it polls
+ * ncclCommGetAsyncError and a deadline of VBFM_COMM_TIMEOUT_S seconds (default 300) instead of
+ * blocking. On an RCCL error or a missed deadline it aborts the communicator (ncclCommAbort) and
+ * the call fails; vbfm_last_error names the rank, the phase, factor and level of the exchange and
+ * the cause, and every later call that exchanges fails with the same message. A host exchange
+ * (vbfm_comm_init_host) fails when the caller's function returns non-zero; its transport owns the
+ * timeout. VBFM_COMM_BLOCKING=1 creates a blocking communicator instead (no deadline). */
+/* The exchanges of the last vbfm_iterate / vbfm_mcmc_iterate (since vbfm_comm_init before the
+ * first): every all-reduce of the path counted with its payload, and its time -- RCCL: an event
+ * pair on the stream that runs it around every all-reduce vbfm_set_profiling's stride samples
+ * (device time from the call's enqueue to its completion: the wait for the slowest rank
+ * included), scaled to all calls; host exchange: the host wall time of every call (copies
+ * included). Zero without a communicator. */
+typedef struct {
+	int32_t transport;        /* as vbfm_comm_info */
+	int32_t n_timed;          /* all-reduces timed */
+	uint64_t n_calls;         /* all-reduces issued */
+	uint64_t bytes;           /* their payload per rank */
+	double ms_timed;          /* summed time of the timed ones */
+	double ms_estimated;      /* ms_timed / n_timed * n_calls (host exchange: = ms_timed) */
+	double timeout_s;         /* the deadline in force (0: blocking communicator or none) */
+} vbfm_exchange_stats;
+int vbfm_exchange_info(vbfm_ctx *ctx, vbfm_exchange_stats *out);
 /* The level store's record-buffer placement (VBFM_PLACE): the score (ms, level 0's pattern to and
  * from a reference buffer) of each candidate record buffer, [0] and [1] being the pair allocated
  * first, and in kept[0], kept[1] the indices of the two buffers kept (records, alternate).

@@ -27,27 +27,193 @@ int fail(vbfm_ctx *c, const std::string &m)
 	return -1;
 }
 
-void sync(vbfm_ctx *c) { HIPCHK(hipStreamSynchronize(c->s)); }
+// ---- the exchange's failure handling ------------------------------------------------------
+// the rank, the phase, factor and level the path was in (XPhase), for every exchange message
+static std::string x_where(vbfm_ctx *c)
+{
+	char b[160];
+	int n = snprintf(b, sizeof(b), "rank %d/%d: %s", c->rank, c->nranks, c->x_phase);
+	if (c->x_f >= 0 && n > 0 && n < (int)sizeof(b)) n += snprintf(b + n, sizeof(b) - n, ", factor %d", c->x_f);
+	if (c->x_l >= 0 && n > 0 && n < (int)sizeof(b)) snprintf(b + n, sizeof(b) - n, ", level %d", c->x_l);
+	return b;
+}
+
+// the stall kernel of VBFM_FAULT=comm_stall is released, and a stream that can still drain gets
+// `grace_s` to do so before the communicator is aborted (an abort under a running collective is
+// RCCL's prescribed way out of a dead peer, but a drained stream needs none of it)
+static void stall_release(vbfm_ctx *c, double grace_s)
+{
+	if (!c->stall_flag) return;
+	__atomic_store_n(c->stall_flag, 1u, __ATOMIC_SEQ_CST);
+	const double end = wall_s() + grace_s;
+	while (hipStreamQuery(c->s) == hipErrorNotReady && wall_s() < end) usleep(1000);
+}
+
+// abort the communicator and fail with `why`; every later exchange refuses with the same message
+[[noreturn]] static void comm_fail(vbfm_ctx *c, const std::string &why)
+{
+	const std::string m = x_where(c) + ": " + why;
+	stall_release(c, 5.0);
+	if (c->comm) {
+		(void)ncclCommAbort(c->comm);
+		c->comm = nullptr;
+	}
+	c->comm_failed = true;
+	c->comm_err = m + " (communicator aborted)";
+	throw c->comm_err;
+}
+
+// VBFM_COMM_TRACE=1: a stderr line per RCCL call and wait of the exchange (time since the first)
+static void comm_trace(vbfm_ctx *c, const char *what, double t)
+{
+	static const bool on = [] { const char *e = getenv("VBFM_COMM_TRACE"); return e && e[0] == '1'; }();
+	static const double t0 = wall_s();
+	if (on) fprintf(stderr, "[vbfm comm] %10.4f rank %d %s (%s) %.4f s\n", wall_s() - t0, c->rank, what, c->x_phase, t);
+}
+
+static ncclResult_t comm_async_error(vbfm_ctx *c)
+{
+	ncclResult_t ae = ncclSuccess;
+	const ncclResult_t r = ncclCommGetAsyncError(c->comm, &ae);
+	return r != ncclSuccess ? r : ae;
+}
+
+// an RCCL call's result: ncclInProgress (a non-blocking communicator still connecting) is polled
+// until it settles or the deadline passes
+static void comm_check(vbfm_ctx *c, ncclResult_t r, const char *what)
+{
+	comm_trace(c, r == ncclInProgress ? "in progress" : "returned", 0.0);
+	if (r == ncclInProgress) {
+		const double end = wall_s() + c->comm_timeout_s;
+		for (;;) {
+			r = comm_async_error(c);
+			if (r != ncclInProgress) break;
+			if (c->comm_timeout_s > 0 && wall_s() > end) {
+				char b[160];
+				snprintf(b, sizeof(b), "%s did not complete within %.0f s (VBFM_COMM_TIMEOUT_S)", what, c->comm_timeout_s);
+				comm_fail(c, b);
+			}
+			usleep(200);
+		}
+	}
+	if (r != ncclSuccess) comm_fail(c, std::string("RCCL ") + ncclGetErrorString(r) + " in " + what);
+}
+
+// wait for stream `st`: hipStreamSynchronize without a communicator; with one, poll the stream,
+// RCCL's asynchronous error and the deadline (a rank that died leaves the others' all-reduce
+// spinning: a blocking wait would never return)
+static void comm_wait(vbfm_ctx *c, hipStream_t st)
+{
+	if (!c->comm) {
+		HIPCHK(hipStreamSynchronize(st));
+		return;
+	}
+	const double t0 = wall_s();
+	comm_trace(c, "wait", 0.0);
+	for (uint32_t spin = 0;; spin++) {
+		const hipError_t e = hipStreamQuery(st);
+		if (e == hipSuccess) {
+			if (st == c->s) c->x_pending.clear();
+			comm_trace(c, "waited", wall_s() - t0);
+			return;
+		}
+		if (e != hipErrorNotReady) throw HipError{e, "hipStreamQuery"};
+		const double ta = wall_s();
+		const ncclResult_t ae = comm_async_error(c);
+		if (wall_s() - ta > 0.5) comm_trace(c, "slow ncclCommGetAsyncError", wall_s() - ta);
+		if (ae != ncclSuccess && ae != ncclInProgress)
+			comm_fail(c, std::string("RCCL asynchronous error: ") + ncclGetErrorString(ae));
+		const double dt = wall_s() - t0;
+		if (c->comm_timeout_s > 0 && dt > c->comm_timeout_s) {
+			char b[200];
+			snprintf(b, sizeof(b), "waiting for the stream, the all-reduces queued since the last wait did not "
+			                       "complete within %.0f s (VBFM_COMM_TIMEOUT_S): a rank failed or stopped",
+			         c->comm_timeout_s);
+			comm_fail(c, std::string(b) + (c->x_pending.empty() ? "" : "; the first of them: " + c->x_pending));
+		}
+		// the first ~2 ms poll back to back (an all-reduce's usual wait), then sleep in steps of
+		// up to 1 ms (a sweep's worth of queued levels)
+		if (spin > 256) usleep(dt < 0.05 ? 50 : 1000);
+	}
+}
+
+void sync(vbfm_ctx *c) { comm_wait(c, c->s); }
+
+hipError_t d2h(vbfm_ctx *c, void *dst, const void *src, size_t bytes)
+{
+	if (c->comm) sync(c);
+	return hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, c->s);
+}
+
+void xs_reset(vbfm_ctx *c)
+{
+	const int32_t t = c->comm ? 1 : c->xfn ? 2 : 0;
+	c->xs = vbfm_exchange_stats{};
+	c->xs.transport = t;
+	c->xs.timeout_s = c->comm ? c->comm_timeout_s : 0.0;
+}
+
+void xs_span(vbfm_ctx *c, float ms)
+{
+	c->xs.ms_timed += ms;
+	c->xs.n_timed++;
+}
+
+// the fault hooks of the exchange (tests): VBFM_FAULT=comm makes rank VBFM_FAULT_RANK (default:
+// the last) fail its first exchange inside a sweep as a failed collective would; comm_stall
+// queues a kernel ahead of that exchange that spins until the deadline releases it (a peer that
+// never arrives, on one GPU)
+static void comm_fault_hooks(vbfm_ctx *c)
+{
+	if (c->x_l < 0) return;
+	const char *fr = getenv("VBFM_FAULT_RANK");
+	const int rank = fr ? atoi(fr) : c->nranks - 1;
+	if (c->rank != rank) return;
+	if (fault_at("comm")) {
+		if (c->comm) comm_fail(c, "VBFM_FAULT=comm");
+		throw x_where(c) + ": VBFM_FAULT=comm";
+	}
+	if (fault_at("comm_stall") && c->comm && !c->stall_done) {
+		c->stall_done = true;
+		if (!c->stall_flag) HIPCHK(hipHostMalloc((void **)&c->stall_flag, 4, hipHostMallocCoherent | hipHostMallocMapped));
+		*c->stall_flag = 0;
+		uint32_t *dflag = nullptr;
+		HIPCHK(hipHostGetDevicePointer((void **)&dflag, c->stall_flag, 0));
+		HIPCHK(vbk::stall(dflag, c->s));
+	}
+}
 
 // in-place all-reduce of a device buffer across the ranks: RCCL on the context's stream, or
 // (vbfm_comm_init_host) staged through host memory and handed to the caller's exchange
 void allreduce_dev(vbfm_ctx *c, void *buf, size_t n, ncclDataType_t t, ncclRedOp_t op)
 {
+	if (c->comm_failed) throw c->comm_err;
+	const size_t es = t == ncclDouble ? 8 : t == ncclUint32 ? 4 : 1;
+	comm_fault_hooks(c);
+	c->xs.n_calls++;
+	c->xs.bytes += n * es;
 	if (c->comm) {
-		NCCLCHK(ncclAllReduce(buf, buf, n, t, op, c->comm, c->s));
+		if (c->x_pending.empty()) c->x_pending = x_where(c);
+		const size_t p = prof_begin(c, 3);
+		const double ta = wall_s();
+		const ncclResult_t r = ncclAllReduce(buf, buf, n, t, op, c->comm, c->s);
+		if (wall_s() - ta > 0.5) comm_trace(c, "slow ncclAllReduce", wall_s() - ta);
+		comm_check(c, r, "ncclAllReduce");
+		prof_end(c, p);
 		return;
 	}
 	if (!c->xfn) throw std::string("all-reduce without a communicator");
-	const size_t es = t == ncclDouble ? 8 : t == ncclUint32 ? 4 : 1;
 	const int32_t xt = t == ncclDouble ? VBFM_X_F64 : t == ncclUint32 ? VBFM_X_U32 : VBFM_X_U8;
 	if (t != ncclDouble && t != ncclUint32 && t != ncclUint8) throw std::string("host exchange: unsupported type");
+	const double t0 = wall_s();
 	if (c->xbuf.size() < n * es) c->xbuf.resize(n * es);
-	if (n) HIPCHK(hipMemcpyAsync(c->xbuf.data(), buf, n * es, hipMemcpyDeviceToHost, c->s));
+	if (n) HIPCHK(d2h(c, c->xbuf.data(), buf, n * es));
 	sync(c);
 	if (c->xfn(c->xuser, c->xbuf.data(), n, xt, op == ncclMax ? VBFM_X_MAX : VBFM_X_SUM) != 0)
-		throw std::string("host exchange failed");
+		throw x_where(c) + ": host exchange failed";
 	if (n) HIPCHK(hipMemcpyAsync(buf, c->xbuf.data(), n * es, hipMemcpyHostToDevice, c->s));
 	sync(c);
+	xs_span(c, (float)((wall_s() - t0) * 1e3));
 }
 
 uint32_t ar_chunks(vbfm_ctx *c, uint32_t nfeat)
@@ -69,6 +235,7 @@ uint32_t ar_chunks(vbfm_ctx *c, uint32_t nfeat)
 
 void allreduce_chunk(vbfm_ctx *c, double2 *buf, size_t n, uint32_t i)
 {
+	if (c->comm_failed) throw c->comm_err;
 	if (!c->comm) {   // the host exchange is synchronous: nothing to overlap
 		allreduce_dev(c, buf, n, ncclDouble, ncclSum);
 		return;
@@ -80,7 +247,13 @@ void allreduce_chunk(vbfm_ctx *c, double2 *buf, size_t n, uint32_t i)
 	}
 	HIPCHK(hipEventRecord(c->ev_ar[i], c->s));
 	HIPCHK(hipStreamWaitEvent(c->s_comm, c->ev_ar[i], 0));
-	NCCLCHK(ncclAllReduce(buf, buf, n, ncclDouble, ncclSum, c->comm, c->s_comm));
+	comm_fault_hooks(c);
+	c->xs.n_calls++;
+	c->xs.bytes += n * 8;
+	if (c->x_pending.empty()) c->x_pending = x_where(c);
+	const size_t p = prof_begin(c, 3, c->s_comm);
+	comm_check(c, ncclAllReduce(buf, buf, n, ncclDouble, ncclSum, c->comm, c->s_comm), "ncclAllReduce");
+	prof_end(c, p, c->s_comm);
 }
 
 void allreduce_join(vbfm_ctx *c)
@@ -96,14 +269,14 @@ void allreduce_host(vbfm_ctx *c, double *v, int n)
 	if (!c->row_comm()) return;   // feature shards hold every row: their sums are already global
 	HIPCHK(hipMemcpyAsync(c->red_d, v, n * sizeof(double), hipMemcpyHostToDevice, c->s));
 	allreduce_dev(c, c->red_d, n, ncclDouble, ncclSum);
-	HIPCHK(hipMemcpyAsync(v, c->red_d, n * sizeof(double), hipMemcpyDeviceToHost, c->s));
+	HIPCHK(d2h(c, v, c->red_d, n * sizeof(double)));
 	sync(c);
 }
 
 // block partials of a row reduction, summed on the host in block order
 double finish_sum(vbfm_ctx *c, uint32_t nblocks)
 {
-	HIPCHK(hipMemcpyAsync(c->red_h.data(), c->red_d, nblocks * sizeof(double), hipMemcpyDeviceToHost, c->s));
+	HIPCHK(d2h(c, c->red_h.data(), c->red_d, nblocks * sizeof(double)));
 	sync(c);
 	double s = 0.0;
 	for (uint32_t i = 0; i < nblocks; i++) s += c->red_h[i];
@@ -262,7 +435,7 @@ bool build_estore(vbfm_ctx *c, const std::vector<uint64_t> &lcp, const std::vect
 	{
 		uint32_t *cnt = dalloc<uint32_t>(1), h = 1;
 		HIPCHK(vbk::count_x_ne1(d.csc, d.nnz, cnt, c->s));
-		HIPCHK(hipMemcpyAsync(&h, cnt, 4, hipMemcpyDeviceToHost, c->s));
+		HIPCHK(d2h(c, &h, cnt, 4));
 		sync(c);
 		dfree(cnt);
 		const char *kx = getenv("VBFM_LX");
@@ -534,7 +707,7 @@ void build_lorder(vbfm_ctx *c, const std::vector<uint64_t> &cp, const std::vecto
 	{
 		uint32_t *cnt = dalloc<uint32_t>(1), h = 1;
 		HIPCHK(vbk::count_x_ne1(d.csc, d.nnz, cnt, c->s));
-		HIPCHK(hipMemcpyAsync(&h, cnt, 4, hipMemcpyDeviceToHost, c->s));
+		HIPCHK(d2h(c, &h, cnt, 4));
 		sync(c);
 		dfree(cnt);
 		const char *kx = getenv("VBFM_LX");
@@ -544,7 +717,8 @@ void build_lorder(vbfm_ctx *c, const std::vector<uint64_t> &cp, const std::vecto
 	c->lrow0 = dalloc<uint32_t>(n);
 	c->lpos0 = dalloc<uint32_t>(n);
 	c->rows_alt = dalloc<RowRec>(n);
-	uint32_t *tmp = dalloc<uint32_t>(n);
+	DevScratch<uint32_t> tmp_buf(n);   // freed on every path out, the placement search's failure included
+	uint32_t *&tmp = tmp_buf.p;
 	auto lev = [&](uint32_t l, uint32_t *&f, uint32_t &nfl, const uint64_t *&lp) {
 		f = c->level_feats + c->level_ptr[l];
 		nfl = c->level_ptr[l + 1] - c->level_ptr[l];
@@ -570,7 +744,8 @@ void build_lorder(vbfm_ctx *c, const std::vector<uint64_t> &cp, const std::vecto
 	if ((c->row_comm() || c->force_split) && !(df && df[0] == '0')) {
 		c->lpidx = dalloc<uint32_t>(d.nnz);
 		c->lpx = dalloc<float>(d.nnz);
-		float *tmpx = dalloc<float>(n);
+		DevScratch<float> tmpx_buf(n);
+		float *&tmpx = tmpx_buf.p;
 		uint32_t maxlev = 0;
 		for (uint32_t l = 0; l < L; l++) {
 			const uint32_t pl = (l + L - 1) % L;
@@ -703,6 +878,9 @@ void fs_pass(vbfm_ctx *c, bool is_w, int f)
 		HIPCHK(vbk::fs_pack(c->rows, n, c->fs_base, c->fs_buf, next, s > s0, c->s));
 	}
 	if (c->multi()) {
+		// the pass's exchange follows its last level
+		XPhase ph(c, is_w ? "w pass (feature shards)" : "v pass (feature shards)", is_w ? -1 : f,
+		          (int)nlevels(c) - 1);
 		allreduce_dev(c, c->fs_buf, (next < 0 ? 2 : 5) * (size_t)n, ncclDouble, ncclSum);
 		// parameters: each rank contributes its own features, zero elsewhere
 		double2 *ms = is_w ? c->ms_w : c->ms_v + f;
@@ -728,7 +906,7 @@ void check_schedule(vbfm_ctx *c)
 		                        c->tr.csc, c->dup, owner, bad, c->s));
 	}
 	uint32_t nb = 0;
-	HIPCHK(hipMemcpyAsync(&nb, bad, 4, hipMemcpyDeviceToHost, c->s));
+	HIPCHK(d2h(c, &nb, bad, 4));
 	sync(c);
 	dfree(owner);
 	dfree(bad);
@@ -758,7 +936,7 @@ static void kahn_levels(vbfm_ctx *c, uint32_t *level)
 		for (int u = t; u < t + batch; u++)
 			HIPCHK(vbk::kahn_round(d.col_ptr, d.csc, d.row_ptr, d.csr, bounds, u, indeg, level, order, tail, c->s));
 		uint32_t tl = 0;
-		HIPCHK(hipMemcpyAsync(&tl, tail, 4, hipMemcpyDeviceToHost, c->s));
+		HIPCHK(d2h(c, &tl, tail, 4));
 		sync(c);
 		c->sched_rounds += batch;
 		if (tl == nf) break;
@@ -805,7 +983,7 @@ void build_schedule(vbfm_ctx *c)
 			if (nf) allreduce_dev(c, level, nf, ncclUint32, ncclMax);
 			allreduce_dev(c, changed, 1, ncclUint32, ncclMax);
 		}
-		HIPCHK(hipMemcpyAsync(&ch, changed, 4, hipMemcpyDeviceToHost, c->s));
+		HIPCHK(d2h(c, &ch, changed, 4));
 		sync(c);
 		if (!ch) break;
 		if (round > (int)nf + 2) throw std::string("level schedule did not converge");
@@ -859,6 +1037,12 @@ void build_schedule(vbfm_ctx *c)
 		c->t_store = wall_s() - t1;
 	} catch (...) {
 		c->sched_ready = false;
+		// the half-built store goes too (the records are still in row order: the search puts them
+		// back before it fails); the next call builds it from scratch
+		try {
+			lord_release(c, true);
+		} catch (...) {
+		}
 		throw;
 	}
 }
@@ -919,7 +1103,7 @@ std::vector<double> seg_sums(vbfm_ctx *c, int model, int mode, const double *hw,
 		                  c->vpart_d, c->vseg_d, c->s));
 	// one copy of what was computed: [w partials | factor sums]
 	const size_t lo = want_w ? 0 : nc, hi = want_v ? nc + kg : nc;
-	if (hi > lo) HIPCHK(hipMemcpyAsync(out.data() + lo, c->chunk_out_d + lo, (hi - lo) * 8, hipMemcpyDeviceToHost, c->s));
+	if (hi > lo) HIPCHK(d2h(c, out.data() + lo, c->chunk_out_d + lo, (hi - lo) * 8));
 	sync(c);
 	if (want_w)
 		for (size_t i = 0; i < nc; i++) seg[c->chunks_h[i].g] += out[i];
@@ -979,6 +1163,7 @@ LevelArgs level_args(vbfm_ctx *c, uint32_t l, bool is_w, int f)
 	a.alpha = c->alpha;
 	a.counters = c->counters;
 	a.stats = c->stats;
+	a.skew = c->debug_skew;
 	a.avg_len = c->level_avg[l];
 	a.first_mask = ROW_FIRST;
 	if (is_w) {
@@ -992,7 +1177,7 @@ LevelArgs level_args(vbfm_ctx *c, uint32_t l, bool is_w, int f)
 }
 
 // event pair around one launch when profiling (the pool grows on first use)
-size_t prof_begin(vbfm_ctx *c, int kind)
+size_t prof_begin(vbfm_ctx *c, int kind, hipStream_t st)
 {
 	if (!c->profiling) return NO_SPAN;
 	if (c->prof_stride > 1 && c->prof_tick[kind]++ % (uint64_t)c->prof_stride != 0) return NO_SPAN;
@@ -1008,14 +1193,14 @@ size_t prof_begin(vbfm_ctx *c, int kind)
 	}
 	const size_t a = c->pev_used;
 	c->pev_used += 2;
-	HIPCHK(hipEventRecord(c->pev[a], c->s));
+	HIPCHK(hipEventRecord(c->pev[a], st ? st : c->s));
 	c->spans.push_back(vbfm_ctx::Span{a, kind});
 	return a;
 }
 
-void prof_end(vbfm_ctx *c, size_t a)
+void prof_end(vbfm_ctx *c, size_t a, hipStream_t st)
 {
-	if (c->profiling && a != NO_SPAN) HIPCHK(hipEventRecord(c->pev[a + 1], c->s));
+	if (c->profiling && a != NO_SPAN) HIPCHK(hipEventRecord(c->pev[a + 1], st ? st : c->s));
 }
 
 void sweep_level(vbfm_ctx *c, uint32_t l, bool is_w, int f)
@@ -1023,6 +1208,7 @@ void sweep_level(vbfm_ctx *c, uint32_t l, bool is_w, int f)
 	LevelArgs a = level_args(c, l, is_w, f);
 	if (a.nfeat == 0) return;
 	Range r("level", 2);
+	XPhase ph(c, is_w ? "w sweep" : "v sweep", is_w ? -1 : f, (int)l);
 	const size_t p = prof_begin(c, is_w ? 1 : 0);
 	if (c->ov) {
 		// online VB: the level's columns restricted to the mini-batch (column layout, one GPU)
@@ -1352,7 +1538,7 @@ bool test_overlap()
 void read_counters(vbfm_ctx *c, vbfm_iter_stats *o)
 {
 	uint32_t h[CNT_N];
-	HIPCHK(hipMemcpyAsync(h, c->counters, sizeof(h), hipMemcpyDeviceToHost, c->s));
+	HIPCHK(d2h(c, h, c->counters, sizeof(h)));
 	sync(c);
 	o->nan_mu_w = h[CNT_NAN_MU_W]; o->nan_sigma_w = h[CNT_NAN_SIGMA_W]; o->inf_mu_w = h[CNT_INF_MU_W];
 	o->nan_mu_v = h[CNT_NAN_MU_V]; o->nan_sigma_v = h[CNT_NAN_SIGMA_V]; o->inf_mu_v = h[CNT_INF_MU_V];
@@ -1408,6 +1594,8 @@ int vbfm_create(vbfm_ctx **out, const vbfm_config *cfg)
 	{
 		const char *fs = getenv("VBFM_FORCE_SPLIT");
 		c->force_split = fs && fs[0] == '1';
+		const char *sk = getenv("VBFM_DEBUG_SKEW");
+		c->debug_skew = sk && sk[0] == '1';
 	}
 	int rc = guarded(c, [&] {
 		HIPCHK(hipStreamCreateWithFlags(&c->s, hipStreamNonBlocking));
@@ -1466,6 +1654,7 @@ void vbfm_destroy(vbfm_ctx *c)
 	mc_free(c);
 	ov_free(c);
 	if (c->comm) ncclCommDestroy(c->comm);
+	if (c->stall_flag) (void)hipHostFree(c->stall_flag);
 	for (hipEvent_t e : c->ev_ar)
 		if (e) (void)hipEventDestroy(e);
 	if (c->ev_arj) (void)hipEventDestroy(c->ev_arj);
@@ -1505,7 +1694,7 @@ static uint32_t global_nf(vbfm_ctx *c, uint32_t nf)
 	HIPCHK(hipMemcpyAsync(w, &nf, 4, hipMemcpyHostToDevice, c->s));
 	allreduce_dev(c, w, 1, ncclUint32, ncclMax);
 	uint32_t out = 0;
-	HIPCHK(hipMemcpyAsync(&out, w, 4, hipMemcpyDeviceToHost, c->s));
+	HIPCHK(d2h(c, &out, w, 4));
 	sync(c);
 	dfree(w);
 	return out;
@@ -1650,7 +1839,7 @@ int vbfm_synth_multihot(vbfm_ctx *c, int32_t which, uint32_t n, uint32_t D, uint
 		HIPCHK(vbk::exclusive_scan_u64(nullptr, &tb, d.row_ptr, d.row_ptr, (size_t)n + 1, c->s));
 		void *tmp = dalloc<uint8_t>(tb);
 		HIPCHK(vbk::exclusive_scan_u64(tmp, &tb, d.row_ptr, d.row_ptr, (size_t)n + 1, c->s));
-		HIPCHK(hipMemcpyAsync(&d.nnz, d.row_ptr + n, 8, hipMemcpyDeviceToHost, c->s));
+		HIPCHK(d2h(c, &d.nnz, d.row_ptr + n, 8));
 		sync(c);
 		dfree(tmp);
 		if (d.nnz >= 0xFFFFFFFFull) throw std::string("multi-hot data set too large (nnz >= 2^32)");
@@ -1766,13 +1955,13 @@ int vbfm_get_params(vbfm_ctx *c, vbfm_params *p)
 		const size_t kd = (size_t)c->k * c->D;
 		double *tmp = dalloc<double>(2 * std::max(kd, (size_t)c->D));
 		HIPCHK(vbk::unpack_pairs(c->ms_w, tmp, tmp + c->D, 1, c->D, c->s));
-		if (p->mu_w) HIPCHK(hipMemcpyAsync(p->mu_w, tmp, c->D * 8, hipMemcpyDeviceToHost, c->s));
-		if (p->sigma_w) HIPCHK(hipMemcpyAsync(p->sigma_w, tmp + c->D, c->D * 8, hipMemcpyDeviceToHost, c->s));
+		if (p->mu_w) HIPCHK(d2h(c, p->mu_w, tmp, c->D * 8));
+		if (p->sigma_w) HIPCHK(d2h(c, p->sigma_w, tmp + c->D, c->D * 8));
 		sync(c);
 		if (kd) {
 			HIPCHK(vbk::unpack_pairs(c->ms_v, tmp, tmp + kd, (uint32_t)c->k, c->D, c->s));
-			if (p->mu_v) HIPCHK(hipMemcpyAsync(p->mu_v, tmp, kd * 8, hipMemcpyDeviceToHost, c->s));
-			if (p->sigma_v) HIPCHK(hipMemcpyAsync(p->sigma_v, tmp + kd, kd * 8, hipMemcpyDeviceToHost, c->s));
+			if (p->mu_v) HIPCHK(d2h(c, p->mu_v, tmp, kd * 8));
+			if (p->sigma_v) HIPCHK(d2h(c, p->sigma_v, tmp + kd, kd * 8));
 			sync(c);
 		}
 		dfree(tmp);
@@ -1959,11 +2148,18 @@ struct StateHeader {
 	uint64_t layout;      // version 2: row layout (VBFM_LAYOUT_*) | shard mode << 8: both decide the
 	                      // order of the data-set sums, so a resume must use the same ones
 	uint64_t flags;       // STATE_FLAG_* (0 in files of libvbfm before round 5: was reserved)
-	uint64_t reserved[2];
+	uint64_t shapes;      // the workgroup shape table the sums ran with (state_shapes; 0 before round 6:
+	                      // was reserved)
+	uint64_t reserved;
 };
 // the layout word of an online checkpoint says whether its batches ran on the per-batch level store
 // (written since round 5; before, an online learner always wrote COLUMN, whichever it used)
 constexpr uint64_t STATE_FLAG_OV_LAYOUT = 1;
+// a column's reduction tree follows its workgroup shape (dispatch_shape, vbfm_device.h), so a resume
+// continues bit for bit only under the same shape table: its revision (3: round 5's, with 128 x 3
+// and the small-shape cutoff at 128) and the cutoff in force (VBFM_SMALL_MAX)
+constexpr uint64_t SHAPE_TABLE_REVISION = 3;
+static uint64_t state_shapes() { return SHAPE_TABLE_REVISION << 32 | shape_small_max(); }
 static_assert(sizeof(StateHeader) == 104, "checkpoint header layout");
 constexpr char STATE_MAGIC[8] = {'V', 'B', 'F', 'M', 'S', 'T', '0', '1'};
 constexpr char MC_STATE_MAGIC[8] = {'V', 'B', 'F', 'M', 'M', 'C', '0', '1'};   // MCMC / ALS payload
@@ -1982,7 +2178,7 @@ uint64_t train_fingerprint(vbfm_ctx *c)
 	HIPCHK(vbk::fingerprint(c->tr.csc, c->tr.nnz, 8, 2, d, c->s));
 	HIPCHK(vbk::fingerprint(c->tr.target, c->tr.n, 4, 3, d, c->s));
 	unsigned long long h = 0;
-	HIPCHK(hipMemcpyAsync(&h, d, 8, hipMemcpyDeviceToHost, c->s));
+	HIPCHK(d2h(c, &h, d, 8));
 	sync(c);
 	dfree(d);
 	return h;
@@ -2011,6 +2207,7 @@ StateHeader state_header(vbfm_ctx *c, uint32_t iter)
 	h.iter = iter;
 	h.layout = state_layout(c);
 	h.flags = STATE_FLAG_OV_LAYOUT;
+	h.shapes = state_shapes();
 	return h;
 }
 
@@ -2027,7 +2224,7 @@ void dev_to_file(vbfm_ctx *c, CkptFile &f, const void *d, size_t bytes)
 	std::vector<uint8_t> buf(std::min(bytes, IO_CHUNK));
 	for (size_t o = 0; o < bytes; o += IO_CHUNK) {
 		const size_t n = std::min(IO_CHUNK, bytes - o);
-		HIPCHK(hipMemcpyAsync(buf.data(), (const uint8_t *)d + o, n, hipMemcpyDeviceToHost, c->s));
+		HIPCHK(d2h(c, buf.data(), (const uint8_t *)d + o, n));
 		sync(c);
 		f.write(buf.data(), n);
 	}
@@ -2119,6 +2316,16 @@ int vbfm_load_state(vbfm_ctx *c, const char *path, uint32_t *iter)
 			throw std::string("an online VB checkpoint written by an older libvbfm, whose layout word does not record "
 			                  "whether the batches ran on the per-batch level store (the order of the batches' data-set "
 			                  "sums): resume it with the libvbfm that wrote it");
+		if (h.shapes != state_shapes()) {
+			char b[320];
+			snprintf(b, sizeof(b), "checkpoint written under another workgroup shape table (%s; this library: revision "
+			         "%llu, VBFM_SMALL_MAX %u): the column sums would change order and the run would not continue bit "
+			         "for bit; resume with the libvbfm and VBFM_SMALL_MAX that wrote it",
+			         h.shapes ? ("revision " + std::to_string(h.shapes >> 32) + ", VBFM_SMALL_MAX " +
+			                     std::to_string(h.shapes & 0xffffffffu)).c_str() : "a libvbfm before round 6, unrecorded",
+			         (unsigned long long)SHAPE_TABLE_REVISION, shape_small_max());
+			throw std::string(b);
+		}
 		if (h.layout != state_layout(c))
 			throw std::string("checkpoint of another row layout or shard mode (the data-set sums would add the rows in "
 			                  "another order): resume with the same VBFM_LAYOUT / vbfm_set_layout and shard mode");
@@ -2182,10 +2389,11 @@ int vbfm_iterate(vbfm_ctx *c, vbfm_iter_stats *o)
 		HIPCHK(hipMemsetAsync(c->counters, 0, CNT_N * 4, c->s));
 		c->pev_used = 0;
 		c->spans.clear();
+		xs_reset(c);
 		Range r_it("vbfm_iterate");
 		HIPCHK(hipEventRecord(c->ev[EV_BEGIN], c->s));
 		// update_all (fm_learn_vb.h:383-501)
-		if (c->k0) { Range r("update_w0"); step_w0(c); }
+		if (c->k0) { Range r("update_w0"); XPhase ph(c, "update_w0"); step_w0(c); }
 		HIPCHK(hipEventRecord(c->ev[EV_W0], c->s));
 		// the sweeps follow each other directly: a deferred split may carry a sweep's last
 		// correction into the next sweep's first level (sweep_level); the last sweep flushes
@@ -2220,6 +2428,7 @@ int vbfm_iterate(vbfm_ctx *c, vbfm_iter_stats *o)
 		bool early;
 		try {
 			Range r("hyper + free energy");
+			XPhase ph(c, "hyper-parameters + free energy");
 			early = step_hyper(c, &energy, &st.nan_alpha, &st.inf_alpha);
 			st.free_energy_valid = early ? 0 : 1;
 			st.free_energy = early ? NAN : free_energy(c, energy);
@@ -2232,6 +2441,7 @@ int vbfm_iterate(vbfm_ctx *c, vbfm_iter_stats *o)
 		HIPCHK(hipEventRecord(c->ev[EV_HYPER], c->s));
 		// test prediction and metrics (fm_learn_vb_simultaneous.h:125-222)
 		Range r_test("test prediction");
+		XPhase ph_test(c, "test metrics");
 		if (overlap) {
 			HIPCHK(hipStreamWaitEvent(c->s, c->ev[EV_TP1], 0));
 		} else {
@@ -2241,7 +2451,7 @@ int vbfm_iterate(vbfm_ctx *c, vbfm_iter_stats *o)
 		}
 		const double mn = c->min_target, mx = c->max_target;
 		HIPCHK(vbk::test_metrics(c->e_test, c->te.target, c->te.n, mn, mx, c->pred_test, c->red_d, c->RED_BLOCKS, c->s));
-		HIPCHK(hipMemcpyAsync(c->red_h.data(), c->red_d, 2 * c->RED_BLOCKS * 8, hipMemcpyDeviceToHost, c->s));
+		HIPCHK(d2h(c, c->red_h.data(), c->red_d, 2 * c->RED_BLOCKS * 8));
 		sync(c);
 		double tm[3] = {0.0, 0.0, 0.0};
 		for (uint32_t i = 0; i < c->RED_BLOCKS; i++) { tm[0] += c->red_h[2 * i]; tm[1] += c->red_h[2 * i + 1]; }
@@ -2271,7 +2481,8 @@ int vbfm_iterate(vbfm_ctx *c, vbfm_iter_stats *o)
 			HIPCHK(hipEventElapsedTime(&ms, c->pev[sp.a], c->pev[sp.a + 1]));
 			if (sp.kind == 0) { st.ms_vlevel_kernels += ms; st.n_vlevel_launches++; }
 			else if (sp.kind == 1) { st.ms_wlevel_kernels += ms; st.n_wlevel_launches++; }
-			else { st.ms_qcache_kernels += ms; st.n_qcache_launches++; }
+			else if (sp.kind == 2) { st.ms_qcache_kernels += ms; st.n_qcache_launches++; }
+			else xs_span(c, ms);
 		}
 		st.ms_qcache = st.ms_qcache_kernels;
 		if (o) *o = st;
@@ -2338,9 +2549,28 @@ int vbfm_comm_init(vbfm_ctx *c, int32_t nranks, int32_t rank, const uint8_t uid[
 		if (nranks == 1 && !(fc && fc[0] == '1')) return;
 		ncclUniqueId id;
 		memcpy(&id, uid, 128);
-		NCCLCHK(ncclCommInitRank(&c->comm, nranks, id, rank));
 		c->nranks = nranks;
 		c->rank = rank;
+		const char *to = getenv("VBFM_COMM_TIMEOUT_S");
+		c->comm_timeout_s = to ? std::max(atof(to), 0.0) : 300.0;
+		const char *bl = getenv("VBFM_COMM_BLOCKING");
+		const bool blocking = bl && bl[0] == '1';
+		// non-blocking: the set-up returns at once (ncclInProgress) and is polled against the
+		// deadline like every later wait on a collective (comm_check / comm_wait)
+		ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
+		cfg.blocking = blocking ? 1 : 0;
+		XPhase ph(c, "communicator set-up");
+		const ncclResult_t r = ncclCommInitRankConfig(&c->comm, nranks, id, rank, &cfg);
+		if (r != ncclSuccess && r != ncclInProgress) {
+			if (c->comm) (void)ncclCommAbort(c->comm);
+			c->comm = nullptr;
+			throw x_where(c) + ": RCCL " + ncclGetErrorString(r) + " in ncclCommInitRankConfig";
+		}
+		if (!c->comm) throw x_where(c) + ": ncclCommInitRankConfig returned no communicator";
+		comm_check(c, r, "ncclCommInitRankConfig");
+		comm_check(c, comm_async_error(c), "ncclCommInitRankConfig");
+		if (blocking) c->comm_timeout_s = 0.0;   // no deadline: every wait blocks
+		xs_reset(c);
 	});
 }
 
@@ -2376,10 +2606,11 @@ int vbfm_comm_info(vbfm_ctx *c, int32_t *nranks, int32_t *rank, int32_t *transpo
 {
 	if (!c) return fail(nullptr, "null context");
 	return guarded(c, [&] {
+		if (c->comm_failed) throw c->comm_err;
 		int n = c->nranks, r = c->rank, t = 0;
 		if (c->comm) {          // ask RCCL itself, not the context's copy
-			NCCLCHK(ncclCommCount(c->comm, &n));
-			NCCLCHK(ncclCommUserRank(c->comm, &r));
+			comm_check(c, ncclCommCount(c->comm, &n), "ncclCommCount");
+			comm_check(c, ncclCommUserRank(c->comm, &r), "ncclCommUserRank");
 			t = 1;
 		} else if (c->xfn) {
 			t = 2;
@@ -2391,6 +2622,14 @@ int vbfm_comm_info(vbfm_ctx *c, int32_t *nranks, int32_t *rank, int32_t *transpo
 		if (rank) *rank = r;
 		if (transport) *transport = t;
 	});
+}
+
+int vbfm_exchange_info(vbfm_ctx *c, vbfm_exchange_stats *o)
+{
+	if (!c || !o) return fail(c, "null argument");
+	*o = c->xs;
+	o->ms_estimated = o->transport == 1 && o->n_timed ? o->ms_timed / o->n_timed * (double)o->n_calls : o->ms_timed;
+	return 0;
 }
 
 int vbfm_comm_init_host(vbfm_ctx *c, int32_t nranks, int32_t rank, vbfm_exchange_fn fn, void *user)
@@ -2405,6 +2644,7 @@ int vbfm_comm_init_host(vbfm_ctx *c, int32_t nranks, int32_t rank, vbfm_exchange
 		c->xuser = user;
 		c->nranks = nranks;
 		c->rank = rank;
+		xs_reset(c);
 	});
 }
 

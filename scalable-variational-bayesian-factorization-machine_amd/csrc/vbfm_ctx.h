@@ -65,6 +65,15 @@ template <class T> inline void dfree(T *&p)
 	p = nullptr;
 }
 
+// a device buffer freed when its scope ends, normally or by an exception (dfree(buf.p) frees it early)
+template <class T> struct DevScratch {
+	T *p = nullptr;
+	explicit DevScratch(size_t n) : p(dalloc<T>(n)) {}
+	~DevScratch() { dfree(p); }
+	DevScratch(const DevScratch &) = delete;
+	DevScratch &operator=(const DevScratch &) = delete;
+};
+
 enum { EV_BEGIN, EV_W0, EV_W, EV_V, EV_HYPER, EV_TEST, EV_TP0, EV_TP1, EV_N };
 
 // host wall clock (s) of the set-up steps vbfm_setup_info reports
@@ -169,7 +178,23 @@ struct vbfm_ctx {
 	// row-sharded multi-GPU
 	int nranks = 1, rank = 0;
 	bool force_split = false;      // VBFM_FORCE_SPLIT=1: the multi-rank kernels on one rank
+	int debug_skew = 0;            // VBFM_DEBUG_SKEW=1: late waves in the split forms' posterior kernels
 	ncclComm_t comm = nullptr;
+	// communicator health: RCCL runs non-blocking (its errors surface through
+	// ncclCommGetAsyncError), polled against a deadline wherever the host waits on work that holds a
+	// collective (comm_wait); a failure or a missed deadline aborts the communicator, and every
+	// later exchange refuses with the first message (comm_err)
+	double comm_timeout_s = 300.0;   // VBFM_COMM_TIMEOUT_S
+	bool comm_failed = false;
+	std::string comm_err;
+	// where the path is when it exchanges (the messages name it): a phase, the factor (-1: none)
+	// and the level (-1: not in a sweep)
+	const char *x_phase = "set-up";
+	int x_f = -1, x_l = -1;
+	std::string x_pending;           // the first exchange issued since the last completed wait (x_where)
+	vbfm_exchange_stats xs = {};     // this iteration's exchanges (vbfm_exchange_info)
+	uint32_t *stall_flag = nullptr;  // VBFM_FAULT=comm_stall: host flag that releases the stall kernel
+	bool stall_done = false;
 	double2 *stats = nullptr;
 	uint32_t stats_cap = 0;
 	uint64_t n_global = 0;
@@ -178,10 +203,10 @@ struct vbfm_ctx {
 	// per-launch profiling (vbfm_set_profiling)
 	bool profiling = false;
 	int prof_stride = 1;             // event pair around every prof_stride-th launch of a kind
-	uint64_t prof_tick[3] = {0, 0, 0};
+	uint64_t prof_tick[4] = {0, 0, 0, 0};
 	std::vector<hipEvent_t> pev;
 	size_t pev_used = 0;
-	struct Span { size_t a; int kind; };   // kind 0 = v level, 1 = w level, 2 = qcache
+	struct Span { size_t a; int kind; };   // kind 0 = v level, 1 = w level, 2 = qcache, 3 = exchange
 	std::vector<Span> spans;
 	// level-ordered row store (vbfm_lorder.hip)
 	int layout_req = VBFM_LAYOUT_AUTO;
@@ -225,7 +250,7 @@ struct vbfm_ctx {
 	void *xuser = nullptr;
 	std::vector<uint8_t> xbuf;      // host staging of a host-exchange all-reduce
 	bool deferred() const { return lpay || lpay2; }
-	bool multi() const { return comm || xfn; }
+	bool multi() const { return comm || xfn || comm_failed; }
 	bool row_comm() const { return multi() && shard_mode == VBFM_SHARD_ROWS; }
 	McState *mc = nullptr;         // set by vbfm_mcmc_init: the context runs the MCMC / ALS learner
 	OvState *ov = nullptr;         // set by vbfm_online_init: the context runs the online VB learner
@@ -258,6 +283,25 @@ template <class F> int guarded(vbfm_ctx *c, F &&fn)
 }
 
 void sync(vbfm_ctx *c);
+// a copy from the device into host memory, queued on the context's stream. A copy into pageable
+// memory holds the calling thread until the stream reaches it, so with an RCCL communicator the
+// stream is waited for first through sync's deadline and error polling, not inside the copy
+hipError_t d2h(vbfm_ctx *c, void *dst, const void *src, size_t bytes);
+// the phase the next exchanges belong to (restored on scope exit), for comm_fail's message
+struct XPhase {
+	vbfm_ctx *c;
+	const char *p;
+	int f, l;
+	XPhase(vbfm_ctx *c_, const char *phase, int f_ = -1, int l_ = -1) : c(c_), p(c_->x_phase), f(c_->x_f), l(c_->x_l)
+	{
+		c->x_phase = phase; c->x_f = f_; c->x_l = l_;
+	}
+	~XPhase() { c->x_phase = p; c->x_f = f; c->x_l = l; }
+};
+// a new iteration's exchange accounting (vbfm_exchange_info)
+void xs_reset(vbfm_ctx *c);
+// fold the timed exchange spans of the iteration into c->xs (vbfm_iterate / vbfm_mcmc_iterate)
+void xs_span(vbfm_ctx *c, float ms);
 void allreduce_host(vbfm_ctx *c, double *v, int n);
 // in-place all-reduce of a device buffer over the ranks (RCCL on c->s, or the host exchange)
 void allreduce_dev(vbfm_ctx *c, void *buf, size_t n, ncclDataType_t t, ncclRedOp_t op);
@@ -307,8 +351,8 @@ void stats_exchange(vbfm_ctx *c, const A &a, F launch)
 void require_train(vbfm_ctx *c);
 uint32_t nlevels(vbfm_ctx *c);
 constexpr size_t NO_SPAN = ~(size_t)0;   // prof_begin: this launch is not timed
-size_t prof_begin(vbfm_ctx *c, int kind);
-void prof_end(vbfm_ctx *c, size_t a);
+size_t prof_begin(vbfm_ctx *c, int kind, hipStream_t st = nullptr);
+void prof_end(vbfm_ctx *c, size_t a, hipStream_t st = nullptr);
 int blocked_predict(const vbfm_ctx *c, const DevData &d);
 float ev_ms(vbfm_ctx *c, int a, int b);
 void mc_free(vbfm_ctx *c);   // vbfm_mcmc_capi.hip

@@ -185,6 +185,7 @@ struct LevelArgs {
 	const LongSeg *segs;       // the level's segments
 	uint32_t nsegs;
 	double2 *seg_part;         // per segment: (sum1, sum2), then the column's old {mu, sigma}
+	int skew;                  // VBFM_DEBUG_SKEW (debug_skew)
 };
 
 // per-level launch description for the MCMC / ALS draws (vbfm_mcmc.hip); parameters are
@@ -240,10 +241,29 @@ struct McArgs {
 	const double2 *par_prev;
 	int pk;
 	int ent;                   // the entry store (as LevelArgs::ent; fused sweeps only)
+	int skew;                  // VBFM_DEBUG_SKEW (debug_skew)
 };
+
+// VBFM_DEBUG_SKEW=1 (tests/test_skew_gpu.py): in the kernels that read a column's parameter, then
+// write its new value from one thread with no reduction between the two -- the split forms'
+// posterior / draw kernels -- every wave but a workgroup's first sleeps ~50 us before it reads the
+// old value. A missing barrier between the waves' reads and the write then shows on every run
+// (the late waves read the new value as "old"), not on a lucky one; with the barrier the result
+// is unchanged. The fused kernels reduce their statistics over the workgroup (a barrier) between
+// the read and the write by construction. The compiler barrier keeps the read after the sleep.
+__device__ __forceinline__ void debug_skew(int on)
+{
+	if (on && threadIdx.x >= 64) {
+		for (int i = 0; i < 16; i++) __builtin_amdgcn_s_sleep(127);
+		__asm__ __volatile__("" ::: "memory");
+	}
+}
 
 // kernels launched from the C-ABI layer (vbfm_kernels.hip)
 namespace vbk {
+// test hook of the exchange's deadline (VBFM_FAULT=comm_stall): one wave that spins until *flag
+// (coherent host memory) turns non-zero, at most ~100 s
+hipError_t stall(const uint32_t *flag, hipStream_t s);
 hipError_t v_level_fused(const LevelArgs &a, hipStream_t s);
 hipError_t w_level_fused(const LevelArgs &a, hipStream_t s);
 hipError_t v_level_stats(const LevelArgs &a, hipStream_t s);

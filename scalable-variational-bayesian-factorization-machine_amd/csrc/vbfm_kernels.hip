@@ -194,6 +194,7 @@ __global__ __launch_bounds__(BLOCK) void k_v_level_correct(LevelArgs a)
 	const uint64_t cb = a.col_ptr[j];
 	const uint32_t n = (uint32_t)(a.col_ptr[j + 1] - cb);
 	const uint2 *col = a.csc + cb;
+	debug_skew(a.skew);
 	const double2 msj = a.ms[(size_t)j * a.ms_stride];
 	const double2 st = a.stats[blockIdx.x];
 	double2 nx = make_double2(0.0, 0.0);
@@ -203,7 +204,7 @@ __global__ __launch_bounds__(BLOCK) void k_v_level_correct(LevelArgs a)
 	const bool go = v_post(st.x, st.y, sv_g, a.alpha, msj.x, msj.y, mu, sig, a.counters, threadIdx.x == 0);
 	// every wave has used the old value (v_post above) before it is overwritten: without the
 	// barrier a wave of this workgroup could still read the new one as its "old"
-	__syncthreads();
+	__syncthreads();   // [raw-barrier]
 	if (threadIdx.x == 0) a.ms[(size_t)j * a.ms_stride] = make_double2(mu, sig);
 	if (!go && !NEXT) return;
 	if (a.dup[j]) {
@@ -322,6 +323,7 @@ __global__ __launch_bounds__(BLOCK) void k_w_level_correct(LevelArgs a)
 	const uint64_t cb = a.col_ptr[j];
 	const uint32_t n = (uint32_t)(a.col_ptr[j + 1] - cb);
 	const uint2 *col = a.csc + cb;
+	debug_skew(a.skew);
 	const double2 msj = a.ms[(size_t)j * a.ms_stride];
 	const double2 st = a.stats[blockIdx.x];
 	double2 nx = make_double2(0.0, 0.0);
@@ -329,9 +331,9 @@ __global__ __launch_bounds__(BLOCK) void k_w_level_correct(LevelArgs a)
 	double mu, sig;
 	const double sw_g = (a.hyp_uniform ? a.hyp0 : a.hyp[(size_t)a.attr_group[j] * a.hyp_stride]);
 	const bool go = w_post(st.x, st.y, sw_g, a.alpha, msj.x, msj.y, mu, sig, a.counters, threadIdx.x == 0);
-	// every wave has used the old value (v_post above) before it is overwritten: without the
+	// every wave has used the old value (w_post above) before it is overwritten: without the
 	// barrier a wave of this workgroup could still read the new one as its "old"
-	__syncthreads();
+	__syncthreads();   // [raw-barrier]
 	if (threadIdx.x == 0) a.ms[(size_t)j * a.ms_stride] = make_double2(mu, sig);
 	if (!go && !NEXT) return;
 	if (a.dup[j]) {
@@ -1362,6 +1364,15 @@ inline unsigned grid_for(uint64_t n, unsigned block = 256) { return (unsigned)((
 }  // namespace
 
 // ------------------------------------------------------------------------------------
+// a collective that never completes, for the deadline test (VBFM_FAULT=comm_stall): the wave
+// polls a flag in coherent host memory with loads only and leaves when the host sets it, or after
+// 60 s of the 100 MHz constant clock whatever happens: every wave reaches the exit
+__global__ __launch_bounds__(64) void k_stall(const volatile uint32_t *flag)
+{
+	const uint64_t t0 = wall_clock64();
+	while (*flag == 0u && wall_clock64() - t0 < 6000000000ull) __builtin_amdgcn_s_sleep(127);
+}
+
 namespace vbk {
 
 // Column-length-adaptive launch shape: threads per column and entries held per thread
@@ -1377,6 +1388,12 @@ template <bool NEXT>
 hipError_t launch_w_fused(const LevelArgs &a, hipStream_t s)
 {
 	dispatch_shape(a.avg_len, [&](auto B, auto R) { k_w_level_fused<B(), R(), NEXT><<<a.nfeat, B(), 0, s>>>(a); });
+	return hipGetLastError();
+}
+
+hipError_t stall(const uint32_t *flag, hipStream_t s)
+{
+	hipLaunchKernelGGL(k_stall, dim3(1), dim3(64), 0, s, flag);
 	return hipGetLastError();
 }
 

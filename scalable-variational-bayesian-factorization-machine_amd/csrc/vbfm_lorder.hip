@@ -482,6 +482,7 @@ __global__ __launch_bounds__(BLOCK) void k_level_lord_move(LevelArgs a)
 	const uint32_t j = level_feat(a, blockIdx.x);
 	const uint64_t sb = a.lcp[blockIdx.x];
 	const uint32_t n = (uint32_t)(a.lcp[blockIdx.x + 1] - sb);
+	debug_skew(a.skew);
 	const double2 msj = a.ms[(size_t)j * a.ms_stride];
 	const double2 st = a.stats[blockIdx.x];
 	VbOp<IS_W, P, NEXT> op;
@@ -489,9 +490,9 @@ __global__ __launch_bounds__(BLOCK) void k_level_lord_move(LevelArgs a)
 	op.nx = NEXT ? a.ms_next[(size_t)j * a.ms_stride_next] : make_double2(0.0, 0.0);
 	const double hyp = (a.hyp_uniform ? a.hyp0 : a.hyp[(size_t)a.attr_group[j] * a.hyp_stride]);
 	op.go = vb_post<IS_W>(st.x, st.y, hyp, a.alpha, op.mo, op.so, op.mu, op.sig, a.counters, threadIdx.x == 0);
-	// every wave has used the old value (v_post above) before it is overwritten: without the
+	// every wave has used the old value (vb_post above) before it is overwritten: without the
 	// barrier a wave of this workgroup could still read the new one as its "old"
-	__syncthreads();
+	__syncthreads();   // [raw-barrier]
 	if (threadIdx.x == 0) a.ms[(size_t)j * a.ms_stride] = make_double2(op.mu, op.sig);
 	lord_move<BLOCK, CAP, VbOp<IS_W, P, NEXT>, ENT>(recs, dsts, a.src + (sb - a.lbase), a.lx ? a.lx + sb : nullptr,
 	                                                a.lnext + sb, n, false, a.dst, a.first_level != 0, op);
@@ -514,6 +515,7 @@ __global__ __launch_bounds__(BLOCK) void k_mc_level_lord(McArgs a)
 	const RowRec *src = a.src + (sb - a.lbase);
 	const float *lx = a.lx ? a.lx + sb : nullptr;
 	McOp<IS_W, P, NEXT> op;
+	if constexpr (MODE == 2) debug_skew(a.skew);
 	op.vo = a.par[(size_t)j * a.stride].x;
 	op.vn = NEXT ? a.par_next[(size_t)j * a.next_stride].x : 0.0;
 	op.pk = IS_W ? 0 : a.pk;
@@ -554,7 +556,7 @@ __global__ __launch_bounds__(BLOCK) void k_mc_level_lord(McArgs a)
 		                mc_z(a, j), a.z != nullptr, a.sample, !IS_W, op.v, a.counters, threadIdx.x == 0);
 		// MODE 2: every wave has used the old value (the draw) before it is overwritten (no
 		// barrier since the kernel began; without one a wave could read the new value as "old")
-		if constexpr (MODE == 2) __syncthreads();
+		if constexpr (MODE == 2) __syncthreads();   // [raw-barrier]
 		if (threadIdx.x == 0) a.par[(size_t)j * a.stride].x = op.v;
 		lord_move<BLOCK, CAP, McOp<IS_W, P, NEXT>, ENT>(recs, dsts, src, lx, a.lnext + sb, n, false, a.dst,
 		                                                a.first_level != 0, op);

@@ -76,6 +76,7 @@ __global__ __launch_bounds__(BLOCK) void k_mc_v_level(McArgs a)
 	const uint64_t cb = a.col_ptr[j];
 	const uint32_t n = (uint32_t)(a.col_ptr[j + 1] - cb);
 	const uint2 *col = a.csc + cb;
+	if constexpr (MODE == 2) debug_skew(a.skew);
 	const double vo = a.par[(size_t)j * a.stride].x;
 	double sm = 0.0, ss = 0.0;
 	if constexpr (MODE != 2) {
@@ -104,7 +105,7 @@ __global__ __launch_bounds__(BLOCK) void k_mc_v_level(McArgs a)
 	const bool go = mc_draw(sm, ss, vo, mc_lambda(a, g), mc_mu(a, g), a.alpha,
 	                        mc_z(a, j), a.z != nullptr, a.sample, true, v, a.counters, threadIdx.x == 0);
 	// MODE 2: every wave has used the old value (the draw) before it is overwritten
-	if constexpr (MODE == 2) __syncthreads();
+	if constexpr (MODE == 2) __syncthreads();   // [raw-barrier]
 	if (threadIdx.x == 0) a.par[(size_t)j * a.stride].x = v;
 	if (!go && !NEXT && !a.pk) return;
 	auto entry = [&](uint2 ent) {
@@ -137,6 +138,7 @@ __global__ __launch_bounds__(BLOCK) void k_mc_w_level(McArgs a)
 	const uint64_t cb = a.col_ptr[j];
 	const uint32_t n = (uint32_t)(a.col_ptr[j + 1] - cb);
 	const uint2 *col = a.csc + cb;
+	if constexpr (MODE == 2) debug_skew(a.skew);
 	const double wo = a.par[(size_t)j * a.stride].x;
 	double sm = 0.0, ss = 0.0;
 	if constexpr (MODE != 2) {
@@ -162,7 +164,7 @@ __global__ __launch_bounds__(BLOCK) void k_mc_w_level(McArgs a)
 	const bool go = mc_draw(sm, ss, wo, mc_lambda(a, g), mc_mu(a, g), a.alpha,
 	                        mc_z(a, j), a.z != nullptr, a.sample, false, w, a.counters, threadIdx.x == 0);
 	// MODE 2: every wave has used the old value (the draw) before it is overwritten
-	if constexpr (MODE == 2) __syncthreads();
+	if constexpr (MODE == 2) __syncthreads();   // [raw-barrier]
 	if (threadIdx.x == 0) a.par[(size_t)j * a.stride].x = w;
 	if (!go && !NEXT) return;
 	if (a.dup[j]) {

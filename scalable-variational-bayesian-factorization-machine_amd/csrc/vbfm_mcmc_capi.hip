@@ -293,6 +293,7 @@ McArgs mc_args(vbfm_ctx *c, uint32_t l, bool is_w, int f)
 	a.sample = m.sample;
 	a.counters = c->counters;
 	a.stats = c->stats;
+	a.skew = c->debug_skew;
 	a.slot = is_w ? 0 : (f & 1);
 	if (m.pred_acc && !is_w && f >= 1) {   // factor f-1 is final: its re-prediction terms ride along
 		a.par_prev = c->ms_v + (f - 1);
@@ -317,6 +318,7 @@ void mc_sweep(vbfm_ctx *c, bool is_w, int f)
 	for (uint32_t l = 0; l < nlevels(c); l++) {
 		McArgs a = mc_args(c, l, is_w, f);
 		if (a.nfeat == 0) continue;
+		XPhase ph(c, is_w ? "draw_w sweep" : "draw_v sweep", is_w ? -1 : f, (int)l);
 		const size_t p = prof_begin(c, is_w ? 1 : 0);
 		if (c->lord) {   // level-ordered store: stream the runs, move the records to level l+1
 			a.lcp = c->lcp + c->level_ptr[l];
@@ -447,7 +449,7 @@ void scan_columns(vbfm_ctx *c)
 		uint8_t *d = dalloc<uint8_t>(nf);
 		HIPCHK(hipMemcpyAsync(d, m.col_nonempty.data(), nf, hipMemcpyHostToDevice, c->s));
 		allreduce_dev(c, d, nf, ncclUint8, ncclMax);
-		HIPCHK(hipMemcpyAsync(m.col_nonempty.data(), d, nf, hipMemcpyDeviceToHost, c->s));
+		HIPCHK(d2h(c, m.col_nonempty.data(), d, nf));
 		sync(c);
 		dfree(d);
 	}
@@ -553,11 +555,11 @@ int vbfm_mcmc_get_params(vbfm_ctx *c, vbfm_mcmc_params *p)
 		const size_t kd = (size_t)c->k * c->D, half = std::max(kd, (size_t)c->D);
 		double *tmp = dalloc<double>(2 * half);
 		HIPCHK(vbk::unpack_pairs(c->ms_w, tmp, tmp + half, 1, c->D, c->s));
-		if (p->w) HIPCHK(hipMemcpyAsync(p->w, tmp, (size_t)c->D * 8, hipMemcpyDeviceToHost, c->s));
+		if (p->w) HIPCHK(d2h(c, p->w, tmp, (size_t)c->D * 8));
 		sync(c);
 		if (kd && p->v) {
 			HIPCHK(vbk::unpack_pairs(c->ms_v, tmp, tmp + half, (uint32_t)c->k, c->D, c->s));
-			HIPCHK(hipMemcpyAsync(p->v, tmp, kd * 8, hipMemcpyDeviceToHost, c->s));
+			HIPCHK(d2h(c, p->v, tmp, kd * 8));
 			sync(c);
 		}
 		dfree(tmp);
@@ -603,6 +605,7 @@ int vbfm_mcmc_iterate(vbfm_ctx *c, vbfm_mcmc_stats *o)
 		HIPCHK(hipMemsetAsync(c->counters, 0, CNT_N * 4, c->s));
 		c->pev_used = 0;
 		c->spans.clear();
+		xs_reset(c);
 		c->q_ready[0] = c->q_ready[1] = -1;
 		HIPCHK(hipEventRecord(m.ev[MEV_BEGIN], c->s));
 		// draw_all (fm_learn_mcmc.h:411-623)
@@ -627,7 +630,7 @@ int vbfm_mcmc_iterate(vbfm_ctx *c, vbfm_mcmc_stats *o)
 		const double mn = c->min_target, mx = c->max_target;
 		HIPCHK(vbk::mc_test_update(c->e_test, c->te.target, c->te.n, mn, mx, 1.0 / (m.iter + 1), m.pred_this,
 		                           m.pred_sum, m.red_d, MC_RED_BLOCKS, c->s));
-		HIPCHK(hipMemcpyAsync(m.red_h.data(), m.red_d, 4 * MC_RED_BLOCKS * 8, hipMemcpyDeviceToHost, c->s));
+		HIPCHK(d2h(c, m.red_h.data(), m.red_d, 4 * MC_RED_BLOCKS * 8));
 		sync(c);
 		double tm[5] = {0, 0, 0, 0, 0};
 		for (uint32_t b = 0; b < MC_RED_BLOCKS; b++)
@@ -676,9 +679,13 @@ int vbfm_mcmc_iterate(vbfm_ctx *c, vbfm_mcmc_stats *o)
 		st.ms_predict = ms(MEV_V, MEV_PRED);
 		st.ms_total = ms(MEV_BEGIN, MEV_PRED);
 		for (const auto &sp : c->spans) {
-			if (sp.kind != 0) continue;
+			if (sp.kind != 0 && sp.kind != 3) continue;
 			float t = 0.f;
 			HIPCHK(hipEventElapsedTime(&t, c->pev[sp.a], c->pev[sp.a + 1]));
+			if (sp.kind == 3) {
+				xs_span(c, t);
+				continue;
+			}
 			st.ms_vlevel_kernels += t;
 			st.n_vlevel_launches++;
 		}

@@ -817,7 +817,8 @@ template <int G>
 bool launch_ov_lord_fast(const LevelArgs &a, int is_w, hipStream_t s)
 {
 	if (is_w || !a.pad_cap || !a.ov_fast || !a.feat_contig || a.nat_stride != 1) return false;
-	if (a.ms_next && a.ms_next != a.ms + 1) return false;
+	// the kernel reads factor f+1 as ms[pi + 1] with factor f's stride
+	if (a.ms_next && (a.ms_next != a.ms + 1 || a.ms_stride_next != a.ms_stride)) return false;
 	auto fits = [](const void *p) { return (reinterpret_cast<uintptr_t>(p) >> 48) == 0; };
 	if (!fits(a.col_ptr) || !fits(a.src) || !fits(a.lnext) || a.ms_stride > 0xffffu) return false;
 	auto tag = [](const void *p, uint64_t v) {
@@ -1044,7 +1045,7 @@ void ov_launch_level(vbfm_ctx *c, LevelArgs &a, uint32_t l, bool is_w)
 	HIPCHK(vbk::ov_lord_level(a, is_w, c->s));
 	if (st) {
 		std::vector<unsigned long long> h((size_t)nwg * 5 * 8);
-		HIPCHK(hipMemcpyAsync(h.data(), st, h.size() * 8, hipMemcpyDeviceToHost, c->s));
+		HIPCHK(d2h(c, h.data(), st, h.size() * 8));
 		sync(c);
 		(void)hipFree(st);
 		fprintf(stderr, "OVSTAMP launch %ld nfeat %u avg %u\n", launch_no - 1, a.nfeat, a.avg_len);
@@ -1148,7 +1149,7 @@ void ov_regroup(vbfm_ctx *c)
 		k_ov_level_bases<<<grid_of((uint64_t)nb * (L + 1)), 256, 0, c->s>>>(o.gptr, o.level_ptr_d, L, nf, nb, o.lvl_d);
 		HIPCHK(hipGetLastError());
 		o.lvl_h.resize((size_t)nb * (L + 1));
-		HIPCHK(hipMemcpyAsync(o.lvl_h.data(), o.lvl_d, o.lvl_h.size() * 8, hipMemcpyDeviceToHost, c->s));
+		HIPCHK(d2h(c, o.lvl_h.data(), o.lvl_d, o.lvl_h.size() * 8));
 	}
 	sync(c);   // nnz (host) must outlive the copy
 	o.batch_lord.assign(nb, 0);
@@ -1167,7 +1168,7 @@ void ov_regroup(vbfm_ctx *c)
 		                                                          vbk::ov_pad_cap(), o.pad_bad_d);
 		HIPCHK(hipGetLastError());
 		std::vector<uint32_t> bad(nb);
-		HIPCHK(hipMemcpyAsync(bad.data(), o.pad_bad_d, (size_t)nb * 4, hipMemcpyDeviceToHost, c->s));
+		HIPCHK(d2h(c, bad.data(), o.pad_bad_d, (size_t)nb * 4));
 		sync(c);
 		for (uint32_t b = 0; b < nb; b++) o.batch_pad[b] = o.batch_lord[b] && !bad[b];
 	}
@@ -1407,7 +1408,7 @@ int vbfm_online_init(vbfm_ctx *c, const vbfm_online_config *cfg)
 					o.lvl_d = dalloc<uint64_t>((size_t)nb * (L + 1));
 					uint32_t *cnt = dalloc<uint32_t>(1), ne1 = 1;
 					HIPCHK(vbk::count_x_ne1(c->tr.csc, nnz, cnt, c->s));
-					HIPCHK(hipMemcpyAsync(&ne1, cnt, 4, hipMemcpyDeviceToHost, c->s));
+					HIPCHK(d2h(c, &ne1, cnt, 4));
 					sync(c);
 					dfree(cnt);
 					o.x_one = ne1 == 0;
@@ -1481,7 +1482,7 @@ int vbfm_online_epoch(vbfm_ctx *c, vbfm_online_stats *out)
 		const uint32_t nb = o.num_batch, nf = c->tr.nf;
 		std::vector<uint64_t> eoff((size_t)nb + 1);
 		for (uint32_t b = 0; b <= nb; b++)
-			HIPCHK(hipMemcpyAsync(&eoff[b], o.gptr + (size_t)b * nf, 8, hipMemcpyDeviceToHost, c->s));
+			HIPCHK(d2h(c, &eoff[b], o.gptr + (size_t)b * nf, 8));
 		sync(c);   // the permutation's copy to the device is done: draw the next one meanwhile
 		ov_prefetch_shuffle(o);
 		const DevData full = c->tr;
@@ -1571,7 +1572,7 @@ int vbfm_online_epoch(vbfm_ctx *c, vbfm_online_stats *out)
 		test_predict(c, c->s);
 		const double mn = c->min_target, mx = c->max_target;
 		HIPCHK(vbk::test_metrics(c->e_test, c->te.target, c->te.n, mn, mx, c->pred_test, c->red_d, c->RED_BLOCKS, c->s));
-		HIPCHK(hipMemcpyAsync(c->red_h.data(), c->red_d, 2 * c->RED_BLOCKS * 8, hipMemcpyDeviceToHost, c->s));
+		HIPCHK(d2h(c, c->red_h.data(), c->red_d, 2 * c->RED_BLOCKS * 8));
 		HIPCHK(hipEventRecord(o.ev[3], c->s));
 		sync(c);
 		double tm[2] = {0.0, 0.0};

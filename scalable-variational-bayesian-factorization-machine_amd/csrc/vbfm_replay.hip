@@ -238,7 +238,7 @@ extern "C" int vbfm_init_params_replay(vbfm_ctx *c, uint32_t seed, double init_s
 			k_find_zeros<<<grid_of(nuni), 256, 0, c->s>>>(out, nuni, zpos, cnt);
 			HIPCHK(hipGetLastError());
 			uint32_t nz = 0;
-			HIPCHK(hipMemcpyAsync(&nz, cnt, 4, hipMemcpyDeviceToHost, c->s));
+			HIPCHK(d2h(c, &nz, cnt, 4));
 			sync(c);
 			if (nz > MAX_ZEROS) throw std::string("init replay: too many zero outputs");
 			std::vector<uint64_t> z(nz);
@@ -262,7 +262,7 @@ extern "C" int vbfm_init_params_replay(vbfm_ctx *c, uint32_t seed, double init_s
 			                                                  cnt + 1);
 			HIPCHK(hipGetLastError());
 			uint32_t nu = 0;
-			HIPCHK(hipMemcpyAsync(&nu, cnt + 1, 4, hipMemcpyDeviceToHost, c->s));
+			HIPCHK(d2h(c, &nu, cnt + 1, 4));
 			sync(c);
 			if (nu > MAX_UNSURE) throw std::string("init replay: too many borderline attempts");
 			if (nu) {   // re-decide with the host's log (the reference's libm)
@@ -286,8 +286,8 @@ extern "C" int vbfm_init_params_replay(vbfm_ctx *c, uint32_t seed, double init_s
 			HIPCHK(rocprim::exclusive_scan(tmp, tb, flag, offs, 0u, (size_t)nattempt, rocprim::plus<uint32_t>(), c->s));
 			uint32_t tail[2] = {0, 0};
 			if (nattempt) {
-				HIPCHK(hipMemcpyAsync(&tail[0], offs + nattempt - 1, 4, hipMemcpyDeviceToHost, c->s));
-				HIPCHK(hipMemcpyAsync(&tail[1], flag + nattempt - 1, 4, hipMemcpyDeviceToHost, c->s));
+				HIPCHK(d2h(c, &tail[0], offs + nattempt - 1, 4));
+				HIPCHK(d2h(c, &tail[1], flag + nattempt - 1, 4));
 			}
 			sync(c);
 			const uint64_t accepted = (uint64_t)tail[0] + tail[1];

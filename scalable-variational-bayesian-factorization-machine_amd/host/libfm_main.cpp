@@ -128,7 +128,8 @@ private:
 	std::map<std::string, double> value;
 };
 
-// -parity_log FILE ("Metrics / logging"): one JSON line per iteration from rank 0 with
+// -parity_log FILE ("Metrics / logging"): a first line {"method": "setup", ...} with the
+// set-up costs (plog_setup, every method), then one JSON line per iteration from rank 0 with
 // the values the reference prints, at 17 significant digits (its test_rmse_* / free_energy_*
 // files carry 6, too few for a 1e-6 comparison), the device time of the phases, and the factor
 // sweep's throughput: nnz*k per second of ms_v over the whole job and, per GPU, the fraction of
@@ -167,6 +168,9 @@ public:
 		num("sweep_nnz_k_per_s", s > 0 ? (double)nnz * k / s : NAN);
 		num("hbm_frac_per_gpu", s > 0 ? bytes * k / ranks / s / 8e12 : NAN);
 	}
+	// the iteration's exchanges over the ranks (vbfm_exchange_info): all-reduces, their payload per
+	// rank and their time (RCCL: the sampled ones scaled to all; host exchange: every call)
+	void exchange(vbfm_ctx *ctx);
 	void end()
 	{
 		fprintf(f, "{%s}\n", line.c_str());
@@ -188,6 +192,16 @@ static double wall_now()
 }
 
 void check(int rc, vbfm_ctx *ctx);
+
+void ParityLog::exchange(vbfm_ctx *ctx)
+{
+	vbfm_exchange_stats xs;
+	check(vbfm_exchange_info(ctx, &xs), ctx);
+	num("exchange_calls", (double)xs.n_calls);
+	num("exchange_bytes", (double)xs.bytes);
+	num("ms_exchange", xs.ms_estimated);
+	num("exchange_timed", xs.n_timed);
+}
 
 // -parity_log's first line: what setting the train set up cost (vbfm_setup_info): the load, the
 // hand-over to the device, the dependency levels, the row store and its placement search
@@ -506,6 +520,7 @@ static void run_mcmc(const McmcRun &r, Data &train, Data &test, const Rank &rk)
 				plog.num("levels", st.num_levels);
 				plog.num("rng_skipped", st.rng_skipped);
 				plog.sweep(st.ms_v, r.k, train.h.nnz, train.h.num_rows, train.h.num_feature, rk.nranks, true);
+				plog.exchange(ctx);
 				plog.end();
 			}
 			if (rk.lead()) {
@@ -628,6 +643,7 @@ static void run_online(const OnlineRun &r, Data &train, Data &test, const Rank &
 		const std::string f_rmse = "test_rmse_" + tag.str() + "_vb_online", f_fe = "free_energy_" + tag.str() + "_vb";
 		if (!resume) { std::ofstream a(f_rmse.c_str()); std::ofstream b(("free_energy_" + tag.str() + "_vb_online").c_str()); }
 		ParityLog plog(r.parity_file, true);
+		plog_setup(plog, ctx, "vb_online");
 		for (uint32_t it = it0; it < it0 + r.num_iter; it++) {
 			const double t_user = usertime();
 			const clock_t t_clock = clock();
@@ -818,6 +834,7 @@ static void run_vb(const VbRun &r, Data &train, Data &test, const Rank &rk)
 				for (size_t i = 0; i < sizeof(nans) / sizeof(nans[0]); i++) plog.num(nkeys[i], nans[i]);
 				plog.num("levels", st.num_levels);
 				plog.sweep(st.ms_v, k, train.h.nnz, train.h.num_rows, train.h.num_feature, rk.nranks, false);
+				plog.exchange(ctx);
 				plog.end();
 			}
 		}
@@ -1023,7 +1040,7 @@ int main(int argc, char **argv)
 		const std::string p_plan = cmd.reg("plan", "1: every rank prints its launch and shard plan as JSON and exits (no GPU)");
 		const std::string p_vfile = cmd.reg("vfile", "write v_file.txt like the reference (1) or not (0); default=1");
 		const std::string p_save = cmd.reg("save_state", "vb, vb_online, mcmc, als: write the learner's state to this file after the last iteration (.<rank> per rank with -devices)");
-		const std::string p_plog = cmd.reg("parity_log", "one JSON line per iteration: the printed values at 17 digits, phase times, sweep nnz*k/s and HBM roofline fraction; default=''");
+		const std::string p_plog = cmd.reg("parity_log", "JSON lines: a 'setup' line (set-up costs), then one per iteration: the printed values at 17 digits, phase times, sweep nnz*k/s, HBM roofline fraction and the exchange's calls / bytes / ms; default=''");
 		const std::string p_resume = cmd.reg("resume", "vb, vb_online, mcmc, als: continue from a -save_state file (same data and -dim) instead of the initial draws");
 		if (cmd.has(p_help) || argc == 1) { cmd.print_help(); return 0; }
 		cmd.check();

@@ -30,7 +30,7 @@ P_u32, P_u64, P_f32, P_f64, P_u8 = (C.POINTER(C.c_uint32), C.POINTER(C.c_uint64)
                                     C.POINTER(C.c_double), C.POINTER(C.c_uint8))
 
 
-ABI_VERSION = 3        # VBFM_ABI_VERSION of include/vbfm.h this binding is written for
+ABI_VERSION = 4        # VBFM_ABI_VERSION of include/vbfm.h this binding is written for
 LAYOUTS = {"auto": 0, "column": 1, "level": 2, "entry": 3}   # VBFM_LAYOUT_* (include/vbfm.h)
 SYNTH_MODEL_SEED = 7   # tests/synth.py MODEL_SEED: the planted model shared by train, test and all shards
 
@@ -73,6 +73,15 @@ class Params(C.Structure):
     _fields_ = [("mu_w", P_f64), ("sigma_w", P_f64), ("mu_v", P_f64), ("sigma_v", P_f64),
                 ("hyp_sigma_w", P_f64), ("hyp_sigma_v", P_f64), ("alpha", C.c_double),
                 ("sigma_0", C.c_double), ("mu_0_dash", C.c_double), ("sigma_0_dash", C.c_double)]
+
+
+class ExchangeStats(C.Structure):
+    """vbfm_exchange_stats: the last iteration's all-reduces (include/vbfm.h)."""
+    _fields_ = [("transport", C.c_int32), ("n_timed", C.c_int32), ("n_calls", C.c_uint64), ("bytes", C.c_uint64),
+                ("ms_timed", C.c_double), ("ms_estimated", C.c_double), ("timeout_s", C.c_double)]
+
+    def as_dict(self):
+        return {k: getattr(self, k) for k, _ in self._fields_}
 
 
 class IterStats(C.Structure):
@@ -160,7 +169,7 @@ EXPORTS = ["vbfm_abi_version", "vbfm_last_error", "vbfm_create", "vbfm_destroy",
            "vbfm_step_v_level", "vbfm_step_hyper", "vbfm_device_count",
            "vbfm_free_energy", "vbfm_get_rows", "vbfm_get_test_e", "vbfm_factor_sweep", "vbfm_set_profiling",
            "vbfm_set_layout", "vbfm_get_layout", "vbfm_set_shard_mode",
-           "vbfm_comm_unique_id", "vbfm_comm_init", "vbfm_comm_init_host", "vbfm_comm_info", "vbfm_placement_info", "vbfm_setup_info", "vbfm_load_data", "vbfm_free_host_data", "vbfm_save_data",
+           "vbfm_comm_unique_id", "vbfm_comm_init", "vbfm_comm_init_host", "vbfm_comm_info", "vbfm_exchange_info", "vbfm_placement_info", "vbfm_setup_info", "vbfm_load_data", "vbfm_free_host_data", "vbfm_save_data",
            "vbfm_init_params_host", "vbfm_mcmc_init", "vbfm_mcmc_set_params", "vbfm_mcmc_get_params",
            "vbfm_mcmc_init_caches", "vbfm_mcmc_iterate", "vbfm_mcmc_get_test_pred", "vbfm_mcmc_factor_sweep",
            "vbfm_online_init", "vbfm_online_epoch", "vbfm_online_get_state", "vbfm_save_state", "vbfm_load_state"]
@@ -224,6 +233,7 @@ def lib():
         L.vbfm_comm_init.argtypes = [V, C.c_int32, C.c_int32, C.POINTER(C.c_uint8)]
         L.vbfm_comm_init_host.argtypes = [V, C.c_int32, C.c_int32, EXCHANGE_FN, V]
         L.vbfm_comm_info.argtypes = [V, C.POINTER(C.c_int32), C.POINTER(C.c_int32), C.POINTER(C.c_int32)]
+        L.vbfm_exchange_info.argtypes = [V, C.POINTER(ExchangeStats)]
         L.vbfm_placement_info.argtypes = [V, C.POINTER(C.c_float), C.POINTER(C.c_int32), C.POINTER(C.c_int32)]
         L.vbfm_setup_info.argtypes = [V, C.POINTER(SetupStats)]
         L.vbfm_load_data.argtypes = [C.c_char_p, C.POINTER(HostData)]
@@ -619,6 +629,13 @@ class FMLearnVB:
         n, r, t = C.c_int32(), C.c_int32(), C.c_int32()
         _check(lib().vbfm_comm_info(self._ctx, C.byref(n), C.byref(r), C.byref(t)), self._ctx)
         return n.value, r.value, {0: "none", 1: "rccl", 2: "host"}[t.value]
+
+    def exchange_info(self):
+        """The last iteration's all-reduces (vbfm_exchange_info): calls, payload bytes per rank,
+        the timed ones' summed ms, their estimate over all calls, and the deadline in force."""
+        st = ExchangeStats()
+        _check(lib().vbfm_exchange_info(self._ctx, C.byref(st)), self._ctx)
+        return st.as_dict()
 
     def placement(self):
         """(score in ms of each candidate record buffer, [indices of the two kept]) of the level

@@ -63,6 +63,12 @@ int vbfm_setup_info(vbfm_ctx *, vbfm_setup_stats *o)
 	return 0;
 }
 int vbfm_set_shard_mode(vbfm_ctx *, int32_t, int32_t) { return 0; }
+int vbfm_exchange_info(vbfm_ctx *c, vbfm_exchange_stats *o)
+{
+	memset(o, 0, sizeof(*o));
+	o->transport = c->fn ? 2 : 0;
+	return 0;
+}
 int vbfm_comm_unique_id(uint8_t *) { return fail(nullptr, "no RCCL in the sanitizer build"); }
 int vbfm_comm_init(vbfm_ctx *c, int32_t, int32_t, const uint8_t *) { return fail(c, "no RCCL in the sanitizer build"); }
 int vbfm_comm_init_host(vbfm_ctx *c, int32_t nranks, int32_t rank, vbfm_exchange_fn fn, void *user)

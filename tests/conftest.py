@@ -18,6 +18,18 @@ def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (runs through the HIP C-ABI library)")
 
 
+def pytest_sessionstart(session):
+    """torch's HIP runtime initialised before libvbfm's (tests that size memory with torch.cuda):
+    torch initialising second, in a process where libvbfm already created contexts, can find no
+    device (a test file run on its own, profiles/r06_*). A no-op without a GPU."""
+    try:
+        import torch
+        if torch.cuda.is_available():
+            torch.cuda.init()
+    except Exception:
+        pass
+
+
 def load_case(name):
     d = os.path.join(GOLDEN, name)
     with open(os.path.join(d, "trace.json")) as fh:

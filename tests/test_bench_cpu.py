@@ -55,6 +55,22 @@ def test_one_gpu_runs_in_process_and_mismatch_fails():
     assert bad.returncode != 0 and "WORLD_SIZE" in bad.stderr
 
 
+@pytest.mark.parametrize("bad_rank", [0, 2])
+def test_dead_rank_stops_the_run(bad_rank):
+    """A rank that exits non-zero at start (VBFM_BENCH_FAULT=exit:R) while the others hang, as they
+    would in a collective waiting for it: the launcher stops the survivors (SIGTERM to each rank's
+    process group) and returns that rank's status within seconds, not at a deadline."""
+    import time
+    t0 = time.time()
+    out = _dry(["--gpus", "4"], {"VBFM_BENCH_FAULT": "exit:%d" % bad_rank})
+    dt = time.time() - t0
+    assert out.returncode == 3, out.stderr
+    assert dt < 30, dt
+    assert "rank %d of 4 exited with status 3" % bad_rank in out.stderr
+    codes = json.loads(out.stderr.split("rank exit codes ")[1].splitlines()[0])
+    assert codes[bad_rank] == 3 and sorted(codes)[:3] == [-15, -15, -15], codes
+
+
 def test_features_shard_holds_every_row():
     out = _dry(["--gpus", "2", "--shard", "features"])
     for l in out.stdout.splitlines():

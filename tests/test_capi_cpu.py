@@ -27,7 +27,7 @@ def test_library_loads_and_exports_every_declared_symbol():
     assert sorted(vbfm.EXPORTS) == declared
     for name in declared:
         assert hasattr(L, name), name
-    assert L.vbfm_abi_version() == vbfm.ABI_VERSION == 3
+    assert L.vbfm_abi_version() == vbfm.ABI_VERSION == 4
 
 
 def test_create_without_gpu_fails_loudly():

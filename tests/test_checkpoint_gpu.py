@@ -109,6 +109,32 @@ def test_load_refuses_other_model_or_data(tmp_path):
     h.close()
 
 
+def test_load_refuses_other_shape_table(tmp_path):
+    """a column's reduction tree follows its workgroup shape, so a checkpoint records the
+    shape table it ran with (StateHeader::shapes: revision << 32 | VBFM_SMALL_MAX) and a file of
+    another table -- another revision, another cutoff, or an older libvbfm that did not record it
+    -- is refused instead of resuming off by the sums' order."""
+    tr, te, nf = _data(n=5000)
+    g = _learner(tr, te, nf, 3, "auto")
+    g.init_caches()
+    g.iterate()
+    path = str(tmp_path / "vb.state")
+    g.save_state(path)
+    g.close()
+    raw = bytearray(open(path, "rb").read())
+    assert raw[88:96] == (3 << 32 | 128).to_bytes(8, "little")   # revision 3, cutoff 128
+    for word, origin in ((0, "before round 6"), (2 << 32 | 96, "revision 2"), (3 << 32 | 64, "VBFM_SMALL_MAX 64")):
+        raw[88:96] = word.to_bytes(8, "little")
+        other = str(tmp_path / ("other_%x.state" % word))
+        open(other, "wb").write(bytes(raw))
+        h = _learner(tr, te, nf, 3, "auto")
+        with pytest.raises(vbfm.VbfmError, match="another workgroup shape table") as ei:
+            h.load_state(other)
+        assert origin in str(ei.value)
+        assert h.load_state(path) == 1
+        h.close()
+
+
 def test_cli_save_state_and_resume(tmp_path):
     """bin/libFM -save_state after 3 iterations, then -resume for 3 more: the appended
     test_rmse / free_energy files and the #Iter lines continue the 6-iteration run's."""

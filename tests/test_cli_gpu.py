@@ -207,6 +207,8 @@ def test_cli_parity_log_17_digits(case, tmp_path):
         for gk, rk in pairs:
             assert abs(got[gk] - ref[rk]) <= 1e-9 * max(abs(ref[rk]), 1e-300), (it, gk, got[gk], ref[rk])
         assert got["ms_v"] > 0 and got["sweep_nnz_k_per_s"] > 0 and 0 < got["hbm_frac_per_gpu"] < 1
+        # one rank: no communicator, no exchange
+        assert got["exchange_calls"] == 0 and got["exchange_bytes"] == 0
 
 
 def test_cli_parity_log_online(tmp_path):
@@ -220,6 +222,8 @@ def test_cli_parity_log_online(tmp_path):
             ["-init_stdev", str(m["init_stdev"]), "-batch", str(m["batch"]), "-parity_log", "p.jsonl", "-vfile", "0"],
             method="vb_online")
     lines = [json.loads(x) for x in open(tmp_path / "p.jsonl")]
+    setup, lines = lines[0], lines[1:]            # the set-up line, as for the other methods
+    assert setup["method"] == "setup" and setup["learner"] == "vb_online"
     assert len(lines) == m["iter"]
     for it, (got, ref) in enumerate(zip(lines, t["trace"])):
         assert got["iter"] == it and got["method"] == "vb_online"
