@@ -43,8 +43,12 @@ CONFIGS = {
                desc="C4: 100M rows x 40 one-hot fields (5M features), nnz 4e9, k=100, -method vb"),
     "c3": dict(rows=10_000_000, fields=40, ids=25_000, k=50,
                desc="C3: 10M rows x 40 one-hot fields (1M features), nnz 4e8, k=50, -method vb"),
-    "c2": dict(rows=900_209, fields=2, ids=6_040, k=20,
-               desc="C2-shaped: 900k rows x 2 fields (users/items), k=20, -method vb"),
+    # BASELINE configs[1]: MovieLens-1M in libfm format (no network: the ML-1M shape, tests/synth.py
+    # generate_movielens -- 6,040 users, 3,952 items with popularity ~ u^3, 900,209 train / 100,000
+    # test rows, generated on the host and handed over through vbfm_set_train / vbfm_set_test)
+    "c2": dict(rows=900_209, test_rows=100_000, movielens=True, k=20,
+               desc="C2: MovieLens-1M-shaped 900,209 train / 100,000 test rows, 6,040 users + 3,952 items "
+                    "(item popularity ~u^3), k=20, -method vb"),
     "tiny": dict(rows=200_000, fields=10, ids=2_000, k=8, desc="smoke-sized synthetic"),
     # no field structure: rows of 5..60 distinct ids out of 1e6 (tests/synth.py generate_multihot);
     # the dependency levels miss rows, so the sweeps run on the column-gather layout
@@ -81,9 +85,14 @@ def write_cpu_sample(vbfm, cfg, rows, base, device):
     """Rows [0, rows) of the bench's train set (tests/synth.py, seed 1000, x = 1) generated on
     the device like the bench's own, copied back and written in the reference's binary format
     (<base>.x/.xt/.y, fmatrix.h:46-52), plus a 64-row test set: the reference loads it with its
-    own Data::load (Data.h:112-171)."""
+    own Data::load (Data.h:112-171). C2: the ML-1M-shaped rows themselves (host generator)."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import synth
+    if cfg.get("movielens"):
+        nf = synth.ML_USERS + synth.ML_ITEMS
+        synth.write_binary(base + "_train", nf, *synth.generate_movielens(rows, 1000))
+        synth.write_binary(base + "_test", nf, *synth.generate_movielens(64, 500000))
+        return
     F, S = cfg["fields"], cfg["ids"]
     g = vbfm.FMLearnVB(1, 1, 1, F * S + 1, min_target=1.0, max_target=5.0, device=device)
     g.synth(0, rows, F, S, seed=1000, xmode=0)
@@ -201,7 +210,7 @@ def cpu_baseline_start(vbfm, cfg, device, samples, core=None, world=1):
         if "error" in res:
             return {"value": None, "error": res["error"]}
         model, llc = host_cpu_info()
-        F, S = cfg["fields"], cfg["ids"]
+        F, S = (2, 0) if cfg.get("movielens") else (cfg["fields"], cfg["ids"])
         out = []
         for (rows, f), r in zip(samples, res["runs"]):
             o = {"rows": rows, "factors": f, "nnz": r["nnz"], "value": r["nnz_k_per_s"], "seconds": r["sweep_s"],
@@ -211,11 +220,12 @@ def cpu_baseline_start(vbfm, cfg, device, samples, core=None, world=1):
         big = out[-1]
         return {"value": big["value"], "unit": "nnz*k/s", "cores": 1, "kind": "reference",
                 "sample": "%d rows x %d fields x %d ids (D=%d), %d factor(s) of the sweep, x=1 (rows 0.. of the "
-                          "bench's data set); oracle/_ref/ref_driver = the reference's fm_learn_vb compiled from its "
+                          "bench's data set; S = 0: the ML-1M shape, users + items); oracle/_ref/ref_driver = the "
+                          "reference's fm_learn_vb compiled from its "
                           "sources, pinned to host core %s (1 of %d host cores: %s, last-level cache %s per core "
                           "complex; the sample's row caches alone are %.1f GB); run by rank 0 of %d during the timed "
                           "GPU steps, every rank's threads kept off that core" % (
-                              big["rows"], F, S, F * S, big["factors"], core, os.cpu_count(), model, llc,
+                              big["rows"], F, S, F * S or 6040 + 3952, big["factors"], core, os.cpu_count(), model, llc,
                               big["row_cache_bytes"] / 1e9, world),
                 "seconds": big["seconds"], "k0_seconds": big["k0_seconds"],
                 "extrapolated_iteration_s": big.get("extrapolated_iteration_s"),
@@ -398,7 +408,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-rows", type=int, default=20_000_000,
                     help="rows of the CPU baseline's sample (reported); a 2e6-row, 2-factor sample runs beside it")
-    ap.add_argument("--cpu-factors", type=int, default=1)
+    ap.add_argument("--cpu-factors", type=int, default=0,
+                    help="factors of the CPU sample's sweep (default 1; C2: all k, the whole sweep of ~2 s)")
     args = ap.parse_args()
 
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
@@ -430,13 +441,15 @@ def main():
         cfg["ids"] = args.ids
     k = cfg["k"]
     multihot = "features" in cfg
-    F, S = (0, 0) if multihot else (cfg["fields"], cfg["ids"])
-    NF = cfg["features"] if multihot else F * S       # train features
+    movielens = cfg.get("movielens", False)
+    F, S = (0, 0) if multihot else (2, 0) if movielens else (cfg["fields"], cfg["ids"])
+    NF = cfg["features"] if multihot else 6040 + 3952 if movielens else F * S       # train features
     D = NF + 1
     fshard = args.shard == "features"
     plan = shard_plan(cfg["rows"], world, rank, "features" if fshard else args.scaling)
     N, row0, n_total = plan["rows"], plan["row_offset"], plan["rows_total"]
-    tplan = shard_plan(max(cfg["rows"] // 100, 1000), world, rank, "features" if fshard else args.scaling)
+    tplan = shard_plan(cfg.get("test_rows", max(cfg["rows"] // 100, 1000)), world, rank,
+                       "features" if fshard else args.scaling)
     n_test, trow0 = tplan["rows"], tplan["row_offset"]
     if args.dry_run:
         out.write(json.dumps({"rank": rank, "local_rank": local_rank, "world_size": world,
@@ -450,13 +463,16 @@ def main():
     import torch.distributed as dist
     import vbfm
 
-    # the library's deadline for a collective (VBFM_COMM_TIMEOUT_S, include/vbfm.h) bounds the
-    # bench's own gloo barriers too
-    comm_timeout_s = float(os.environ.get("VBFM_COMM_TIMEOUT_S", "300"))
+    # the library's deadline for a collective (VBFM_COMM_TIMEOUT_S, include/vbfm.h; 300 s by default):
+    # the bench gives it 900 s, since rank 0 writes the CPU leg's sample files while the other ranks
+    # already wait in the first iteration's exchanges; the gloo barriers get at least as long. A
+    # rank that dies is caught sooner by the launcher (spawn_ranks) or torchrun
+    os.environ.setdefault("VBFM_COMM_TIMEOUT_S", "900")
+    comm_timeout_s = float(os.environ["VBFM_COMM_TIMEOUT_S"])
     if world > 1:
         import datetime
         dist.init_process_group("gloo", rank=rank, world_size=world,
-                                timeout=datetime.timedelta(seconds=max(comm_timeout_s, 30.0)))
+                                timeout=datetime.timedelta(seconds=max(comm_timeout_s, 1800.0)))
     ndev = torch.cuda.device_count()
     device = local_rank % max(1, ndev)      # one rank per GPU; a rehearsal with more ranks than GPUs shares them
     torch.cuda.set_device(device)
@@ -496,7 +512,12 @@ def main():
         fml.init_device(42)
     # one data set, one planted model (tests/synth.py): this rank's slice of the train and
     # test rows; feature shards hold every row
-    if multihot:
+    if movielens:
+        sys.path.insert(0, os.path.join(ROOT, "tests"))
+        import synth
+        fml.set_data(vbfm.DataSubset.from_csr(*synth.generate_movielens(N, 1000, row_offset=row0), NF),
+                     vbfm.DataSubset.from_csr(*synth.generate_movielens(n_test, 500000, row_offset=trow0), NF))
+    elif multihot:
         fml.synth_multihot(0, N, NF, cfg["lo"], cfg["hi"], seed=1000, xmode=0, row_offset=row0)
         fml.synth_multihot(1, n_test, NF, cfg["lo"], cfg["hi"], seed=500000, xmode=0, row_offset=trow0)
     elif args.host_upload:
@@ -547,7 +568,8 @@ def main():
         try:   # the samples written now (device generator); the reference runs during the timed steps
             rows = min(args.cpu_rows, n_total)   # rows [0, rows) of the whole data set, at any N
             samples = [(min(2_000_000, rows), min(2, k))] if rows > 2_000_000 else []
-            samples.append((rows, min(args.cpu_factors, k)))
+            cpu_factors = args.cpu_factors or (k if movielens else 1)
+            samples.append((rows, min(cpu_factors, k)))
             cpu_leg = cpu_baseline_start(vbfm, cfg, device, samples, core=core, world=world)
         except Exception as exc:
             cpu_leg = (lambda e=str(exc): {"value": None, "error": e})
@@ -731,6 +753,11 @@ def main():
              "ms_total"))},
         "cpu_baseline": None,
     }
+    if movielens:
+        # 900k rows x 64 B of records (58 MB) and 1.8e6 entries: the level store sits in the 256 MB
+        # MALL (Infinity Cache), so the fraction below is not an HBM measurement
+        result["roofline"]["note"] = ("C2's working set (records %.0f MB, entries %.0f MB) is cache-resident: the "
+                                      "fraction of 8 TB/s is not an HBM roofline" % (64e-6 * N, 8e-6 * nnz))
     if cpu_leg is not None:
         result["cpu_baseline"] = cpu_leg()
     if rank == 0:   # the line first: nothing in the teardown can cost it

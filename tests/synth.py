@@ -242,3 +242,28 @@ def generate_multihot(n_rows, n_features, lo, hi, seed, xmode=0, model_seed=MODE
     noise = _u(seed, 4, R) - 0.5
     y = np.clip(np.rint(((3.0 + cl * s) + gl * t) + 1.5 * noise), 1.0, 5.0).astype(np.float32)
     return row_ptr, feat, val, y
+
+
+ML_USERS, ML_ITEMS = 6040, 3952      # MovieLens-1M (BASELINE configs[1])
+
+
+def generate_movielens(n_rows, seed, row_offset=0, model_seed=MODEL_SEED):
+    """ML-1M-shaped rows (BASELINE configs[1]): a user uniform over 6,040 ids, an
+    item over 3,952 ids with popularity ~ u^3 (a few items own tens of thousands of rows), x = 1,
+    targets 1..5 from per-id biases of the planted model:
+
+      user(R) = h_row(1, R) % 6040;  item(R) = 6040 + min(floor(u_row(2, R)^3 * 3952), 3951)
+      y(R)    = clamp(rint(3 + 1.5 (b(user) + b(item)) + 1.5 (u_row(4, R) - 0.5)), 1, 5),
+      b(j)    = u_model(3, j) - 0.5
+    R = row_offset + r, as generate(): a rank's rows are a slice of the one-rank data set."""
+    U, I = ML_USERS, ML_ITEMS
+    idx = np.arange(row_offset, row_offset + n_rows, dtype=np.uint64)
+    user = (h(seed, 1, idx) % np.uint64(U)).astype(np.uint32)
+    u = _u(seed, 2, idx)
+    item = (U + np.minimum((u ** 3 * I).astype(np.int64), I - 1)).astype(np.uint32)
+    feat = np.stack([user, item], axis=1).reshape(-1)
+    val = np.ones(2 * n_rows, dtype=np.float32)
+    bu = _u(model_seed, 3, np.arange(U + I, dtype=np.uint64)) - 0.5
+    y = np.clip(np.rint(3.0 + 1.5 * (bu[user] + bu[item]) + 1.5 * (_u(seed, 4, idx) - 0.5)), 1, 5)
+    rp = np.arange(n_rows + 1, dtype=np.uint64) * np.uint64(2)
+    return rp, feat, val, y.astype(np.float32)

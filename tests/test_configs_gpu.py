@@ -49,19 +49,8 @@ def close(a, b, tol=REL):
 
 
 def c2_data(n, seed):
-    """ML-1M-shaped rows: user uniform over 6,040 ids, item over 3,952 ids with popularity
-    ~ u^3 (a few items own thousands of rows), targets from the planted model's shape."""
-    U, I = 6040, 3952
-    idx = np.arange(n, dtype=np.uint64)
-    user = (synth.h(seed, 1, idx) % np.uint64(U)).astype(np.uint32)
-    u = synth._u(seed, 2, idx)
-    item = (U + np.minimum((u ** 3 * I).astype(np.int64), I - 1)).astype(np.uint32)
-    feat = np.stack([user, item], axis=1).reshape(-1)
-    val = np.ones(2 * n, dtype=np.float32)
-    bu = synth._u(synth.MODEL_SEED, 3, np.arange(U + I, dtype=np.uint64)) - 0.5
-    y = np.clip(np.rint(3.0 + 1.5 * (bu[user] + bu[item]) + 1.5 * (synth._u(seed, 4, idx) - 0.5)), 1, 5)
-    rp = np.arange(n + 1, dtype=np.uint64) * np.uint64(2)
-    return rp, feat, val, y.astype(np.float32)
+    """ML-1M-shaped rows (tests/synth.py generate_movielens, the bench's C2)."""
+    return synth.generate_movielens(n, seed)
 
 
 def test_c2_movielens_shape_three_iterations_vs_oracle():
