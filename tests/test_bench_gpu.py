@@ -70,3 +70,25 @@ def test_eight_rank_bench_matches_one_rank():
         assert abs(a - b) <= 1e-8 * b, (eight["test_rmse_trace"], one["test_rmse_trace"])
     _close(eight["test_rmse"], one["test_rmse"])
     _close(eight["free_energy"], one["free_energy"])
+
+
+def test_bench_rank_fault_ends_the_run():
+    """The N-rank launch with a faulting rank (VBFM_FAULT=comm on rank 2 of 4: its first exchange
+    inside a sweep fails as a failed collective would): that rank exits non-zero and the launcher
+    stops the ranks waiting for it in the exchange, well before any deadline; the exchange fields
+    of a good run are in the line (host transport: every call timed)."""
+    import time
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env.update(VBFM_FAULT="comm", VBFM_FAULT_RANK="2")
+    t0 = time.time()
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--config", "tiny", "--steps", "2",
+                          "--warmup", "1", "--no-cpu-baseline", "--gpus", "4", "--transport", "host"],
+                         env=env, capture_output=True, text=True, timeout=300)
+    assert out.returncode != 0 and not [l for l in out.stdout.splitlines() if l.startswith("{")]
+    assert "rank 2/4: w sweep, level 0: VBFM_FAULT=comm" in out.stderr, out.stderr[-3000:]
+    # the first rank seen failing: rank 2, or a rank whose exchange failed when rank 2 left
+    assert " of 4 exited with status" in out.stderr, out.stderr[-3000:]
+    assert time.time() - t0 < 200
+    good = _bench("--gpus", "2", "--transport", "host")
+    ex = good["exchange"]
+    assert good["exchange_bytes"] > 0 and ex["calls_per_step"] > 0 and ex["timed"] > 0 and good["ms_exchange"] > 0
