@@ -193,6 +193,30 @@ static int pads_mode(uint32_t n, const uint32_t *perm_d, int nalloc)
 	return 0;
 }
 
+// mode "bigwin": one large hipMalloc of `gb` GB; the level pattern (destination side, from a plain
+// reference buffer) into windows of n records at every `step_mb` MB of it: does the rate vary inside
+// one allocation, and with what period?
+static int bigwin_mode(uint32_t n, const uint32_t *perm_d, int gb, int step_mb)
+{
+	const size_t bytes = (size_t)n * 64, total = (size_t)gb << 30, step = (size_t)step_mb << 20;
+	dv2 *ref, *big;
+	CK(hipMalloc(&ref, bytes));
+	CK(hipMemset(ref, 0, bytes));
+	CK(hipMalloc(&big, total));
+	CK(hipMemset(big, 0, total));
+	printf("one allocation of %d GB at %p; windows of %.2f GB every %d MB; w = ps per record (destination), "
+	       "c = streaming copy into it\n", gb, (void *)big, bytes / 1e9, step_mb);
+	for (size_t o = 0; o + bytes <= total; o += step) {
+		dv2 *w = (dv2 *)((char *)big + o);
+		Job jw = {ref, w, perm_d, n, nullptr, 0};
+		const float ws = timed(run_scatter, &jw, 2) / 4 * 1e9f / n;
+		const float c = timed(run_copy, &jw, 2) / 4 * 1e9f / n;
+		printf("offset %6zu MB  w %6.2f  c %6.2f\n", o >> 20, ws, c);
+		fflush(stdout);
+	}
+	return 0;
+}
+
 int main(int argc, char **argv)
 {
 	const uint32_t n = argc > 1 ? (uint32_t)atof(argv[1]) : 10000000u;
@@ -216,6 +240,8 @@ int main(int argc, char **argv)
 	CK(hipMemcpy(perm_d, perm.data(), (size_t)n * 4, hipMemcpyHostToDevice));
 	CK(hipMalloc(&out, 8));
 	if (argc > 2 && std::string(argv[2]) == "pads") return pads_mode(n, perm_d, argc > 3 ? atoi(argv[3]) : 4);
+	if (argc > 2 && std::string(argv[2]) == "bigwin")
+		return bigwin_mode(n, perm_d, argc > 3 ? atoi(argv[3]) : 64, argc > 4 ? atoi(argv[4]) : 1024);
 	CK(hipMalloc(&ref, bytes));
 	CK(hipMemset(ref, 0, bytes));
 	std::vector<dv2 *> bufs;
