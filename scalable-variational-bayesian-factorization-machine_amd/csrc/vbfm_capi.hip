@@ -340,6 +340,7 @@ void lord_release(vbfm_ctx *c, bool keep_rows)
 	dfree(c->lpidx); dfree(c->lpx); dfree(c->post_tab); dfree(c->lpay); dfree(c->lpay2);
 	dfree(c->long_segs); dfree(c->seg_part);
 	c->seg_ptr.clear();
+	c->long_min_l.clear();
 	c->place_ms.clear();
 	c->place_pick[0] = c->place_pick[1] = -1;
 	c->long_min = 0;
@@ -358,36 +359,50 @@ static int layout_request(const vbfm_ctx *c)
 	return c->layout_req;
 }
 
-// Long columns (skewed data): columns longer than SEG_MIN entries are cut into segments of
-// SEG_LEN, one workgroup each, in the fused single-rank sweep of either layout (lord_long /
-// col_long); columns listing a row twice stay sequential. VBFM_LONG=0: one workgroup per column.
+// Long columns (skewed data): a column longer than its level's threshold is cut into segments of
+// SEG_LEN = 1024 entries (one resident run of the 512-thread segment kernels), one workgroup each,
+// in the fused single-rank sweep of either layout (lord_long / col_long); columns listing a row
+// twice stay sequential. The threshold is max(1024, 4 x the level's mean column): the level's
+// workgroup shape is sized for its mean (dispatch_shape), and a column far beyond it streams its
+// run in many rounds while the rest of the launch has drained. ML-1M-shaped data (C2: items with
+// popularity ~u^3, mean 228, longest 56,803): 2.79 -> 1.97 ms per iteration against the round-5
+// rule (longer than 8192, in segments of 4096; profiles/r06_c2/seg_ab/). Uniform field data stays
+// unsegmented (C4's longest column ~950 entries of a mean of 800). VBFM_SEG_MIN / VBFM_SEG_LEN
+// override the threshold and the segment length, VBFM_LONG=0 turns segments off.
 // lcp: prefix sums of the level features' column lengths (level_feats order).
 static void build_long_segs(vbfm_ctx *c, const std::vector<uint64_t> &lcp, const std::vector<uint8_t> &dup,
                             const std::vector<uint32_t> &feats)
 {
-	constexpr uint32_t SEG_MIN = 8192, SEG_LEN = 4096;
+	const char *smn = getenv("VBFM_SEG_MIN"), *sln = getenv("VBFM_SEG_LEN");
+	const uint32_t SEG_LEN = sln ? (uint32_t)std::max(atoi(sln), 64) : 1024u;
 	const uint32_t L = nlevels(c);
 	const char *lg = getenv("VBFM_LONG");
 	const bool on = !(lg && lg[0] == '0');
 	std::vector<LongSeg> segs;
 	c->seg_ptr.assign((size_t)L + 1, 0);
+	c->long_min_l.assign(L, 0);
 	uint32_t maxs = 0;
 	for (uint32_t l = 0; l < L; l++) {
 		c->seg_ptr[l] = (uint32_t)segs.size();
+		const uint32_t nfl = c->level_ptr[l + 1] - c->level_ptr[l];
+		const uint64_t mean = nfl ? (lcp[c->level_ptr[l + 1]] - lcp[c->level_ptr[l]]) / nfl : 0;
+		const uint32_t thr = smn ? (uint32_t)std::max(atoi(smn), 64)
+		                         : (uint32_t)std::max<uint64_t>(1024u, std::min<uint64_t>(4 * mean, 1u << 30));
 		for (uint32_t i = c->level_ptr[l]; on && i < c->level_ptr[l + 1]; i++) {
 			const uint64_t len = lcp[i + 1] - lcp[i];
-			if (len <= SEG_MIN || dup[feats[i]]) continue;
+			if (len <= thr || dup[feats[i]]) continue;
 			// seg0: the column's first segment, counted from the level's first (blockIdx)
 			const uint32_t ns = (uint32_t)((len + SEG_LEN - 1) / SEG_LEN), s0 = (uint32_t)segs.size() - c->seg_ptr[l];
 			for (uint32_t q = 0; q < ns; q++)
 				segs.push_back({i - c->level_ptr[l], q * SEG_LEN,
 				                (uint32_t)std::min<uint64_t>(SEG_LEN, len - (uint64_t)q * SEG_LEN), s0, ns});
 		}
+		if ((uint32_t)segs.size() > c->seg_ptr[l]) c->long_min_l[l] = thr;   // (0: nothing skipped)
 		maxs = std::max(maxs, (uint32_t)segs.size() - c->seg_ptr[l]);
 	}
 	c->seg_ptr[L] = (uint32_t)segs.size();
 	if (segs.empty()) return;
-	c->long_min = SEG_MIN;
+	c->long_min = 1;   // some level has segments (each level's threshold: long_min_l)
 	c->long_segs = dalloc<LongSeg>(segs.size());
 	HIPCHK(hipMemcpyAsync(c->long_segs, segs.data(), segs.size() * sizeof(LongSeg), hipMemcpyHostToDevice, c->s));
 	c->seg_part = dalloc<double2>(2 * (size_t)maxs);
@@ -1248,7 +1263,7 @@ void sweep_level(vbfm_ctx *c, uint32_t l, bool is_w, int f)
 		}
 		if (!c->row_comm() && !c->force_split) {
 			if (c->long_min) {
-				a.long_min = c->long_min;
+				a.long_min = c->long_min_l[l];
 				a.segs = c->long_segs + c->seg_ptr[l];
 				a.nsegs = c->seg_ptr[l + 1] - c->seg_ptr[l];
 				a.seg_part = c->seg_part;
@@ -1297,7 +1312,7 @@ void sweep_level(vbfm_ctx *c, uint32_t l, bool is_w, int f)
 	}
 	if (!c->row_comm() && !c->force_split) {
 		if (c->long_min) {
-			a.long_min = c->long_min;
+			a.long_min = c->long_min_l[l];
 			a.segs = c->long_segs + c->seg_ptr[l];
 			a.nsegs = c->seg_ptr[l + 1] - c->seg_ptr[l];
 			a.seg_part = c->seg_part;
@@ -2155,11 +2170,25 @@ struct StateHeader {
 // the layout word of an online checkpoint says whether its batches ran on the per-batch level store
 // (written since round 5; before, an online learner always wrote COLUMN, whichever it used)
 constexpr uint64_t STATE_FLAG_OV_LAYOUT = 1;
-// a column's reduction tree follows its workgroup shape (dispatch_shape, vbfm_device.h), so a resume
-// continues bit for bit only under the same shape table: its revision (3: round 5's, with 128 x 3
-// and the small-shape cutoff at 128) and the cutoff in force (VBFM_SMALL_MAX)
-constexpr uint64_t SHAPE_TABLE_REVISION = 3;
-static uint64_t state_shapes() { return SHAPE_TABLE_REVISION << 32 | shape_small_max(); }
+// a column's reduction tree follows its workgroup shape (dispatch_shape, vbfm_device.h) and, for a
+// long column, its segments (build_long_segs), so a resume continues bit for bit only under the same
+// tables: their revision (4: round 6's -- the round-5 shapes with 128 x 3 and the small-shape cutoff
+// at 128, and segments of 1024 beyond max(1024, 4 x the level's mean)), an id of any segment
+// override in force (VBFM_LONG / VBFM_SEG_MIN / VBFM_SEG_LEN; 0: none) and the small-shape cutoff
+// (VBFM_SMALL_MAX): revision << 48 | segment id << 32 | cutoff
+constexpr uint64_t SHAPE_TABLE_REVISION = 4;
+static uint64_t seg_rule_id()
+{
+	const char *v[3] = {getenv("VBFM_LONG"), getenv("VBFM_SEG_MIN"), getenv("VBFM_SEG_LEN")};
+	if (!v[0] && !v[1] && !v[2]) return 0;
+	uint64_t h = 1469598103934665603ull;   // FNV-1a over the three settings
+	for (const char *p : v) {
+		for (const char *q = p ? p : "-"; *q; q++) h = (h ^ (uint8_t)*q) * 1099511628211ull;
+		h = (h ^ 0xffu) * 1099511628211ull;
+	}
+	return (h & 0xfffeu) | 1u;
+}
+static uint64_t state_shapes() { return SHAPE_TABLE_REVISION << 48 | seg_rule_id() << 32 | shape_small_max(); }
 static_assert(sizeof(StateHeader) == 104, "checkpoint header layout");
 constexpr char STATE_MAGIC[8] = {'V', 'B', 'F', 'M', 'S', 'T', '0', '1'};
 constexpr char MC_STATE_MAGIC[8] = {'V', 'B', 'F', 'M', 'M', 'C', '0', '1'};   // MCMC / ALS payload
@@ -2317,13 +2346,15 @@ int vbfm_load_state(vbfm_ctx *c, const char *path, uint32_t *iter)
 			                  "whether the batches ran on the per-batch level store (the order of the batches' data-set "
 			                  "sums): resume it with the libvbfm that wrote it");
 		if (h.shapes != state_shapes()) {
-			char b[320];
-			snprintf(b, sizeof(b), "checkpoint written under another workgroup shape table (%s; this library: revision "
-			         "%llu, VBFM_SMALL_MAX %u): the column sums would change order and the run would not continue bit "
-			         "for bit; resume with the libvbfm and VBFM_SMALL_MAX that wrote it",
-			         h.shapes ? ("revision " + std::to_string(h.shapes >> 32) + ", VBFM_SMALL_MAX " +
-			                     std::to_string(h.shapes & 0xffffffffu)).c_str() : "a libvbfm before round 6, unrecorded",
-			         (unsigned long long)SHAPE_TABLE_REVISION, shape_small_max());
+			char b[512];
+			auto desc = [](uint64_t w) {
+				return "revision " + std::to_string(w >> 48) + ", segment override " +
+				       std::to_string((w >> 32) & 0xffffu) + ", VBFM_SMALL_MAX " + std::to_string(w & 0xffffffffu);
+			};
+			snprintf(b, sizeof(b), "checkpoint written under another workgroup shape table (%s; this library: %s): the "
+			         "column sums would change order and the run would not continue bit for bit; resume with the "
+			         "libvbfm and settings that wrote it",
+			         h.shapes ? desc(h.shapes).c_str() : "a libvbfm before round 6, unrecorded", desc(state_shapes()).c_str());
 			throw std::string(b);
 		}
 		if (h.layout != state_layout(c))

@@ -227,7 +227,8 @@ struct vbfm_ctx {
 	                               // 16-B load (lx / lnext / lpidx / lpx are freed once packed)
 	PostT *post_tab = nullptr;     // [max level width] posteriors of the last level swept
 	// long columns of the level store (fused single-rank sweep): segments of every level
-	uint32_t long_min = 0;         // columns longer than this are split (0: none)
+	uint32_t long_min = 0;         // nonzero: some level has long columns split into segments
+	std::vector<uint32_t> long_min_l;  // [L] each level's threshold (0: no segments in the level)
 	std::vector<uint32_t> seg_ptr; // [L+1] each level's segments in long_segs
 	LongSeg *long_segs = nullptr;
 	double2 *seg_part = nullptr;   // [2 * max segments of a level]

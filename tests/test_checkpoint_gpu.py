@@ -110,10 +110,11 @@ def test_load_refuses_other_model_or_data(tmp_path):
 
 
 def test_load_refuses_other_shape_table(tmp_path):
-    """a column's reduction tree follows its workgroup shape, so a checkpoint records the
-    shape table it ran with (StateHeader::shapes: revision << 32 | VBFM_SMALL_MAX) and a file of
-    another table -- another revision, another cutoff, or an older libvbfm that did not record it
-    -- is refused instead of resuming off by the sums' order."""
+    """a column's reduction tree follows its workgroup shape and long-column segments, so
+    a checkpoint records the tables it ran with (StateHeader::shapes: revision << 48 | segment override
+    id << 32 | VBFM_SMALL_MAX) and a file of other tables -- another revision, another cutoff, a
+    segment override, or an older libvbfm that did not record it -- is refused instead of resuming
+    off by the sums' order."""
     tr, te, nf = _data(n=5000)
     g = _learner(tr, te, nf, 3, "auto")
     g.init_caches()
@@ -122,8 +123,9 @@ def test_load_refuses_other_shape_table(tmp_path):
     g.save_state(path)
     g.close()
     raw = bytearray(open(path, "rb").read())
-    assert raw[88:96] == (3 << 32 | 128).to_bytes(8, "little")   # revision 3, cutoff 128
-    for word, origin in ((0, "before round 6"), (2 << 32 | 96, "revision 2"), (3 << 32 | 64, "VBFM_SMALL_MAX 64")):
+    assert raw[88:96] == (4 << 48 | 128).to_bytes(8, "little")   # revision 4, no segment override, cutoff 128
+    for word, origin in ((0, "before round 6"), (3 << 48 | 128, "revision 3"), (4 << 48 | 64, "VBFM_SMALL_MAX 64"),
+                         (4 << 48 | 0x1235 << 32 | 128, "segment override 4661")):
         raw[88:96] = word.to_bytes(8, "little")
         other = str(tmp_path / ("other_%x.state" % word))
         open(other, "wb").write(bytes(raw))

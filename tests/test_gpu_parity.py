@@ -358,8 +358,8 @@ def test_unit_x_store_bit_identical(method, split, monkeypatch):
 @pytest.mark.parametrize("k1", [1, 0])
 def test_long_columns_split_into_segments(k1, monkeypatch):
     """Skewed two-field data (a Zipf item field: the top items hold 10k-20k rows): columns
-    longer than 8192 entries are swept by segment workgroups (statistics partials, then the
-    posterior + move / correction) on both layouts. Against the oracle (1e-9) and against one
+    longer than max(1024, 4 x the level's mean) entries are swept by segment workgroups of 1024
+    entries (statistics partials, then the posterior + move / correction) on both layouts. Against the oracle (1e-9) and against one
     workgroup per column (VBFM_LONG=0) on either layout (summation order only, 1e-12)."""
     n, U, I, k = 60000, 5000, 400, 4
     rng = np.random.default_rng(11)
