@@ -220,12 +220,14 @@ def cpu_baseline_start(vbfm, cfg, device, samples, core=None, world=1):
         big = out[-1]
         return {"value": big["value"], "unit": "nnz*k/s", "cores": 1, "kind": "reference",
                 "sample": "%d rows x %d fields x %d ids (D=%d), %d factor(s) of the sweep, x=1 (rows 0.. of the "
-                          "bench's data set; S = 0: the ML-1M shape, users + items); oracle/_ref/ref_driver = the "
+                          "bench's data set%s); oracle/_ref/ref_driver = the "
                           "reference's fm_learn_vb compiled from its "
                           "sources, pinned to host core %s (1 of %d host cores: %s, last-level cache %s per core "
                           "complex; the sample's row caches alone are %.1f GB); run by rank 0 of %d during the timed "
                           "GPU steps, every rank's threads kept off that core" % (
-                              big["rows"], F, S, F * S or 6040 + 3952, big["factors"], core, os.cpu_count(), model, llc,
+                              big["rows"], F, S, F * S or 6040 + 3952, big["factors"],
+                              "; S = 0: the ML-1M shape, users + items" if cfg.get("movielens") else "",
+                              core, os.cpu_count(), model, llc,
                               big["row_cache_bytes"] / 1e9, world),
                 "seconds": big["seconds"], "k0_seconds": big["k0_seconds"],
                 "extrapolated_iteration_s": big.get("extrapolated_iteration_s"),
