@@ -242,10 +242,15 @@ def cpu_baseline_port(cfg, sample_rows, sample_factors, seed=1):
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import synth
     import oracle_ctypes as oc
-    F, S = cfg["fields"], cfg["ids"]
-    rp, f, v, y = synth.generate(sample_rows, F, S, seed, 0)
+    if cfg.get("movielens"):
+        F, S, D = 2, 0, synth.ML_USERS + synth.ML_ITEMS + 1
+        rp, f, v, y = synth.generate_movielens(sample_rows, seed)
+    else:
+        F, S = cfg["fields"], cfg["ids"]
+        D = F * S + 1
+        rp, f, v, y = synth.generate(sample_rows, F, S, seed, 0)
     tr = oc.Data(csr=(sample_rows, rp, f, v, y))
-    vb = oc.VB(1, 1, sample_factors, F * S + 1)
+    vb = oc.VB(1, 1, sample_factors, D)
     vb.init_params(1, 0.1)
     vb.attach(tr, tr)
     vb.init_caches()
