@@ -54,6 +54,24 @@ __global__ __launch_bounds__(BLOCK) void klds(const dv2 *__restrict__ src, dv2 *
 	}
 }
 
+// the mirror pattern: run b of RUN consecutive destination records is gathered from random source
+// positions (the same permutation, read as "where does my record come from"), staged through LDS,
+// and written out contiguously
+__global__ __launch_bounds__(BLOCK) void kgather(const dv2 *__restrict__ src, dv2 *__restrict__ dst,
+                                                 const uint32_t *__restrict__ from, uint32_t n)
+{
+	__shared__ dv2 recs[512 * 4];
+	const uint32_t b = blockIdx.x * RUN;
+	const uint32_t m = min(RUN, n - b);
+	for (uint32_t t = threadIdx.x; t < m * 4; t += BLOCK) {
+		const uint32_t i = t >> 2, c = t & 3;
+		recs[lslot(i, c)] = src[(size_t)from[b + i] * 4 + c];
+	}
+	__syncthreads();
+	for (uint32_t t = threadIdx.x; t < m * 4; t += BLOCK)
+		dst[(size_t)b * 4 + t] = recs[lslot(t >> 2, t & 3)];
+}
+
 __global__ void kcopy(const dv2 *__restrict__ src, dv2 *__restrict__ dst, size_t n)
 {
 	for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
@@ -112,6 +130,13 @@ static void run_scatter(void *p)
 	Job *j = (Job *)p;
 	const uint32_t nrun = (j->n + RUN - 1) / RUN;
 	for (int it = 0; it < 4; ++it) klds<<<nrun, BLOCK>>>(j->a, j->b, j->perm, j->n);
+}
+
+static void run_gather(void *p)
+{
+	Job *j = (Job *)p;
+	const uint32_t nrun = (j->n + RUN - 1) / RUN;
+	for (int it = 0; it < 4; ++it) kgather<<<nrun, BLOCK>>>(j->a, j->b, j->perm, j->n);
 }
 
 static void run_copy(void *p)
@@ -291,7 +316,8 @@ int main(int argc, char **argv)
 	CK(hipDeviceSynchronize());
 	printf("records %u (%.2f GB per buffer); ps per record for w / r / c, ns per touch for t4k / t64k / t2m\n", n,
 	       bytes / 1e9);
-	printf("%-3s %-8s %8s %8s %8s %8s %8s %8s\n", "#", "kind", "w", "r", "c", "t4k", "t64k", "t2m");
+	printf("%-3s %-8s %8s %8s %8s %8s %8s %8s %8s %8s\n", "#", "kind", "w", "r", "c", "t4k", "t64k", "t2m", "gsrc",
+	       "gdst");
 	for (int pass = 0; pass < 2; ++pass)
 		for (size_t i = 0; i < bufs.size(); ++i) {
 			Job jw = {ref, bufs[i], perm_d, n, out, 0}, jr = {bufs[i], ref, perm_d, n, out, 0};
@@ -304,7 +330,13 @@ int main(int argc, char **argv)
 				Job jt = {bufs[i], nullptr, nullptr, n, out, sh[q]};
 				t[q] = timed(run_touch, &jt, 3) * 1e6f / (1u << 22);
 			}
-			printf("%-3zu %-8s %8.2f %8.2f %8.2f %8.3f %8.3f %8.3f\n", i, kind[i], w, r, c, t[0], t[1], t[2]);
+			// gather: the candidate as the randomly read source (gsrc), or as the contiguously written
+			// destination of a gather from the reference (gdst)
+			Job jg = {bufs[i], ref, perm_d, n, out, 0}, jg2 = {ref, bufs[i], perm_d, n, out, 0};
+			const float gs = timed(run_gather, &jg, 2) / 4 * 1e9f / n;
+			const float gd = timed(run_gather, &jg2, 2) / 4 * 1e9f / n;
+			printf("%-3zu %-8s %8.2f %8.2f %8.2f %8.3f %8.3f %8.3f %8.2f %8.2f\n", i, kind[i], w, r, c, t[0], t[1], t[2],
+			       gs, gd);
 			fflush(stdout);
 		}
 	// streaming-write rate of each 256 MB window of every buffer (ps per 64 B): is a buffer slow as a
