@@ -2573,6 +2573,7 @@ int vbfm_comm_init(vbfm_ctx *c, int32_t nranks, int32_t rank, const uint8_t uid[
 	if (!c) return fail(nullptr, "null context");
 	return guarded(c, [&] {
 		if (c->rows) throw std::string("vbfm_comm_init must precede vbfm_set_train");
+		if (c->multi()) throw c->comm_failed ? c->comm_err : std::string("the context already has a communicator");
 		if (nranks < 1 || rank < 0 || rank >= nranks) throw std::string("bad rank / nranks");
 		// one rank needs no communicator; VBFM_FORCE_COMM=1 creates it anyway so that every
 		// RCCL call of the sharded path runs (the 1-GPU test box cannot host two ranks)
