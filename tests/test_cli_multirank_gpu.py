@@ -165,6 +165,11 @@ def test_checkpoint_per_rank_resume_mcmc(method, synth_files, tmp_path):
     got = its(cwd / "p1.jsonl") + its(cwd / "p2.jsonl")
     keys = ("iter", "train", "test_rmse", "test_mae", "test_rmse_this", "alpha", "w0")
     assert [[g[k] for k in keys] for g in got] == [[w[k] for k in keys] for w in want]
+    # every iteration's exchange (vbfm_exchange_info): the same calls and bytes each iteration, timed
+    # in full over the host transport
+    assert len({(w["exchange_calls"], w["exchange_bytes"]) for w in want}) == 1
+    assert all(w["exchange_calls"] > 0 and w["exchange_bytes"] > 0 and w["exchange_timed"] == w["exchange_calls"]
+               and w["ms_exchange"] > 0 for w in want)
 
 
 def test_feature_shards_run(synth_files, tmp_path):

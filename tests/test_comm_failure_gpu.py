@@ -188,3 +188,17 @@ def test_exchange_info_counts_every_level(monkeypatch):
     assert x["bytes"] >= (K + 1) * 16 * nf
     assert x["n_timed"] == x["n_calls"] and x["ms_timed"] > 0 and x["ms_estimated"] == pytest.approx(x["ms_timed"])
     fml.close()
+
+
+def test_second_communicator_refused(monkeypatch):
+    """A context takes one communicator: a second vbfm_comm_init (or one after a host exchange) is
+    refused instead of leaking the first."""
+    sys.path.insert(0, PKG)
+    import vbfm
+    monkeypatch.setenv("VBFM_FORCE_COMM", "1")
+    fml = vbfm.FMLearnVB(1, 1, 2, 101, min_target=1.0, max_target=5.0, device=0)
+    fml.comm_init(1, 0, vbfm.FMLearnVB.comm_unique_id())
+    with pytest.raises(vbfm.VbfmError, match="already has a communicator"):
+        fml.comm_init(1, 0, vbfm.FMLearnVB.comm_unique_id())
+    assert fml.comm_info() == (1, 0, "rccl")
+    fml.close()
