@@ -1657,6 +1657,16 @@ void vbfm_destroy(vbfm_ctx *c)
 {
 	if (!c) return;
 	(void)hipSetDevice(c->dev);
+	if (c->comm_failed && c->s) {
+		// an aborted communicator: RCCL's kernels leave on the abort, but a stream still busy after
+		// 10 s is left to the process's exit (freeing under it would block in a device synchronise)
+		const double end = wall_s() + 10.0;
+		while (hipStreamQuery(c->s) == hipErrorNotReady && wall_s() < end) usleep(1000);
+		if (hipStreamQuery(c->s) == hipErrorNotReady) {
+			delete c;
+			return;
+		}
+	}
 	if (c->s) (void)hipStreamSynchronize(c->s);
 	free_data(c->tr);
 	free_data(c->te);
