@@ -360,6 +360,20 @@ def bench_fault_hook(rank):
     time.sleep(600)
 
 
+def host_allreduce(arr, op):
+    """The host transport's exchange (vbfm_comm_init_host): reduce the staged buffer in place over
+    the ranks with a gloo all_reduce -- fp64 sums, uint32 level maxima (through fp64: exact below
+    2^53), uint8 flags (through int32)."""
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+    t = torch.from_numpy(arr.astype(np.float64) if arr.dtype == np.uint32 else arr.copy())
+    if arr.dtype == np.uint8:
+        t = t.to(torch.int32)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX if op == "max" else dist.ReduceOp.SUM)
+    arr[:] = t.numpy().astype(arr.dtype)
+
+
 def loaded_libs(name):
     """Distinct files named like `name` mapped into this process (one RCCL, not two)."""
     paths = set()
@@ -504,12 +518,6 @@ def main():
     if args.one_rank_comm:
         fml.comm_init(1, 0, vbfm.FMLearnVB.comm_unique_id())
     if world > 1 and args.transport == "host":
-        def host_allreduce(arr, op):
-            t = torch.from_numpy(arr.astype(np.float64) if arr.dtype == np.uint32 else arr.copy())
-            if arr.dtype == np.uint8:
-                t = t.to(torch.int32)
-            dist.all_reduce(t, op=dist.ReduceOp.MAX if op == "max" else dist.ReduceOp.SUM)
-            arr[:] = t.numpy().astype(arr.dtype)
         fml.comm_init_host(world, rank, host_allreduce)
     elif world > 1:
         obj = [vbfm.FMLearnVB.comm_unique_id() if rank == 0 else None]

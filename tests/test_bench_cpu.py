@@ -211,3 +211,44 @@ def test_cpu_leg_core_and_pinning():
                 os.sched_setaffinity(int(tid), before)
             except OSError:
                 pass
+
+
+def _exchange_worker(rank, world, port, q):
+    import numpy as np
+    import torch.distributed as dist
+    sys.path.insert(0, ROOT)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import bench
+    f = np.array([0.1 * (rank + 1), -2.5, 1e300 / (rank + 1)], dtype=np.float64)
+    u = np.array([rank, 7, 4294967295 - rank], dtype=np.uint32)
+    b = np.array([rank % 2, 0, 1], dtype=np.uint8)
+    bench.host_allreduce(f, "sum")
+    bench.host_allreduce(u, "max")
+    bench.host_allreduce(b, "max")
+    q.put((rank, f.tolist(), u.tolist(), b.tolist()))
+    dist.destroy_process_group()
+
+
+def test_host_exchange_reduces_every_dtype_over_gloo():
+    """bench.py's host transport (the exchange behind vbfm_comm_init_host on an N-rank run sharing
+    GPUs) over gloo with 3 CPU ranks: fp64 sums, uint32 maxima up to 2^32 - 1, uint8 flags, in place
+    and in the caller's dtype."""
+    import socket
+    import torch.multiprocessing as mp
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_exchange_worker, args=(r, 3, port, q)) for r in range(3)]
+    for p in procs:
+        p.start()
+    got = sorted(q.get(timeout=120) for _ in range(3))
+    for p in procs:
+        p.join(timeout=30)
+    want_f = [0.1 + 0.2 + 0.30000000000000004, -7.5, 1e300 + 1e300 / 2 + 1e300 / 3]
+    for rank, f, u, b in got:
+        assert abs(f[0] - 0.6) < 1e-15 and f[1] == -7.5 and abs(f[2] - want_f[2]) <= 1e-15 * want_f[2]
+        assert u == [2, 7, 4294967295]
+        assert b == [1, 0, 1]
