@@ -91,7 +91,9 @@ typedef struct {
 	int32_t place_candidates;
 	uint64_t place_budget_bytes;
 } vbfm_config;
-#define VBFM_PLACE_BUDGET_DEFAULT ((uint64_t)48 << 30)   /* 48 GiB: 8 candidates at C4 (6.4 GB buffers) */
+/* 96 GiB: 16 candidates at C4 (6.4 GB buffers). Fast regions can first appear past the first
+ * ~50 GB of allocations (profiles/r06_placement/README.md, calls 1 and wide_search) */
+#define VBFM_PLACE_BUDGET_DEFAULT ((uint64_t)96 << 30)
 
 /* Variational and hyper parameters (fm_learn_vb.h:36-46). Arrays are caller-allocated. */
 typedef struct {
