@@ -1,10 +1,9 @@
 #!/bin/bash
-# C3 (BASELINE configs[2], "rocprof HBM GB/s vs roofline"): kernel trace and one PMC pass of the
-# default C3 bench on the final tree, plus the bench line itself
+# C3 (BASELINE configs[2], "rocprof HBM GB/s vs roofline"): the bench line and a kernel trace of the
+# default C3 bench on the final tree (the PMC passes: r06_c3_pmc.sh, one counter per pass)
 cd "$GRAFT_REPO_ROOT" || exit 1
 export TMPDIR=/tmp
 out=gpurun_out/${1:-r06_c3_trace}
 mkdir -p $out
 timeout -k 10 400 python3 -u bench.py --config c3 --steps 3 --warmup 1 > $out/bench.json 2> $out/bench.log && \
-timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $out/kt -o kt -- python3 -u bench.py --config c3 --steps 2 --warmup 1 > $out/bench_kt.json 2> $out/bench_kt.log && \
-timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE WRITE_SIZE --output-format csv -d $out/pmc -o pmc -- python3 -u bench.py --config c3 --steps 1 --warmup 0 --no-launch-events > $out/bench_pmc.json 2> $out/bench_pmc.log
+timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $out/kt -o kt -- python3 -u bench.py --config c3 --steps 2 --warmup 1 > $out/bench_kt.json 2> $out/bench_kt.log
